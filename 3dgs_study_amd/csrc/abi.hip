@@ -1,0 +1,192 @@
+// abi.hip — the C ABI (include/gsr.h): argument checks, orchestration of the
+// kernel launches on the caller's stream, error reporting.
+//
+// Mirrors upstream rasterize_points.cu (RasterizeGaussiansCUDA,
+// RasterizeGaussiansBackwardCUDA, markVisible) and Rasterizer::forward /
+// Rasterizer::backward (rasterizer_impl.cu).  No device allocation happens
+// here: every buffer belongs to the caller (torch's caching allocator on the
+// Python side).  The only host synchronisation is the num_rendered read-back
+// in gsr_forward_preprocess, as upstream.
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "gsr_kernels.hpp"
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_err;
+thread_local uint32_t *g_pinned = nullptr;  // 16 control words read back per forward
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int check_hip(hipError_t e, const char *what) {
+    if (e != hipSuccess) return fail(GSR_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    return GSR_OK;
+}
+
+// upstream debug mode: synchronise and check after every kernel
+int step(hipError_t e, const char *what, bool debug, hipStream_t s) {
+    int rc = check_hip(e, what);
+    if (rc || !debug) return rc;
+    return check_hip(hipStreamSynchronize(s), what);
+}
+
+int validate(const gsr_inputs *in, bool forward) {
+    if (!in) return fail(GSR_ERR_ARGS, "inputs is NULL");
+    if (in->P < 0) return fail(GSR_ERR_ARGS, "means3D must have dimensions (num_points, 3)");
+    if (in->W <= 0 || in->H <= 0) return fail(GSR_ERR_ARGS, "image size must be positive (got %dx%d)", in->W, in->H);
+    if ((int64_t)in->W * in->H > (int64_t)1 << 30) return fail(GSR_ERR_CAPACITY, "image too large");
+    if (in->P == 0) return GSR_OK;
+    if (!in->means3D || !in->viewmatrix || !in->projmatrix || !in->bg || (forward && !in->opacities))
+        return fail(GSR_ERR_ARGS, "missing required input (means3D/opacities/viewmatrix/projmatrix/bg)");
+    if ((in->sh == nullptr) == (in->colors_precomp == nullptr))
+        return fail(GSR_ERR_ARGS, "Please provide excatly one of either SHs or precomputed colors!");
+    const bool have_sr = in->scales && in->rotations;
+    if (have_sr == (in->cov3D_precomp != nullptr))
+        return fail(GSR_ERR_ARGS,
+                    "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (in->sh) {
+        if (!in->campos) return fail(GSR_ERR_ARGS, "campos required with SH colours");
+        if (in->D < 0 || in->D > 3) return fail(GSR_ERR_ARGS, "sh_degree must be in [0, 3] (got %d)", in->D);
+        if (in->M < (in->D + 1) * (in->D + 1))
+            return fail(GSR_ERR_ARGS, "sh has %d coefficients per channel, degree %d needs %d", in->M, in->D,
+                        (in->D + 1) * (in->D + 1));
+    }
+    return GSR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gsr_geom_bytes(int32_t P, int32_t W, int32_t H) { return geom_layout(P, W, H).bytes; }
+size_t gsr_binning_bytes(int64_t num_rendered, int32_t W, int32_t H) {
+    return binning_layout(num_rendered, W, H).bytes;
+}
+size_t gsr_img_bytes(int32_t W, int32_t H) { return img_layout(W, H).bytes; }
+size_t gsr_accum_bytes(int32_t P) { return (size_t)(P > 0 ? P : 1) * ACCUM_STRIDE * sizeof(float); }
+
+int gsr_geom_layout(int32_t P, int32_t W, int32_t H, size_t *offsets, int cap) {
+    const GeomLayout L = geom_layout(P, W, H);
+    int n = 0;
+    for (; n < cap && n < GSR_GEOM_NFIELDS; n++) offsets[n] = L.off[n];
+    return n;
+}
+int gsr_binning_layout(int64_t num_rendered, int32_t W, int32_t H, size_t *offsets, int cap) {
+    const BinningLayout L = binning_layout(num_rendered, W, H);
+    int n = 0;
+    for (; n < cap && n < GSR_BIN_NFIELDS; n++) offsets[n] = L.off[n];
+    return n;
+}
+int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap) {
+    const ImgLayout L = img_layout(W, H);
+    int n = 0;
+    for (; n < cap && n < GSR_IMG_NFIELDS; n++) offsets[n] = L.off[n];
+    return n;
+}
+
+const char *gsr_last_error(void) { return g_err.c_str(); }
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+
+int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered,
+                           uint32_t *max_tile_len, void *stream) {
+    if (int rc = validate(in, true)) return rc;
+    if (!num_rendered) return fail(GSR_ERR_ARGS, "num_rendered is NULL");
+    *num_rendered = 0;
+    if (max_tile_len) *max_tile_len = 0;
+    if (in->P == 0) return GSR_OK;
+    if (!geom || !radii) return fail(GSR_ERR_ARGS, "geom/radii buffers are NULL");
+    hipStream_t s = (hipStream_t)stream;
+    const bool dbg = in->debug != 0;
+    if (int rc = step(launch_preprocess(*in, geom, radii, s), "preprocess", dbg, s)) return rc;
+    if (int rc = step(launch_scan(in->P, geom, in->W, in->H, s), "inclusive scan", dbg, s)) return rc;
+    if (int rc = step(launch_bin_count(in->P, in->W, in->H, geom, radii, s), "tile count", dbg, s)) return rc;
+    if (!g_pinned) {
+        if (int rc = check_hip(hipHostMalloc((void **)&g_pinned, CTRL_WORDS * 4, hipHostMallocDefault), "hipHostMalloc"))
+            return rc;
+    }
+    const GeomLayout L = geom_layout(in->P, in->W, in->H);
+    if (int rc = check_hip(hipMemcpyAsync(g_pinned, at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), CTRL_WORDS * 4,
+                                          hipMemcpyDeviceToHost, s),
+                           "num_rendered read-back"))
+        return rc;
+    if (int rc = check_hip(hipStreamSynchronize(s), "num_rendered read-back")) return rc;
+    if (g_pinned[CTRL_PREFILTER_ERR])
+        return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    const int64_t I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
+    if (I > 0xFFFFFFFFll) return fail(GSR_ERR_CAPACITY, "num_rendered %lld exceeds 32-bit list indexing", (long long)I);
+    if ((uint32_t)I != g_pinned[CTRL_TILE_TOTAL_LO])
+        return fail(GSR_ERR_HIP, "internal: scan total %u != tile bucket total %u", (uint32_t)I,
+                    g_pinned[CTRL_TILE_TOTAL_LO]);
+    *num_rendered = I;
+    if (max_tile_len) *max_tile_len = g_pinned[CTRL_MAX_TILE];
+    return GSR_OK;
+}
+
+int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
+                       uint32_t max_tile_len, const int32_t *radii, float *out_color, void *stream) {
+    if (int rc = validate(in, true)) return rc;
+    if (!out_color) return fail(GSR_ERR_ARGS, "out_color is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    const bool dbg = in->debug != 0;
+    if (in->P == 0)  // upstream returns the zero-initialised image untouched
+        return check_hip(hipMemsetAsync(out_color, 0, (size_t)3 * in->W * in->H * sizeof(float), s), "memset");
+    if (!geom || !img || (num_rendered > 0 && !binning)) return fail(GSR_ERR_ARGS, "scratch buffers are NULL");
+    if (num_rendered > 0) {
+        if (int rc = step(launch_bin_scatter(in->P, in->W, in->H, geom, radii, binning, num_rendered, s),
+                          "duplicateWithKeys (tile scatter)", dbg, s))
+            return rc;
+        if (int rc = step(launch_tile_sort(in->P, in->W, in->H, geom, binning, num_rendered, max_tile_len, s),
+                          "per-tile sort", dbg, s))
+            return rc;
+    }
+    return step(launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s), "render", dbg, s);
+}
+
+int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning, const void *img,
+                 int64_t num_rendered, const float *dL_dout_color, void *accum, float *dmeans2D, float *dcolors,
+                 float *dopacity, float *dmeans3D, float *dcov3D, float *dsh, float *dscales, float *drot,
+                 void *stream) {
+    if (int rc = validate(in, false)) return rc;
+    if (in->P == 0) return GSR_OK;
+    if (!radii || !geom || !img || !accum || !dL_dout_color || (num_rendered > 0 && !binning))
+        return fail(GSR_ERR_ARGS, "backward scratch/inputs are NULL");
+    if (!dmeans2D || !dcolors || !dopacity || !dmeans3D || !dcov3D)
+        return fail(GSR_ERR_ARGS, "backward outputs are NULL");
+    if (in->sh && in->M > 0 && !dsh) return fail(GSR_ERR_ARGS, "dsh is NULL");
+    if (in->scales && (!dscales || !drot)) return fail(GSR_ERR_ARGS, "dscales/drot are NULL");
+    hipStream_t s = (hipStream_t)stream;
+    const bool dbg = in->debug != 0;
+    float *acc = (float *)accum;
+    if (int rc = check_hip(hipMemsetAsync(acc, 0, gsr_accum_bytes(in->P), s), "accumulator memset")) return rc;
+    if (num_rendered > 0) {
+        if (int rc = step(launch_render_bwd(*in, geom, binning, num_rendered, img, dL_dout_color, acc, s),
+                          "render backward", dbg, s))
+            return rc;
+    }
+    BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot};
+    return step(launch_preprocess_bwd(*in, radii, geom, acc, o, s), "preprocess backward", dbg, s);
+}
+
+int gsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *present, void *stream) {
+    (void)projmatrix;
+    if (P < 0) return fail(GSR_ERR_ARGS, "means3D must have dimensions (num_points, 3)");
+    if (P == 0) return GSR_OK;
+    if (!means3D || !viewmatrix || !present) return fail(GSR_ERR_ARGS, "mark_visible: NULL input");
+    hipStream_t s = (hipStream_t)stream;
+    return check_hip(launch_mark_visible(P, means3D, viewmatrix, present, s), "mark_visible");
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+// gsr_common.hpp — shared constants, scratch layouts and device helpers of the
+// gfx950 Gaussian rasterizer.  Helpers that decide integer outputs (projection,
+// ndc2Pix, getRect, covariance) follow the exact operation order of the CPU
+// oracle (oracle/gsr_oracle.c), which restates upstream cuda_rasterizer/
+// auxiliary.h + forward.cu.  Translation units that
+// produce those integers compile with `#pragma clang fp contract(off)`.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gsr.h"
+
+namespace gsr {
+
+constexpr int TILE_X = 16;  // BLOCK_X (upstream config.h)
+constexpr int TILE_Y = 16;  // BLOCK_Y
+constexpr int TILE_PIX = TILE_X * TILE_Y;
+constexpr int WAVE = 64;
+
+// Binning: Gaussians per binning block and tile-histogram chunk (LDS words).
+constexpr int BIN_THREADS = 512;
+constexpr int BIN_MAX_BLOCKS = 256;       // one block per CU on MI355X
+constexpr int BIN_MIN_GPB = 1024;
+constexpr int BIN_TILE_CHUNK = 16384;     // 64 KiB of LDS counters per pass
+constexpr int SORT_MAX_LDS = 8192;        // tiles up to this length sort in LDS
+constexpr int PRE_THREADS = 256;          // preprocess block (scan granule)
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct GridDims {
+    int gx, gy, tiles;
+};
+__host__ __device__ inline GridDims grid_dims(int W, int H) {
+    GridDims g;
+    g.gx = (W + TILE_X - 1) / TILE_X;
+    g.gy = (H + TILE_Y - 1) / TILE_Y;
+    g.tiles = g.gx * g.gy;
+    return g;
+}
+
+// Gaussians per binning block (multiple of BIN_THREADS), and number of blocks.
+__host__ __device__ inline int bin_gpb(int P) {
+    int gpb = (P + BIN_MAX_BLOCKS - 1) / BIN_MAX_BLOCKS;
+    if (gpb < BIN_MIN_GPB) gpb = BIN_MIN_GPB;
+    return (int)align_up((size_t)gpb, BIN_THREADS);
+}
+__host__ __device__ inline int bin_blocks(int P) {
+    int gpb = bin_gpb(P);
+    int nb = (P + gpb - 1) / gpb;
+    return nb < 1 ? 1 : nb;
+}
+__host__ __device__ inline int pre_blocks(int P) { return (P + PRE_THREADS - 1) / PRE_THREADS; }
+
+// ---- control words (uint32 [16]) inside the geom buffer ----
+enum CtrlWord {
+    CTRL_NUM_RENDERED_LO = 0,
+    CTRL_NUM_RENDERED_HI = 1,
+    CTRL_PREFILTER_ERR = 2,
+    CTRL_MAX_TILE = 3,
+    CTRL_TILE_TOTAL_LO = 4,  // Σ tile counts (must equal num_rendered)
+    CTRL_WORDS = 16
+};
+
+struct GeomLayout {
+    size_t off[GSR_GEOM_NFIELDS];
+    size_t scan_sums;   // uint32 [pre_blocks(P)] block sums -> exclusive block prefixes
+    size_t bin_counts;  // uint32 [bin_blocks(P)][T] per (block, tile) counts -> offsets
+    size_t tile_total;  // uint32 [T]
+    size_t bytes;
+};
+__host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
+    GeomLayout L;
+    GridDims g = grid_dims(W, H);
+    size_t o = 0;
+    auto take = [&](size_t n) { size_t r = o; o = align_up(o + n, 256); return r; };
+    L.off[GSR_GEOM_DEPTHS] = take((size_t)P * 4);
+    L.off[GSR_GEOM_MEANS2D] = take((size_t)P * 8);
+    L.off[GSR_GEOM_SPLATS] = take((size_t)P * 48);
+    L.off[GSR_GEOM_CLAMPED] = take((size_t)P);
+    L.off[GSR_GEOM_TILES_TOUCHED] = take((size_t)P * 4);
+    L.off[GSR_GEOM_POINT_OFFSETS] = take((size_t)P * 4);
+    L.off[GSR_GEOM_RANGES] = take((size_t)g.tiles * 8);
+    L.off[GSR_GEOM_CTRL] = take(CTRL_WORDS * 4);
+    L.scan_sums = take((size_t)pre_blocks(P) * 4 + 4);
+    L.bin_counts = take((size_t)bin_blocks(P) * g.tiles * 4);
+    L.tile_total = take((size_t)g.tiles * 4);
+    L.bytes = o;
+    return L;
+}
+
+struct BinningLayout {
+    size_t off[GSR_BIN_NFIELDS];
+    size_t tmp_keys;  // uint64 [I] merge scratch for tiles longer than SORT_MAX_LDS
+    size_t bytes;
+};
+__host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H) {
+    BinningLayout L;
+    size_t n = (size_t)(I > 0 ? I : 1);
+    size_t o = 0;
+    auto take = [&](size_t b) { size_t r = o; o = align_up(o + b, 256); return r; };
+    L.off[GSR_BIN_KEYS] = take(n * 8);
+    L.off[GSR_BIN_POINT_LIST] = take(n * 4);
+    L.tmp_keys = take(n * 8);
+    L.bytes = o;
+    return L;
+}
+
+struct ImgLayout {
+    size_t off[GSR_IMG_NFIELDS];
+    size_t bytes;
+};
+__host__ __device__ inline ImgLayout img_layout(int W, int H) {
+    ImgLayout L;
+    GridDims g = grid_dims(W, H);
+    size_t o = 0;
+    auto take = [&](size_t b) { size_t r = o; o = align_up(o + b, 256); return r; };
+    L.off[GSR_IMG_FINAL_T] = take((size_t)W * H * 4);
+    L.off[GSR_IMG_N_CONTRIB] = take((size_t)W * H * 4);
+    L.off[GSR_IMG_TILE_MAX_CONTRIB] = take((size_t)g.tiles * 4);
+    L.bytes = o;
+    return L;
+}
+
+constexpr int ACCUM_STRIDE = 16;  // floats per Gaussian in the backward accumulator (64 B row)
+enum AccumSlot {
+    ACC_MEAN2D_X = 0,
+    ACC_MEAN2D_Y,
+    ACC_CONIC_X,
+    ACC_CONIC_Y,
+    ACC_CONIC_W,
+    ACC_OPACITY,
+    ACC_COLOR_R,
+    ACC_COLOR_G,
+    ACC_COLOR_B,
+    ACC_NVALS
+};
+
+template <typename T>
+__host__ __device__ inline T *at(void *base, size_t off) {
+    return reinterpret_cast<T *>(reinterpret_cast<char *>(base) + off);
+}
+template <typename T>
+__host__ __device__ inline const T *at(const void *base, size_t off) {
+    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + off);
+}
+
+// ---------------------------------------------------------------- device math
+__device__ constexpr float SH_C0 = 0.28209479177387814f;
+__device__ constexpr float SH_C1 = 0.4886025119029199f;
+__device__ constexpr float SH_C2_0 = 1.0925484305920792f;
+__device__ constexpr float SH_C2_1 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_2 = 0.31539156525252005f;
+__device__ constexpr float SH_C2_3 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_4 = 0.5462742152960396f;
+__device__ constexpr float SH_C3_0 = -0.5900435899266435f;
+__device__ constexpr float SH_C3_1 = 2.890611442640554f;
+__device__ constexpr float SH_C3_2 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_3 = 0.3731763325901154f;
+__device__ constexpr float SH_C3_4 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_5 = 1.445305721320277f;
+__device__ constexpr float SH_C3_6 = -0.5900435899266435f;
+
+// 4x4 matrices arrive as 16 floats (row-major storage of the transposed
+// matrix); like upstream they are read column-major.
+struct Mat4 {
+    float m[16];
+};
+__device__ inline Mat4 load_mat4(const float *p) {
+    Mat4 r;
+#pragma unroll
+    for (int i = 0; i < 16; i++) r.m[i] = p[i];
+    return r;
+}
+
+struct M3 {
+    float m[3][3];  // glm layout m[col][row]
+};
+
+}  // namespace gsr

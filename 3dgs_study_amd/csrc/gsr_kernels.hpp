@@ -1,0 +1,38 @@
+// gsr_kernels.hpp — host-side launchers of the gfx950 kernels (internal).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "gsr_common.hpp"
+
+namespace gsr {
+
+// preprocess.hip
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, hipStream_t s);
+hipError_t launch_scan(int P, void *geom, int W, int H, hipStream_t s);
+hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
+                               hipStream_t s);
+
+// binning.hip
+hipError_t launch_bin_count(int P, int W, int H, void *geom, const int32_t *radii, hipStream_t s);
+hipError_t launch_bin_scatter(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
+                              hipStream_t s);
+hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, uint32_t max_tile,
+                            hipStream_t s);
+
+// render_fwd.hip
+hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,
+                             float *out_color, hipStream_t s);
+
+// render_bwd.hip
+hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
+                             const void *img, const float *dL_dpix, float *accum, hipStream_t s);
+
+// preprocess_bwd.hip
+struct BwdOutputs {
+    float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *dsh, *dscales, *drot;
+};
+hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, const void *geom, const float *accum,
+                                 const BwdOutputs &o, hipStream_t s);
+
+}  // namespace gsr

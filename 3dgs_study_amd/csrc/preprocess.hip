@@ -1,0 +1,238 @@
+// preprocess.hip — forward per-Gaussian stage and the tile-count scan.
+//
+// Replaces upstream FORWARD::preprocessCUDA (forward.cu) and the
+// cub::DeviceScan::InclusiveSum of Rasterizer::forward (rasterizer_impl.cu),
+// SURVEY.md §8a rows a9/a10 and Appendix A.2-A.4.  One thread per Gaussian;
+// the per-block sums of tiles_touched are produced in the same pass so the
+// scan costs one extra small launch (block prefixes) plus a down-sweep.
+//
+// No floating-point contraction in this file: radii and tile rects must match
+// the oracle (oracle/gsr_oracle.c, built with -ffp-contract=off) bit for bit.
+#pragma clang fp contract(off)
+
+#include "gsr_kernels.hpp"
+#include "gsr_math.hpp"
+#include "gsr_wave.hpp"
+
+namespace gsr {
+
+struct PreArgs {
+    gsr_inputs in;
+    float focal_x, focal_y;
+    int gx, gy;
+    float *depths;
+    float2 *means2D;
+    float4 *splats;  // [P][3]
+    uint8_t *clamped;
+    uint32_t *tiles_touched;
+    uint32_t *scan_sums;
+    uint32_t *ctrl;
+    int32_t *radii;
+};
+
+// SH -> RGB for one Gaussian, per channel (forward.cu computeColorFromSH).
+__device__ inline float sh_channel(const float *sh, int c, int deg, float x, float y, float z) {
+#define SH(k) sh[3 * (k) + c]
+    float result = SH_C0 * SH(0);
+    if (deg > 0) {
+        result = ((result - (SH_C1 * y) * SH(1)) + (SH_C1 * z) * SH(2)) - (SH_C1 * x) * SH(3);
+        if (deg > 1) {
+            float xx = x * x, yy = y * y, zz = z * z;
+            float xy = x * y, yz = y * z, xz = x * z;
+            result = ((((result + (SH_C2_0 * xy) * SH(4)) + (SH_C2_1 * yz) * SH(5)) +
+                       (SH_C2_2 * ((2.0f * zz - xx) - yy)) * SH(6)) +
+                      (SH_C2_3 * xz) * SH(7)) +
+                     (SH_C2_4 * (xx - yy)) * SH(8);
+            if (deg > 2) {
+                result = ((((((result + ((SH_C3_0 * y) * (3.0f * xx - yy)) * SH(9)) + ((SH_C3_1 * xy) * z) * SH(10)) +
+                            ((SH_C3_2 * y) * ((4.0f * zz - xx) - yy)) * SH(11)) +
+                           ((SH_C3_3 * z) * ((2.0f * zz - 3.0f * xx) - 3.0f * yy)) * SH(12)) +
+                          ((SH_C3_4 * x) * ((4.0f * zz - xx) - yy)) * SH(13)) +
+                         ((SH_C3_5 * z) * (xx - yy)) * SH(14)) +
+                        ((SH_C3_6 * x) * (xx - 3.0f * yy)) * SH(15);
+            }
+        }
+    }
+#undef SH
+    return result + 0.5f;
+}
+
+__global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) {
+    __shared__ uint32_t wsum[PRE_THREADS / 64];
+    const gsr_inputs &in = a.in;
+    const int idx = blockIdx.x * PRE_THREADS + threadIdx.x;
+    uint32_t touched = 0;
+    if (idx < in.P) {
+        int radius_out = 0;
+        const f3 p = {in.means3D[3 * idx], in.means3D[3 * idx + 1], in.means3D[3 * idx + 2]};
+        const Mat4 V = load_mat4(in.viewmatrix);
+        const Mat4 Pm = load_mat4(in.projmatrix);
+        const f4 p_hom = xform_point4x4(p, Pm);
+        const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+        const f3 p_proj = {p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w};
+        const f3 p_view = xform_point4x3(p, V);
+        bool ok = true;
+        if (p_view.z <= 0.2f) {
+            ok = false;
+            if (in.prefiltered) atomicOr(&a.ctrl[CTRL_PREFILTER_ERR], 1u);
+        }
+        float c3[6];
+        if (ok) {
+            if (in.cov3D_precomp) {
+#pragma unroll
+                for (int k = 0; k < 6; k++) c3[k] = in.cov3D_precomp[6 * (size_t)idx + k];
+            } else {
+                const float *s = in.scales + 3 * (size_t)idx;
+                const float *q = in.rotations + 4 * (size_t)idx;
+                compute_cov3d(s[0], s[1], s[2], in.scale_modifier, q[0], q[1], q[2], q[3], c3);
+            }
+        }
+        f3 cov = {0, 0, 0};
+        float det = 0.f;
+        if (ok) {
+            cov = compute_cov2d(p, a.focal_x, a.focal_y, in.tan_fovx, in.tan_fovy, c3, V);
+            det = (cov.x * cov.z - cov.y * cov.y);
+            if (det == 0.0f) ok = false;
+        }
+        if (ok) {
+            const float det_inv = 1.f / det;
+            const float conic_x = cov.z * det_inv, conic_y = -cov.y * det_inv, conic_z = cov.x * det_inv;
+            const float mid = 0.5f * (cov.x + cov.z);
+            const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+            const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+            const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+            const float px = ndc2pix(p_proj.x, in.W), py = ndc2pix(p_proj.y, in.H);
+            const int r = f2i_sat(my_radius);
+            const TileRect rc = get_rect(px, py, r, a.gx, a.gy);
+            const uint32_t area = (rc.x1 - rc.x0) * (rc.y1 - rc.y0);
+            if (area != 0) {
+                float rgb[3];
+                uint8_t clampbits = 0;
+                if (in.colors_precomp) {
+                    rgb[0] = in.colors_precomp[3 * (size_t)idx];
+                    rgb[1] = in.colors_precomp[3 * (size_t)idx + 1];
+                    rgb[2] = in.colors_precomp[3 * (size_t)idx + 2];
+                } else {
+                    const float dx = p.x - in.campos[0], dy = p.y - in.campos[1], dz = p.z - in.campos[2];
+                    const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+                    const float x = dx / len, y = dy / len, z = dz / len;
+                    const float *sh = in.sh + (size_t)idx * in.M * 3;
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        const float v = sh_channel(sh, c, in.D, x, y, z);
+                        clampbits |= (v < 0) ? (uint8_t)(1u << c) : (uint8_t)0;
+                        rgb[c] = fmaxf(v, 0.0f);
+                    }
+                }
+                // Conservative box of the alpha >= 1/255 region: power >= -ln(255 o)
+                // <=> d^T Sigma^-1 d <= 2 ln(255 o); half-extents sqrt(2 ln(255 o) Sigma_ii),
+                // widened for rounding.  Used only to skip work that the blend
+                // would reject anyway (alpha < 1/255), never to change a result.
+                const float opac = in.opacities[idx];
+                const float lnr = logf(255.0f * opac) + 1e-3f;  // 0.1% slack on the threshold
+                float ex = -1.0f, ey = -1.0f;
+                if (lnr > 0.0f) {
+                    ex = sqrtf(2.0f * lnr * cov.x) * 1.01f + 0.5f;
+                    ey = sqrtf(2.0f * lnr * cov.z) * 1.01f + 0.5f;
+                }
+                a.depths[idx] = p_view.z;
+                a.means2D[idx] = make_float2(px, py);
+                float4 *sp = a.splats + 3 * (size_t)idx;
+                sp[0] = make_float4(px, py, conic_x, conic_y);
+                sp[1] = make_float4(conic_z, opac, rgb[0], rgb[1]);
+                sp[2] = make_float4(rgb[2], ex, ey, 0.0f);
+                a.clamped[idx] = clampbits;
+                radius_out = r;
+                touched = area;
+            }
+        }
+        a.radii[idx] = radius_out;
+        a.tiles_touched[idx] = touched;
+    }
+    const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
+    if (threadIdx.x == 0) a.scan_sums[blockIdx.x] = tot;
+}
+
+// Exclusive scan of the per-block sums in place (one workgroup, any length);
+// the grand total is num_rendered.
+constexpr int TOP_THREADS = 1024;
+__global__ void __launch_bounds__(TOP_THREADS) scan_top_kernel(uint32_t *sums, int n, uint32_t *ctrl) {
+    __shared__ uint32_t wsum[TOP_THREADS / 64];
+    uint64_t carry = 0;
+    for (int base = 0; base < n; base += TOP_THREADS) {
+        const int i = base + threadIdx.x;
+        const uint32_t v = i < n ? sums[i] : 0u;
+        uint32_t tot;
+        const uint32_t inc = block_inclusive_scan<TOP_THREADS>(v, wsum, &tot);
+        if (i < n) sums[i] = (uint32_t)carry + inc - v;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        ctrl[CTRL_NUM_RENDERED_LO] = (uint32_t)carry;
+        ctrl[CTRL_NUM_RENDERED_HI] = (uint32_t)(carry >> 32);
+    }
+}
+
+// point_offsets = inclusive scan of tiles_touched (block prefix + in-block scan).
+__global__ void __launch_bounds__(PRE_THREADS)
+    scan_down_kernel(const uint32_t *tiles_touched, const uint32_t *block_prefix, uint32_t *offsets, int P) {
+    __shared__ uint32_t wsum[PRE_THREADS / 64];
+    const int idx = blockIdx.x * PRE_THREADS + threadIdx.x;
+    const uint32_t v = idx < P ? tiles_touched[idx] : 0u;
+    uint32_t tot;
+    const uint32_t inc = block_inclusive_scan<PRE_THREADS>(v, wsum, &tot);
+    if (idx < P) offsets[idx] = block_prefix[blockIdx.x] + inc;
+}
+
+// auxiliary.h in_frustum via checkFrustum (markVisible).
+__global__ void mark_visible_kernel(int P, const float *means3D, const float *viewmatrix, uint8_t *present) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const Mat4 V = load_mat4(viewmatrix);
+    const f3 p = {means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]};
+    const f3 pv = xform_point4x3(p, V);
+    present[idx] = !(pv.z <= 0.2f);
+}
+
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, hipStream_t s) {
+    const GeomLayout L = geom_layout(in.P, in.W, in.H);
+    const GridDims g = grid_dims(in.W, in.H);
+    PreArgs a;
+    a.in = in;
+    a.focal_y = in.H / (2.0f * in.tan_fovy);  // rasterizer_impl.cu: height / (2.0f * tan_fovy)
+    a.focal_x = in.W / (2.0f * in.tan_fovx);
+    a.gx = g.gx;
+    a.gy = g.gy;
+    a.depths = at<float>(geom, L.off[GSR_GEOM_DEPTHS]);
+    a.means2D = at<float2>(geom, L.off[GSR_GEOM_MEANS2D]);
+    a.splats = at<float4>(geom, L.off[GSR_GEOM_SPLATS]);
+    a.clamped = at<uint8_t>(geom, L.off[GSR_GEOM_CLAMPED]);
+    a.tiles_touched = at<uint32_t>(geom, L.off[GSR_GEOM_TILES_TOUCHED]);
+    a.scan_sums = at<uint32_t>(geom, L.scan_sums);
+    a.ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+    a.radii = radii;
+    hipError_t e = hipMemsetAsync(a.ctrl, 0, CTRL_WORDS * 4, s);
+    if (e != hipSuccess) return e;
+    const int nb = pre_blocks(in.P);
+    hipLaunchKernelGGL(preprocess_fwd_kernel, dim3(nb), dim3(PRE_THREADS), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(int P, void *geom, int W, int H, hipStream_t s) {
+    const GeomLayout L = geom_layout(P, W, H);
+    uint32_t *sums = at<uint32_t>(geom, L.scan_sums);
+    uint32_t *ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+    const int nb = pre_blocks(P);
+    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(TOP_THREADS), 0, s, sums, nb, ctrl);
+    hipLaunchKernelGGL(scan_down_kernel, dim3(nb), dim3(PRE_THREADS), 0, s,
+                       at<const uint32_t>(geom, L.off[GSR_GEOM_TILES_TOUCHED]), (const uint32_t *)sums,
+                       at<uint32_t>(geom, L.off[GSR_GEOM_POINT_OFFSETS]), P);
+    return hipGetLastError();
+}
+
+hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present, hipStream_t s) {
+    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, viewmatrix, present);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

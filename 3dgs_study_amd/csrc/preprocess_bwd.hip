@@ -1,0 +1,291 @@
+// preprocess_bwd.hip — per-Gaussian backward (fused).
+//
+// Replaces upstream BACKWARD::computeCov2DCUDA + BACKWARD::preprocessCUDA
+// (+ computeColorFromSH / computeCov3D backward) of backward.cu (SURVEY.md
+// §8a rows a16/a17, Appendix A.8) with ONE kernel: it reads the Gaussian's
+// accumulator row written by render_bwd, recomputes cov3D/cov2D (instead of
+// storing cov3D in the forward: 24 B/Gaussian written + read saved), and
+// writes every output tensor exactly once, zeros for culled Gaussians, so the
+// caller needs no memset of the 8 gradient tensors.
+#pragma clang fp contract(off)
+
+#include "gsr_kernels.hpp"
+#include "gsr_math.hpp"
+
+namespace gsr {
+
+struct PreBwdArgs {
+    gsr_inputs in;
+    float focal_x, focal_y;
+    const int32_t *radii;
+    const uint8_t *clamped;
+    const float *accum;
+    BwdOutputs o;
+};
+
+__device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, float ox, float oy, float oz,
+                                   const float dRGB[3], f3 &dmean) {
+    const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
+    const float x = ox / len, y = oy / len, z = oz / len;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    float dRGBdx[3] = {0, 0, 0}, dRGBdy[3] = {0, 0, 0}, dRGBdz[3] = {0, 0, 0};
+    const int ncoef = (deg + 1) * (deg + 1);
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+#define SH(k) sh[3 * (k) + c]
+        const float d = dRGB[c];
+        dsh[c] = SH_C0 * d;
+        if (deg > 0) {
+            dsh[3 * 1 + c] = (-SH_C1 * y) * d;
+            dsh[3 * 2 + c] = (SH_C1 * z) * d;
+            dsh[3 * 3 + c] = (-SH_C1 * x) * d;
+            dRGBdx[c] = -SH_C1 * SH(3);
+            dRGBdy[c] = -SH_C1 * SH(1);
+            dRGBdz[c] = SH_C1 * SH(2);
+            if (deg > 1) {
+                dsh[3 * 4 + c] = (SH_C2_0 * xy) * d;
+                dsh[3 * 5 + c] = (SH_C2_1 * yz) * d;
+                dsh[3 * 6 + c] = (SH_C2_2 * (2.f * zz - xx - yy)) * d;
+                dsh[3 * 7 + c] = (SH_C2_3 * xz) * d;
+                dsh[3 * 8 + c] = (SH_C2_4 * (xx - yy)) * d;
+                dRGBdx[c] += SH_C2_0 * y * SH(4) + SH_C2_2 * 2.f * -x * SH(6) + SH_C2_3 * z * SH(7) +
+                             SH_C2_4 * 2.f * x * SH(8);
+                dRGBdy[c] += SH_C2_0 * x * SH(4) + SH_C2_1 * z * SH(5) + SH_C2_2 * 2.f * -y * SH(6) +
+                             SH_C2_4 * 2.f * -y * SH(8);
+                dRGBdz[c] += SH_C2_1 * y * SH(5) + SH_C2_2 * 2.f * 2.f * z * SH(6) + SH_C2_3 * x * SH(7);
+                if (deg > 2) {
+                    dsh[3 * 9 + c] = (SH_C3_0 * y * (3.f * xx - yy)) * d;
+                    dsh[3 * 10 + c] = (SH_C3_1 * xy * z) * d;
+                    dsh[3 * 11 + c] = (SH_C3_2 * y * (4.f * zz - xx - yy)) * d;
+                    dsh[3 * 12 + c] = (SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy)) * d;
+                    dsh[3 * 13 + c] = (SH_C3_4 * x * (4.f * zz - xx - yy)) * d;
+                    dsh[3 * 14 + c] = (SH_C3_5 * z * (xx - yy)) * d;
+                    dsh[3 * 15 + c] = (SH_C3_6 * x * (xx - 3.f * yy)) * d;
+                    dRGBdx[c] += (SH_C3_0 * SH(9) * 3.f * 2.f * xy + SH_C3_1 * SH(10) * yz +
+                                  SH_C3_2 * SH(11) * -2.f * xy + SH_C3_3 * SH(12) * -3.f * 2.f * xz +
+                                  SH_C3_4 * SH(13) * (-3.f * xx + 4.f * zz - yy) + SH_C3_5 * SH(14) * 2.f * xz +
+                                  SH_C3_6 * SH(15) * 3.f * (xx - yy));
+                    dRGBdy[c] += (SH_C3_0 * SH(9) * 3.f * (xx - yy) + SH_C3_1 * SH(10) * xz +
+                                  SH_C3_2 * SH(11) * (-3.f * yy + 4.f * zz - xx) + SH_C3_3 * SH(12) * -3.f * 2.f * yz +
+                                  SH_C3_4 * SH(13) * -2.f * xy + SH_C3_5 * SH(14) * -2.f * yz +
+                                  SH_C3_6 * SH(15) * -3.f * 2.f * xy);
+                    dRGBdz[c] += (SH_C3_1 * SH(10) * xy + SH_C3_2 * SH(11) * 4.f * 2.f * yz +
+                                  SH_C3_3 * SH(12) * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * SH(13) * 4.f * 2.f * xz +
+                                  SH_C3_5 * SH(14) * (xx - yy));
+                }
+            }
+        }
+#undef SH
+    }
+    for (int k = ncoef; k < M; k++) {
+        dsh[3 * k + 0] = 0.f;
+        dsh[3 * k + 1] = 0.f;
+        dsh[3 * k + 2] = 0.f;
+    }
+    const float ddx = (dRGBdx[0] * dRGB[0] + dRGBdx[1] * dRGB[1]) + dRGBdx[2] * dRGB[2];
+    const float ddy = (dRGBdy[0] * dRGB[0] + dRGBdy[1] * dRGB[1]) + dRGBdy[2] * dRGB[2];
+    const float ddz = (dRGBdz[0] * dRGB[0] + dRGBdz[1] * dRGB[1]) + dRGBdz[2] * dRGB[2];
+    // auxiliary.h dnormvdv
+    const float sum2 = ox * ox + oy * oy + oz * oz;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    dmean.x += ((+sum2 - ox * ox) * ddx - oy * ox * ddy - oz * ox * ddz) * invsum32;
+    dmean.y += (-ox * oy * ddx + (sum2 - oy * oy) * ddy - oz * oy * ddz) * invsum32;
+    dmean.z += (-ox * oz * ddx - oy * oz * ddy + (sum2 - oz * oz) * ddz) * invsum32;
+}
+
+__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreBwdArgs a) {
+    const gsr_inputs &in = a.in;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= in.P) return;
+    const BwdOutputs &o = a.o;
+    const bool vis = a.radii[idx] > 0;
+    float *dsh = (o.dsh && in.M > 0) ? o.dsh + (size_t)idx * in.M * 3 : nullptr;
+    if (!vis) {
+        for (int k = 0; k < 3; k++) {
+            o.dmeans2D[3 * (size_t)idx + k] = 0.f;
+            o.dcolors[3 * (size_t)idx + k] = 0.f;
+            o.dmeans3D[3 * (size_t)idx + k] = 0.f;
+            if (o.dscales) o.dscales[3 * (size_t)idx + k] = 0.f;
+        }
+        o.dopacity[idx] = 0.f;
+        for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = 0.f;
+        if (o.drot)
+            for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = 0.f;
+        if (dsh)
+            for (int k = 0; k < 3 * in.M; k++) dsh[k] = 0.f;
+        return;
+    }
+    const float *acc = a.accum + (size_t)idx * ACCUM_STRIDE;
+    const float4 acc0 = *reinterpret_cast<const float4 *>(acc);      // mean2D.x, mean2D.y, conic.x, conic.y
+    const float4 acc1 = *reinterpret_cast<const float4 *>(acc + 4);  // conic.w, opacity, color r, color g
+    const float accb = acc[8];                                       // color b
+    const float dcol[3] = {acc1.z, acc1.w, accb};
+    o.dmeans2D[3 * (size_t)idx + 0] = acc0.x;
+    o.dmeans2D[3 * (size_t)idx + 1] = acc0.y;
+    o.dmeans2D[3 * (size_t)idx + 2] = 0.f;
+    o.dcolors[3 * (size_t)idx + 0] = dcol[0];
+    o.dcolors[3 * (size_t)idx + 1] = dcol[1];
+    o.dcolors[3 * (size_t)idx + 2] = dcol[2];
+    o.dopacity[idx] = acc1.y;
+
+    const Mat4 V = load_mat4(in.viewmatrix);
+    const Mat4 Pm = load_mat4(in.projmatrix);
+    const f3 mean = {in.means3D[3 * idx], in.means3D[3 * idx + 1], in.means3D[3 * idx + 2]};
+
+    // ---- 3D covariance (recomputed exactly as the forward did)
+    float c3[6];
+    float s[3] = {0, 0, 0}, q[4] = {0, 0, 0, 0};
+    if (in.cov3D_precomp) {
+        for (int k = 0; k < 6; k++) c3[k] = in.cov3D_precomp[6 * (size_t)idx + k];
+    } else {
+        for (int k = 0; k < 3; k++) s[k] = in.scales[3 * (size_t)idx + k];
+        for (int k = 0; k < 4; k++) q[k] = in.rotations[4 * (size_t)idx + k];
+        compute_cov3d(s[0], s[1], s[2], in.scale_modifier, q[0], q[1], q[2], q[3], c3);
+    }
+
+    // ---- computeCov2DCUDA (backward.cu)
+    f3 t = xform_point4x3(mean, V);
+    const float h_x = a.focal_x, h_y = a.focal_y;
+    const float limx = 1.3f * in.tan_fovx, limy = 1.3f * in.tan_fovy;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float x_grad_mul = txtz < -limx || txtz > limx ? 0.f : 1.f;
+    const float y_grad_mul = tytz < -limy || tytz > limy ? 0.f : 1.f;
+    const M3 J = m3_cols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z, -(h_y * t.y) / (t.z * t.z), 0,
+                         0, 0);
+    const float *v = V.m;
+    const M3 W = m3_cols(v[0], v[4], v[8], v[1], v[5], v[9], v[2], v[6], v[10]);
+    const M3 Vk = m3_cols(c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]);
+    const M3 T = m3_mul(W, J);
+    M3 cov2D = m3_mul(m3_mul(m3_transpose(T), m3_transpose(Vk)), T);
+    const float ca = cov2D.m[0][0] += 0.3f;
+    const float cb = cov2D.m[0][1];
+    const float cc = cov2D.m[1][1] += 0.3f;
+    const float gx = acc0.z, gy = acc0.w, gz = acc1.x;  // dL/dconic x, y, w
+    const float denom = ca * cc - cb * cb;
+    float dL_da = 0, dL_db = 0, dL_dc = 0;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    float dc3[6] = {0, 0, 0, 0, 0, 0};
+#define TT(i, j) T.m[i][j]
+#define VV(i, j) Vk.m[i][j]
+    if (denom2inv != 0) {
+        dL_da = denom2inv * (-cc * cc * gx + 2 * cb * cc * gy + (denom - ca * cc) * gz);
+        dL_dc = denom2inv * (-ca * ca * gz + 2 * ca * cb * gy + (denom - ca * cc) * gx);
+        dL_db = denom2inv * 2 * (cb * cc * gx - (denom + 2 * cb * cb) * gy + ca * cb * gz);
+        dc3[0] = (TT(0, 0) * TT(0, 0) * dL_da + TT(0, 0) * TT(1, 0) * dL_db + TT(1, 0) * TT(1, 0) * dL_dc);
+        dc3[3] = (TT(0, 1) * TT(0, 1) * dL_da + TT(0, 1) * TT(1, 1) * dL_db + TT(1, 1) * TT(1, 1) * dL_dc);
+        dc3[5] = (TT(0, 2) * TT(0, 2) * dL_da + TT(0, 2) * TT(1, 2) * dL_db + TT(1, 2) * TT(1, 2) * dL_dc);
+        dc3[1] = 2 * TT(0, 0) * TT(0, 1) * dL_da + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dL_db +
+                 2 * TT(1, 0) * TT(1, 1) * dL_dc;
+        dc3[2] = 2 * TT(0, 0) * TT(0, 2) * dL_da + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dL_db +
+                 2 * TT(1, 0) * TT(1, 2) * dL_dc;
+        dc3[4] = 2 * TT(0, 2) * TT(0, 1) * dL_da + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dL_db +
+                 2 * TT(1, 1) * TT(1, 2) * dL_dc;
+    }
+    const float dL_dT00 = 2 * (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_da +
+                          (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_db;
+    const float dL_dT01 = 2 * (TT(0, 0) * VV(1, 0) + TT(0, 1) * VV(1, 1) + TT(0, 2) * VV(1, 2)) * dL_da +
+                          (TT(1, 0) * VV(1, 0) + TT(1, 1) * VV(1, 1) + TT(1, 2) * VV(1, 2)) * dL_db;
+    const float dL_dT02 = 2 * (TT(0, 0) * VV(2, 0) + TT(0, 1) * VV(2, 1) + TT(0, 2) * VV(2, 2)) * dL_da +
+                          (TT(1, 0) * VV(2, 0) + TT(1, 1) * VV(2, 1) + TT(1, 2) * VV(2, 2)) * dL_db;
+    const float dL_dT10 = 2 * (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_dc +
+                          (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_db;
+    const float dL_dT11 = 2 * (TT(1, 0) * VV(1, 0) + TT(1, 1) * VV(1, 1) + TT(1, 2) * VV(1, 2)) * dL_dc +
+                          (TT(0, 0) * VV(1, 0) + TT(0, 1) * VV(1, 1) + TT(0, 2) * VV(1, 2)) * dL_db;
+    const float dL_dT12 = 2 * (TT(1, 0) * VV(2, 0) + TT(1, 1) * VV(2, 1) + TT(1, 2) * VV(2, 2)) * dL_dc +
+                          (TT(0, 0) * VV(2, 0) + TT(0, 1) * VV(2, 1) + TT(0, 2) * VV(2, 2)) * dL_db;
+#undef TT
+#undef VV
+    const float dL_dJ00 = W.m[0][0] * dL_dT00 + W.m[0][1] * dL_dT01 + W.m[0][2] * dL_dT02;
+    const float dL_dJ02 = W.m[2][0] * dL_dT00 + W.m[2][1] * dL_dT01 + W.m[2][2] * dL_dT02;
+    const float dL_dJ11 = W.m[1][0] * dL_dT10 + W.m[1][1] * dL_dT11 + W.m[1][2] * dL_dT12;
+    const float dL_dJ12 = W.m[2][0] * dL_dT10 + W.m[2][1] * dL_dT11 + W.m[2][2] * dL_dT12;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+    const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+    const float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
+                         (2 * h_y * t.y) * tz3 * dL_dJ12;
+    f3 dmean = xform_vec4x3_transpose(f3{dL_dtx, dL_dty, dL_dtz}, V);
+    for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = dc3[k];
+
+    // ---- preprocessCUDA (backward.cu): 2D-mean gradient through the projection
+    const f4 m_hom = xform_point4x4(mean, Pm);
+    const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+    const float *pm = Pm.m;
+    const float mul1 = (pm[0] * mean.x + pm[4] * mean.y + pm[8] * mean.z + pm[12]) * m_w * m_w;
+    const float mul2 = (pm[1] * mean.x + pm[5] * mean.y + pm[9] * mean.z + pm[13]) * m_w * m_w;
+    const float g2x = acc0.x, g2y = acc0.y;
+    dmean.x += (pm[0] * m_w - pm[3] * mul1) * g2x + (pm[1] * m_w - pm[3] * mul2) * g2y;
+    dmean.y += (pm[4] * m_w - pm[7] * mul1) * g2x + (pm[5] * m_w - pm[7] * mul2) * g2y;
+    dmean.z += (pm[8] * m_w - pm[11] * mul1) * g2x + (pm[9] * m_w - pm[11] * mul2) * g2y;
+
+    // ---- SH backward (colour gradient masked where the forward clamped)
+    if (in.sh && dsh) {
+        const uint8_t cl = a.clamped[idx];
+        const float dRGB[3] = {dcol[0] * ((cl & 1) ? 0.f : 1.f), dcol[1] * ((cl & 2) ? 0.f : 1.f),
+                               dcol[2] * ((cl & 4) ? 0.f : 1.f)};
+        sh_backward(in.sh + (size_t)idx * in.M * 3, dsh, in.D, in.M, mean.x - in.campos[0], mean.y - in.campos[1],
+                    mean.z - in.campos[2], dRGB, dmean);
+    }
+    o.dmeans3D[3 * (size_t)idx + 0] = dmean.x;
+    o.dmeans3D[3 * (size_t)idx + 1] = dmean.y;
+    o.dmeans3D[3 * (size_t)idx + 2] = dmean.z;
+
+    // ---- computeCov3D backward: dSigma -> dM = 2 M dSigma -> dscale, drot (q as given)
+    if (in.scales && o.dscales && o.drot) {
+        const float qr = q[0], qx = q[1], qy = q[2], qz = q[3];
+        const M3 R = quat_to_rot(qr, qx, qy, qz);
+        M3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        const float sm[3] = {in.scale_modifier * s[0], in.scale_modifier * s[1], in.scale_modifier * s[2]};
+        S.m[0][0] = sm[0];
+        S.m[1][1] = sm[1];
+        S.m[2][2] = sm[2];
+        const M3 Mm = m3_mul(S, R);
+        const float *d = dc3;
+        const M3 dSig = m3_cols(d[0], 0.5f * d[1], 0.5f * d[2], 0.5f * d[1], d[3], 0.5f * d[4], 0.5f * d[2],
+                                0.5f * d[4], d[5]);
+        M3 twoM;
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) twoM.m[i][j] = 2.0f * Mm.m[i][j];
+        const M3 dM = m3_mul(twoM, dSig);
+        const M3 Rt = m3_transpose(R);
+        M3 dMt = m3_transpose(dM);
+        for (int k = 0; k < 3; k++)
+            o.dscales[3 * (size_t)idx + k] =
+                (Rt.m[k][0] * dMt.m[k][0] + Rt.m[k][1] * dMt.m[k][1]) + Rt.m[k][2] * dMt.m[k][2];
+        for (int k = 0; k < 3; k++)
+            for (int j = 0; j < 3; j++) dMt.m[k][j] *= sm[k];
+#define D(i, j) dMt.m[i][j]
+        o.drot[4 * (size_t)idx + 0] = 2 * qz * (D(0, 1) - D(1, 0)) + 2 * qy * (D(2, 0) - D(0, 2)) + 2 * qx * (D(1, 2) - D(2, 1));
+        o.drot[4 * (size_t)idx + 1] = 2 * qy * (D(1, 0) + D(0, 1)) + 2 * qz * (D(2, 0) + D(0, 2)) +
+                                      2 * qr * (D(1, 2) - D(2, 1)) - 4 * qx * (D(2, 2) + D(1, 1));
+        o.drot[4 * (size_t)idx + 2] = 2 * qx * (D(1, 0) + D(0, 1)) + 2 * qr * (D(2, 0) - D(0, 2)) +
+                                      2 * qz * (D(1, 2) + D(2, 1)) - 4 * qy * (D(2, 2) + D(0, 0));
+        o.drot[4 * (size_t)idx + 3] = 2 * qr * (D(0, 1) - D(1, 0)) + 2 * qx * (D(2, 0) + D(0, 2)) +
+                                      2 * qy * (D(1, 2) + D(2, 1)) - 4 * qz * (D(1, 1) + D(0, 0));
+#undef D
+    } else {
+        if (o.dscales)
+            for (int k = 0; k < 3; k++) o.dscales[3 * (size_t)idx + k] = 0.f;
+        if (o.drot)
+            for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = 0.f;
+    }
+}
+
+hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, const void *geom, const float *accum,
+                                 const BwdOutputs &o, hipStream_t s) {
+    const GeomLayout G = geom_layout(in.P, in.W, in.H);
+    PreBwdArgs a;
+    a.in = in;
+    a.focal_y = in.H / (2.0f * in.tan_fovy);
+    a.focal_x = in.W / (2.0f * in.tan_fovx);
+    a.radii = radii;
+    a.clamped = at<uint8_t>(geom, G.off[GSR_GEOM_CLAMPED]);
+    a.accum = accum;
+    a.o = o;
+    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -1,0 +1,243 @@
+"""``_C`` — the native entry points of ``diff_gaussian_rasterization``, bound to the
+C ABI of ``libgsr.so`` (``include/gsr.h``) with ctypes.
+
+Upstream this module is a pybind11 extension (``ext.cpp`` + ``rasterize_points.cu``)
+exporting ``rasterize_gaussians``, ``rasterize_gaussians_backward`` and ``mark_visible``
+([UPSTREAM-SPEC]); the reference calls them through the autograd
+wrapper in ``__init__.py`` from ``gaussian_renderer/__init__.py:98-106``.  This module
+keeps those three names, their positional argument order, their return tuples and
+their error behaviour, and does the work the C++ glue did upstream:
+
+* ``.contiguous()`` on every input, ``torch.Tensor([])`` / empty -> NULL pointer,
+  ``M = sh.size(1)`` when ``sh`` is non-empty;
+* output and scratch allocation through torch's caching allocator (the library
+  never allocates device memory): color [3,H,W] f32, radii [P] i32 and three
+  uint8 scratch buffers whose sizes come from the library;
+* the launches go to ``torch.cuda.current_stream()``.
+
+There is no CPU path: the library must be present and the tensors must live on a
+ROCm device, otherwise these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_LIB_NAME = "libgsr.so"
+_DEFAULT = Path(__file__).resolve().parent.parent / "lib" / _LIB_NAME
+
+
+class GsrInputs(ctypes.Structure):
+    """Mirror of ``struct gsr_inputs`` in include/gsr.h."""
+    _fields_ = [
+        ("P", ctypes.c_int32), ("D", ctypes.c_int32), ("M", ctypes.c_int32),
+        ("W", ctypes.c_int32), ("H", ctypes.c_int32),
+        ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float), ("scale_modifier", ctypes.c_float),
+        ("prefiltered", ctypes.c_int32), ("debug", ctypes.c_int32),
+        ("bg", ctypes.c_void_p), ("means3D", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
+        ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p), ("rotations", ctypes.c_void_p),
+        ("cov3D_precomp", ctypes.c_void_p), ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
+        ("sh", ctypes.c_void_p), ("campos", ctypes.c_void_p),
+    ]
+
+
+# every symbol include/gsr.h declares (checked by tests/test_abi.py)
+EXPORTED = (
+    "gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr_accum_bytes",
+    "gsr_forward_preprocess", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
+    "gsr_geom_layout", "gsr_binning_layout", "gsr_img_layout", "gsr_last_error", "gsr_abi_version",
+)
+ABI_VERSION = 1
+
+_lib = None
+
+
+def library_path() -> Path:
+    return Path(os.environ.get("GSR_LIBRARY", str(_DEFAULT)))
+
+
+def load_library():
+    """Load libgsr.so; raise loudly if it is missing (no fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not path.exists():
+        raise ImportError(
+            f"diff_gaussian_rasterization: native library {path} not found; build it with "
+            "`python -c 'import __graft_entry__; __graft_entry__.build()'` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(str(path))
+    sz, i32, i64, vp = ctypes.c_size_t, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
+    lib.gsr_geom_bytes.argtypes = [i32, i32, i32]
+    lib.gsr_geom_bytes.restype = sz
+    lib.gsr_binning_bytes.argtypes = [i64, i32, i32]
+    lib.gsr_binning_bytes.restype = sz
+    lib.gsr_img_bytes.argtypes = [i32, i32]
+    lib.gsr_img_bytes.restype = sz
+    lib.gsr_accum_bytes.argtypes = [i32]
+    lib.gsr_accum_bytes.restype = sz
+    pin = ctypes.POINTER(GsrInputs)
+    lib.gsr_forward_preprocess.argtypes = [pin, vp, vp, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_uint32), vp]
+    lib.gsr_forward_preprocess.restype = ctypes.c_int
+    lib.gsr_forward_render.argtypes = [pin, vp, vp, vp, i64, ctypes.c_uint32, vp, vp, vp]
+    lib.gsr_forward_render.restype = ctypes.c_int
+    lib.gsr_backward.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
+    lib.gsr_backward.restype = ctypes.c_int
+    lib.gsr_mark_visible.argtypes = [i32, vp, vp, vp, vp, vp]
+    lib.gsr_mark_visible.restype = ctypes.c_int
+    for name in ("gsr_geom_layout", "gsr_binning_layout", "gsr_img_layout"):
+        getattr(lib, name).restype = ctypes.c_int
+    lib.gsr_geom_layout.argtypes = [i32, i32, i32, ctypes.POINTER(sz), ctypes.c_int]
+    lib.gsr_binning_layout.argtypes = [i64, i32, i32, ctypes.POINTER(sz), ctypes.c_int]
+    lib.gsr_img_layout.argtypes = [i32, i32, ctypes.POINTER(sz), ctypes.c_int]
+    lib.gsr_last_error.restype = ctypes.c_char_p
+    lib.gsr_abi_version.restype = ctypes.c_int
+    if lib.gsr_abi_version() != ABI_VERSION:
+        raise ImportError(f"{path}: ABI version {lib.gsr_abi_version()} != {ABI_VERSION}; rebuild")
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.gsr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+def _ptr(t):
+    """Device pointer of a tensor, or None (NULL) for an empty/absent tensor."""
+    if t is None or t.numel() == 0:
+        return None
+    return t.data_ptr()
+
+
+def _prep(t, name, device):
+    """upstream `.contiguous()` + dtype/device checks; empty stays empty."""
+    if t is None or t.numel() == 0:
+        return None
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    if t.device != device:
+        raise RuntimeError(f"{name} is on {t.device}, expected {device}")
+    return t.contiguous()
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+            tan_fovx, tan_fovy, H, W, sh, degree, campos, prefiltered, debug):
+    if means3D.ndim != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    device = means3D.device
+    if device.type != "cuda":
+        raise RuntimeError("diff_gaussian_rasterization: tensors must be on a ROCm device (got %s); "
+                           "there is no CPU implementation" % device)
+    keep = {}
+    for name, t in (("background", bg), ("means3D", means3D), ("colors", colors), ("opacity", opacity),
+                    ("scales", scales), ("rotations", rotations), ("cov3D_precomp", cov3D_precomp),
+                    ("viewmatrix", viewmatrix), ("projmatrix", projmatrix), ("sh", sh), ("campos", campos)):
+        keep[name] = _prep(t, name, device)
+    P = means3D.size(0)
+    sh_t = keep["sh"]
+    M = sh_t.size(1) if (sh_t is not None and sh_t.size(0) != 0) else 0
+    s = GsrInputs(P=P, D=int(degree), M=M, W=int(W), H=int(H), tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
+                  scale_modifier=float(scale_modifier), prefiltered=int(bool(prefiltered)), debug=int(bool(debug)),
+                  bg=_ptr(keep["background"]), means3D=_ptr(keep["means3D"]), colors_precomp=_ptr(keep["colors"]),
+                  opacities=_ptr(keep["opacity"]), scales=_ptr(keep["scales"]), rotations=_ptr(keep["rotations"]),
+                  cov3D_precomp=_ptr(keep["cov3D_precomp"]), viewmatrix=_ptr(keep["viewmatrix"]),
+                  projmatrix=_ptr(keep["projmatrix"]), sh=_ptr(sh_t), campos=_ptr(keep["campos"]))
+    return s, keep, device, M
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                        prefiltered, debug):
+    """-> (num_rendered, color [3,H,W], radii [P] int32, geomBuffer, binningBuffer, imgBuffer)"""
+    lib = load_library()
+    H, W = int(image_height), int(image_width)
+    s, keep, device, M = _inputs(background, means3D, colors, opacity, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos,
+                                 prefiltered, debug)
+    P = s.P
+    u8 = dict(dtype=torch.uint8, device=device)
+    out_color = torch.empty((3, H, W), dtype=torch.float32, device=device)
+    radii = torch.empty((P,), dtype=torch.int32, device=device)
+    geom = torch.empty((lib.gsr_geom_bytes(P, W, H),), **u8)
+    img = torch.empty((lib.gsr_img_bytes(W, H),), **u8)
+    stream = _stream(device)
+    num_rendered = ctypes.c_int64(0)
+    max_tile = ctypes.c_uint32(0)
+    _check(lib.gsr_forward_preprocess(ctypes.byref(s), geom.data_ptr(), _ptr(radii), ctypes.byref(num_rendered),
+                                      ctypes.byref(max_tile), stream), "rasterize_gaussians (preprocess)")
+    binning = torch.empty((lib.gsr_binning_bytes(num_rendered.value, W, H),), **u8)
+    _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
+                                  num_rendered.value, max_tile.value, _ptr(radii), out_color.data_ptr(), stream),
+           "rasterize_gaussians (render)")
+    return num_rendered.value, out_color, radii, geom, binning, img
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
+                                 viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
+                                 geomBuffer, R, binningBuffer, imageBuffer, debug):
+    """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)"""
+    lib = load_library()
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    s, keep, device, M = _inputs(background, means3D, colors, None, scales, rotations, scale_modifier, cov3D_precomp,
+                                 viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
+    P = s.P
+    f32 = dict(dtype=torch.float32, device=device)
+    dmeans2D = torch.empty((P, 3), **f32)
+    dcolors = torch.empty((P, 3), **f32)
+    dopacity = torch.empty((P, 1), **f32)
+    dmeans3D = torch.empty((P, 3), **f32)
+    dcov3D = torch.empty((P, 6), **f32)
+    dsh = torch.empty((P, M, 3), **f32)
+    dscales = torch.empty((P, 3), **f32)
+    drot = torch.empty((P, 4), **f32)
+    if P == 0:
+        return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
+    accum = torch.empty((lib.gsr_accum_bytes(P),), dtype=torch.uint8, device=device)
+    grad = _prep(dL_dout_color, "dL_dout_color", device)
+    radii = radii.contiguous()
+    _check(lib.gsr_backward(ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),
+                            binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+                            int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), dcolors.data_ptr(),
+                            dopacity.data_ptr(), dmeans3D.data_ptr(), dcov3D.data_ptr(), _ptr(dsh),
+                            dscales.data_ptr(), drot.data_ptr(), _stream(device)),
+           "rasterize_gaussians_backward")
+    return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """-> present [P] bool (view-space z > 0.2)"""
+    lib = load_library()
+    if means3D.ndim != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    device = means3D.device
+    P = means3D.size(0)
+    present = torch.empty((P,), dtype=torch.bool, device=device)
+    m = _prep(means3D, "means3D", device)
+    v = _prep(viewmatrix, "viewmatrix", device)
+    p = _prep(projmatrix, "projmatrix", device)
+    _check(lib.gsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(device)), "mark_visible")
+    return present
+
+
+# ------------------------------------------------------------------ test hooks
+def layouts(P, W, H, num_rendered):
+    """Byte offsets of the named scratch sub-arrays (parity tests read intermediates)."""
+    lib = load_library()
+    g = (ctypes.c_size_t * 16)()
+    n = lib.gsr_geom_layout(P, W, H, g, 16)
+    b = (ctypes.c_size_t * 16)()
+    nb = lib.gsr_binning_layout(num_rendered, W, H, b, 16)
+    im = (ctypes.c_size_t * 16)()
+    ni = lib.gsr_img_layout(W, H, im, 16)
+    geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "point_offsets", "ranges", "ctrl")
+    return (dict(zip(geom_names, list(g)[:n])), dict(zip(("keys", "point_list"), list(b)[:nb])),
+            dict(zip(("final_T", "n_contrib", "tile_max_contrib"), list(im)[:ni])))

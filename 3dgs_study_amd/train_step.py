@@ -1,0 +1,154 @@
+"""The render -> loss -> backward unit around the rasterizer (host side).
+
+``render`` reproduces the reference's ``gaussian_renderer.render``
+(gaussian_renderer/__init__.py:20-112) against this
+package's ``diff_gaussian_rasterization``: the dummy screen-space means
+(``zeros_like(xyz) + 0`` with ``retain_grad``), tan-FoV, the 12-field settings,
+the SH-vs-precomputed-colour and scale/rotation-vs-cov3D branches, and the
+returned dict.  It exists so that tests and ``bench.py`` can drive the boundary
+exactly as the reference does on a machine where the reference is absent (the
+GPU box).  ``eval_sh`` / ``covariance`` restate utils/sh_utils.py:57-112 and
+utils/general_utils.py:86-128 + scene/gaussian_model.py:27-32 for the
+``convert_SHs_python`` / ``compute_cov3D_python`` branches.
+
+``train_step`` is the unit bench.py times: one view's render, the loss of
+train.py:102-104 (L1, or L1 + 0.2·(1 - SSIM)), and ``loss.backward()``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+
+SH_C0 = 0.28209479177387814
+SH_C1 = 0.4886025119029199
+SH_C2 = (1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396)
+SH_C3 = (-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+         1.445305721320277, -0.5900435899266435)
+
+
+def eval_sh(deg: int, sh: torch.Tensor, dirs: torch.Tensor) -> torch.Tensor:
+    """SH -> value for degree <= 3; sh [..., C, (deg+1)^2], dirs [..., 3] (utils/sh_utils.py:57-112)."""
+    assert 0 <= deg <= 3 and sh.shape[-1] >= (deg + 1) ** 2
+    out = SH_C0 * sh[..., 0]
+    if deg > 0:
+        x, y, z = dirs[..., 0:1], dirs[..., 1:2], dirs[..., 2:3]
+        out = out - SH_C1 * y * sh[..., 1] + SH_C1 * z * sh[..., 2] - SH_C1 * x * sh[..., 3]
+        if deg > 1:
+            xx, yy, zz = x * x, y * y, z * z
+            xy, yz, xz = x * y, y * z, x * z
+            out = (out + SH_C2[0] * xy * sh[..., 4] + SH_C2[1] * yz * sh[..., 5] +
+                   SH_C2[2] * (2.0 * zz - xx - yy) * sh[..., 6] + SH_C2[3] * xz * sh[..., 7] +
+                   SH_C2[4] * (xx - yy) * sh[..., 8])
+            if deg > 2:
+                out = (out + SH_C3[0] * y * (3 * xx - yy) * sh[..., 9] + SH_C3[1] * xy * z * sh[..., 10] +
+                       SH_C3[2] * y * (4 * zz - xx - yy) * sh[..., 11] +
+                       SH_C3[3] * z * (2 * zz - 3 * xx - 3 * yy) * sh[..., 12] +
+                       SH_C3[4] * x * (4 * zz - xx - yy) * sh[..., 13] + SH_C3[5] * z * (xx - yy) * sh[..., 14] +
+                       SH_C3[6] * x * (xx - 3 * yy) * sh[..., 15])
+    return out
+
+
+def rotation_matrix(q: torch.Tensor) -> torch.Tensor:
+    """Normalised quaternion (r,x,y,z) -> R [P,3,3] (utils/general_utils.py:86-117)."""
+    q = q / torch.sqrt((q * q).sum(dim=1, keepdim=True))
+    r, x, y, z = q.unbind(dim=1)
+    return torch.stack([
+        1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+        2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+        2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], dim=1).view(-1, 3, 3)
+
+
+def covariance(scaling: torch.Tensor, scaling_modifier: float, rotation: torch.Tensor) -> torch.Tensor:
+    """Upper triangle of (R S)(R S)^T -> [P,6] (scene/gaussian_model.py:27-32)."""
+    L = rotation_matrix(rotation) * (scaling_modifier * scaling)[:, None, :]
+    S = L @ L.transpose(1, 2)
+    return torch.stack([S[:, 0, 0], S[:, 0, 1], S[:, 0, 2], S[:, 1, 1], S[:, 1, 2], S[:, 2, 2]], dim=1)
+
+
+def render(viewpoint_camera, pc, bg_color: torch.Tensor, scaling_modifier: float = 1.0, override_color=None,
+           convert_SHs_python: bool = False, compute_cov3D_python: bool = False, debug: bool = False) -> dict:
+    xyz = pc.get_xyz
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device) + 0
+    try:
+        screenspace_points.retain_grad()
+    except Exception:
+        pass
+    tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
+    tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
+    raster_settings = GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+        tanfovx=tanfovx, tanfovy=tanfovy, bg=bg_color, scale_modifier=scaling_modifier,
+        viewmatrix=viewpoint_camera.world_view_transform, projmatrix=viewpoint_camera.full_proj_transform,
+        sh_degree=pc.active_sh_degree, campos=viewpoint_camera.camera_center, prefiltered=False, debug=debug)
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    scales = rotations = cov3D_precomp = None
+    if compute_cov3D_python:
+        cov3D_precomp = covariance(pc.get_scaling, scaling_modifier, pc.rotation)
+    else:
+        scales = pc.get_scaling
+        rotations = pc.get_rotation
+    shs = colors_precomp = None
+    if override_color is None:
+        if convert_SHs_python:
+            feats = pc.get_features
+            shs_view = feats.transpose(1, 2).view(-1, 3, (pc.max_sh_degree + 1) ** 2)
+            dir_pp = xyz - viewpoint_camera.camera_center.repeat(feats.shape[0], 1)
+            dir_pp_normalized = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+            colors_precomp = torch.clamp_min(eval_sh(pc.active_sh_degree, shs_view, dir_pp_normalized) + 0.5, 0.0)
+        else:
+            shs = pc.get_features
+    else:
+        colors_precomp = override_color
+    rendered_image, radii = rasterizer(means3D=xyz, means2D=screenspace_points, shs=shs, colors_precomp=colors_precomp,
+                                       opacities=pc.get_opacity, scales=scales, rotations=rotations,
+                                       cov3D_precomp=cov3D_precomp)
+    return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
+            "radii": radii}
+
+
+# ---------------------------------------------------------------- losses (utils/loss_utils.py)
+def l1_loss(network_output: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+    return torch.abs(network_output - gt).mean()
+
+
+def _gaussian_window(window_size: int, sigma: float, channel: int, device, dtype) -> torch.Tensor:
+    x = torch.arange(window_size, dtype=torch.float64) - window_size // 2
+    g = torch.exp(-(x ** 2) / (2 * sigma ** 2))
+    g = (g / g.sum()).to(dtype)
+    w2 = g[:, None] @ g[None, :]
+    return w2.expand(channel, 1, window_size, window_size).contiguous().to(device)
+
+
+def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11) -> torch.Tensor:
+    """SSIM with an 11x11 Gaussian window (sigma 1.5), depthwise conv2d, mean over pixels."""
+    channel = img1.size(-3)
+    w = _gaussian_window(window_size, 1.5, channel, img1.device, img1.dtype)
+    x1 = img1.unsqueeze(0) if img1.dim() == 3 else img1
+    x2 = img2.unsqueeze(0) if img2.dim() == 3 else img2
+    pad = window_size // 2
+    mu1 = F.conv2d(x1, w, padding=pad, groups=channel)
+    mu2 = F.conv2d(x2, w, padding=pad, groups=channel)
+    mu1_sq, mu2_sq, mu1_mu2 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+    sigma1_sq = F.conv2d(x1 * x1, w, padding=pad, groups=channel) - mu1_sq
+    sigma2_sq = F.conv2d(x2 * x2, w, padding=pad, groups=channel) - mu2_sq
+    sigma12 = F.conv2d(x1 * x2, w, padding=pad, groups=channel) - mu1_mu2
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    ssim_map = ((2 * mu1_mu2 + C1) * (2 * sigma12 + C2)) / ((mu1_sq + mu2_sq + C1) * (sigma1_sq + sigma2_sq + C2))
+    return ssim_map.mean()
+
+
+def train_step(camera, gaussians, target: torch.Tensor, bg: torch.Tensor, lambda_dssim: float = 0.0) -> dict:
+    """render -> loss -> backward for one view (train.py:98-105). lambda_dssim=0 is the
+    L1-only headline unit; 0.2 is the reference's default loss."""
+    out = render(camera, gaussians, bg)
+    image = out["render"]
+    loss = l1_loss(image, target)
+    if lambda_dssim:
+        loss = (1.0 - lambda_dssim) * loss + lambda_dssim * (1.0 - ssim(image, target))
+    loss.backward()
+    out["loss"] = loss
+    return out

@@ -1,0 +1,155 @@
+/*
+ * gsr.h — C ABI of the MI355X (gfx950) differentiable Gaussian rasterizer.
+ *
+ * This is the drop-in boundary beneath the Python package
+ * `diff_gaussian_rasterization` (3dgs_study_amd/diff_gaussian_rasterization),
+ * which the reference imports at gaussian_renderer/__init__.py:14 and calls at
+ * gaussian_renderer/__init__.py:98-106.  Upstream, the same boundary is the
+ * pybind11 module `_C` with three entry points ([UPSTREAM-SPEC]):
+ *
+ *   _C.rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations,
+ *       scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tanfovx,
+ *       tanfovy, image_height, image_width, sh, sh_degree, campos,
+ *       prefiltered, debug)
+ *       -> (num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer)
+ *   _C.rasterize_gaussians_backward(bg, means3D, radii, colors, scales,
+ *       rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+ *       tanfovx, tanfovy, dL_dout_color, sh, sh_degree, campos, geomBuffer,
+ *       num_rendered, binningBuffer, imgBuffer, debug)
+ *       -> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)
+ *   _C.mark_visible(means3D, viewmatrix, projmatrix) -> present
+ *
+ * Here the same work is split into C functions with plain pointers and sizes
+ * (no torch types).  The caller owns every buffer: the library never
+ * allocates device memory.  All pointers are device pointers unless noted;
+ * `stream` is a hipStream_t.  Optional inputs use NULL = absent (upstream's
+ * empty-tensor convention).  Every function returns 0 on success or a
+ * nonzero gsr_status; gsr_last_error() then describes the failure
+ * (thread-local string).
+ *
+ * Forward is two calls because the binning buffer's size depends on
+ * num_rendered, which needs one device->host read (upstream does the same
+ * cudaMemcpy inside Rasterizer::forward):
+ *   1. gsr_forward_preprocess: per-Gaussian projection, SH, tile counts, scan
+ *      -> *num_rendered (host), synchronises `stream` once;
+ *   2. caller allocates gsr_binning_bytes(num_rendered, W, H) bytes;
+ *   3. gsr_forward_render: bucket by tile, per-tile depth sort, blend.
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_ABI_VERSION 1
+
+enum gsr_status {
+    GSR_OK = 0,
+    GSR_ERR_ARGS = 1,        /* bad sizes / pointer combination (upstream AT_ERROR / Exception) */
+    GSR_ERR_HIP = 2,         /* HIP runtime error (launch failure, fault) */
+    GSR_ERR_PREFILTERED = 3, /* a point was culled although prefiltered=1 (upstream __trap) */
+    GSR_ERR_CAPACITY = 4     /* image/tile count beyond the supported range */
+};
+
+/* Inputs shared by forward and backward.  Mirrors the argument list of
+ * _C.rasterize_gaussians (rasterize_points.cu RasterizeGaussiansCUDA). */
+typedef struct gsr_inputs {
+    int32_t P;                  /* number of Gaussians (means3D.size(0)) */
+    int32_t D;                  /* active SH degree (sh_degree) */
+    int32_t M;                  /* SH coefficients per channel = sh.size(1), 0 if sh == NULL */
+    int32_t W, H;               /* image_width, image_height */
+    float tan_fovx, tan_fovy;   /* tanfovx, tanfovy */
+    float scale_modifier;
+    int32_t prefiltered;        /* bool */
+    int32_t debug;              /* bool: synchronise + check after every kernel */
+    const float *bg;            /* [3]   background colour */
+    const float *means3D;       /* [P,3] */
+    const float *colors_precomp;/* [P,3] or NULL */
+    const float *opacities;     /* [P,1] */
+    const float *scales;        /* [P,3] or NULL */
+    const float *rotations;     /* [P,4] or NULL (quaternion r,x,y,z, used as given) */
+    const float *cov3D_precomp; /* [P,6] or NULL */
+    const float *viewmatrix;    /* [4,4] row-major storage of W2C^T (scene/cameras.py:103) */
+    const float *projmatrix;    /* [4,4] full_proj_transform (scene/cameras.py:114-118) */
+    const float *sh;            /* [P,M,3] or NULL */
+    const float *campos;        /* [3]   camera_center (scene/cameras.py:121) */
+} gsr_inputs;
+
+/* Scratch sizes in bytes (all buffers 256-byte aligned internally).
+ * geom:    per-Gaussian state + per-tile counting scratch (upstream GeometryState)
+ * binning: per-instance keys and the sorted point list (upstream BinningState)
+ * img:     per-pixel final T / contributor counts (ImageState)
+ * accum:   backward per-Gaussian gradient accumulators (64 B per Gaussian) */
+size_t gsr_geom_bytes(int32_t P, int32_t W, int32_t H);
+size_t gsr_binning_bytes(int64_t num_rendered, int32_t W, int32_t H);
+size_t gsr_img_bytes(int32_t W, int32_t H);
+size_t gsr_accum_bytes(int32_t P);
+
+/* Replaces the first half of RasterizeGaussiansCUDA -> Rasterizer::forward
+ * (preprocess + InclusiveSum + the num_rendered cudaMemcpy), and also runs the
+ * per-tile counting that yields the tile ranges (identifyTileRanges' output).
+ * Writes radii [P] int32, *num_rendered and *max_tile_len (host pointers;
+ * max_tile_len may be NULL). */
+int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered,
+                           uint32_t *max_tile_len, void *stream);
+
+/* Replaces the second half of Rasterizer::forward (duplicateWithKeys,
+ * SortPairs, FORWARD::render).  out_color is [3,H,W]; radii as written by
+ * gsr_forward_preprocess; max_tile_len as returned by it. */
+int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
+                       uint32_t max_tile_len, const int32_t *radii, float *out_color, void *stream);
+
+/* Replaces RasterizeGaussiansBackwardCUDA -> Rasterizer::backward.
+ * Every output is fully written (no pre-zeroing needed); dsh may be NULL when
+ * in->sh is NULL, dscales/drot may be NULL when in->scales is NULL.
+ * Shapes: dmeans2D [P,3], dcolors [P,3], dopacity [P,1], dmeans3D [P,3],
+ * dcov3D [P,6], dsh [P,M,3], dscales [P,3], drot [P,4]. */
+int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning, const void *img,
+                 int64_t num_rendered, const float *dL_dout_color, void *accum, float *dmeans2D, float *dcolors,
+                 float *dopacity, float *dmeans3D, float *dcov3D, float *dsh, float *dscales, float *drot,
+                 void *stream);
+
+/* Replaces markVisible (rasterize_points.cu) / checkFrustum:
+ * present[i] = (viewmatrix * means3D[i]).z > 0.2.  present is [P] bytes. */
+int gsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *present, void *stream);
+
+/* Introspection for parity tests: byte offsets of the named sub-arrays inside
+ * the scratch buffers.  Returns the number of entries written (<= cap). */
+enum gsr_geom_field {
+    GSR_GEOM_DEPTHS = 0,     /* float  [P] */
+    GSR_GEOM_MEANS2D,        /* float2 [P]  pixel-space centre */
+    GSR_GEOM_SPLATS,         /* float4 [P][3] {x,y,conic.x,conic.y},{conic.z,opacity,r,g},{b,ext_x,ext_y,0} */
+    GSR_GEOM_CLAMPED,        /* uint8  [P]  bit c set = channel c clamped in SH->RGB */
+    GSR_GEOM_TILES_TOUCHED,  /* uint32 [P] */
+    GSR_GEOM_POINT_OFFSETS,  /* uint32 [P]  inclusive scan of tiles_touched */
+    GSR_GEOM_RANGES,         /* uint2  [T]  [start,end) of each tile in point_list */
+    GSR_GEOM_CTRL,           /* uint32 [16] num_rendered, status flags, max tile length */
+    GSR_GEOM_NFIELDS
+};
+enum gsr_binning_field {
+    GSR_BIN_KEYS = 0,        /* uint64 [I]  per-tile bucketed (depth_bits<<32 | id), sorted in place */
+    GSR_BIN_POINT_LIST,      /* uint32 [I]  Gaussian ids in (tile, depth, id) order */
+    GSR_BIN_NFIELDS
+};
+enum gsr_img_field {
+    GSR_IMG_FINAL_T = 0,     /* float  [H*W] */
+    GSR_IMG_N_CONTRIB,       /* uint32 [H*W] */
+    GSR_IMG_TILE_MAX_CONTRIB,/* uint32 [T]  max n_contrib over the tile's pixels */
+    GSR_IMG_NFIELDS
+};
+int gsr_geom_layout(int32_t P, int32_t W, int32_t H, size_t *offsets, int cap);
+int gsr_binning_layout(int64_t num_rendered, int32_t W, int32_t H, size_t *offsets, int cap);
+int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap);
+
+const char *gsr_last_error(void);
+int gsr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H */
