@@ -10,6 +10,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "gsr_kernels.hpp"
 
@@ -33,6 +35,42 @@ int fail(int code, const char *fmt, ...) {
 int check_hip(hipError_t e, const char *what) {
     if (e != hipSuccess) return fail(GSR_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
     return GSR_OK;
+}
+
+// Optional per-stage timing with HIP events recorded on the launch stream
+// (bench.py reads it to price the dominant kernel against the HBM roofline).
+struct StageTimer {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+    std::vector<int> stage;  // stage of each used pair
+    size_t used = 0;
+    double total_ms[GSR_STAGE_COUNT] = {};
+    int64_t launches[GSR_STAGE_COUNT] = {};
+};
+StageTimer g_timer;  // the ABI is driven from one host thread per process
+
+const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess", "scan",       "tile_count",    "tile_scatter",
+                                            "tile_sort",  "render_fwd", "render_bwd",    "preprocess_bwd"};
+
+template <typename F>
+hipError_t timed(int st, hipStream_t s, F &&launch) {
+    if (!g_timer.on) return launch();
+    if (g_timer.used == g_timer.pool.size()) {
+        hipEvent_t a, b;
+        hipError_t e = hipEventCreate(&a);
+        if (e == hipSuccess) e = hipEventCreate(&b);
+        if (e != hipSuccess) return e;
+        g_timer.pool.emplace_back(a, b);
+        g_timer.stage.push_back(st);
+    }
+    auto &ev = g_timer.pool[g_timer.used];
+    g_timer.stage[g_timer.used] = st;
+    g_timer.used++;
+    hipError_t e = hipEventRecord(ev.first, s);
+    if (e != hipSuccess) return e;
+    e = launch();
+    if (e != hipSuccess) return e;
+    return hipEventRecord(ev.second, s);
 }
 
 // upstream debug mode: synchronise and check after every kernel
@@ -109,9 +147,9 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (!geom || !radii) return fail(GSR_ERR_ARGS, "geom/radii buffers are NULL");
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
-    if (int rc = step(launch_preprocess(*in, geom, radii, s), "preprocess", dbg, s)) return rc;
-    if (int rc = step(launch_scan(in->P, geom, in->W, in->H, s), "inclusive scan", dbg, s)) return rc;
-    if (int rc = step(launch_bin_count(in->P, in->W, in->H, geom, radii, s), "tile count", dbg, s)) return rc;
+    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, s); }), "preprocess", dbg, s)) return rc;
+    if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_scan(in->P, geom, in->W, in->H, s); }), "inclusive scan", dbg, s)) return rc;
+    if (int rc = step(timed(GSR_STAGE_TILE_COUNT, s, [&] { return launch_bin_count(in->P, in->W, in->H, geom, radii, s); }), "tile count", dbg, s)) return rc;
     if (!g_pinned) {
         if (int rc = check_hip(hipHostMalloc((void **)&g_pinned, CTRL_WORDS * 4, hipHostMallocDefault), "hipHostMalloc"))
             return rc;
@@ -144,14 +182,14 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
         return check_hip(hipMemsetAsync(out_color, 0, (size_t)3 * in->W * in->H * sizeof(float), s), "memset");
     if (!geom || !img || (num_rendered > 0 && !binning)) return fail(GSR_ERR_ARGS, "scratch buffers are NULL");
     if (num_rendered > 0) {
-        if (int rc = step(launch_bin_scatter(in->P, in->W, in->H, geom, radii, binning, num_rendered, s),
+        if (int rc = step(timed(GSR_STAGE_TILE_SCATTER, s, [&] { return launch_bin_scatter(in->P, in->W, in->H, geom, radii, binning, num_rendered, s); }),
                           "duplicateWithKeys (tile scatter)", dbg, s))
             return rc;
-        if (int rc = step(launch_tile_sort(in->P, in->W, in->H, geom, binning, num_rendered, max_tile_len, s),
+        if (int rc = step(timed(GSR_STAGE_TILE_SORT, s, [&] { return launch_tile_sort(in->P, in->W, in->H, geom, binning, num_rendered, max_tile_len, s); }),
                           "per-tile sort", dbg, s))
             return rc;
     }
-    return step(launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s), "render", dbg, s);
+    return step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s); }), "render", dbg, s);
 }
 
 int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning, const void *img,
@@ -171,12 +209,12 @@ int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, c
     float *acc = (float *)accum;
     if (int rc = check_hip(hipMemsetAsync(acc, 0, gsr_accum_bytes(in->P), s), "accumulator memset")) return rc;
     if (num_rendered > 0) {
-        if (int rc = step(launch_render_bwd(*in, geom, binning, num_rendered, img, dL_dout_color, acc, s),
+        if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, num_rendered, img, dL_dout_color, acc, s); }),
                           "render backward", dbg, s))
             return rc;
     }
     BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot};
-    return step(launch_preprocess_bwd(*in, radii, geom, acc, o, s), "preprocess backward", dbg, s);
+    return step(timed(GSR_STAGE_PREPROCESS_BWD, s, [&] { return launch_preprocess_bwd(*in, radii, geom, acc, o, s); }), "preprocess backward", dbg, s);
 }
 
 int gsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,
@@ -188,5 +226,35 @@ int gsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, c
     hipStream_t s = (hipStream_t)stream;
     return check_hip(launch_mark_visible(P, means3D, viewmatrix, present, s), "mark_visible");
 }
+
+int gsr_timing_enable(int on) {
+    g_timer.on = on != 0;
+    g_timer.used = 0;
+    for (int k = 0; k < GSR_STAGE_COUNT; k++) {
+        g_timer.total_ms[k] = 0;
+        g_timer.launches[k] = 0;
+    }
+    return GSR_OK;
+}
+
+int gsr_timing_read(double *total_ms, int64_t *launches, int cap) {
+    for (size_t i = 0; i < g_timer.used; i++) {
+        auto &ev = g_timer.pool[i];
+        if (int rc = check_hip(hipEventSynchronize(ev.second), "timing event")) return -rc;
+        float ms = 0.f;
+        if (int rc = check_hip(hipEventElapsedTime(&ms, ev.first, ev.second), "timing event")) return -rc;
+        g_timer.total_ms[g_timer.stage[i]] += ms;
+        g_timer.launches[g_timer.stage[i]] += 1;
+    }
+    g_timer.used = 0;
+    int n = 0;
+    for (; n < cap && n < GSR_STAGE_COUNT; n++) {
+        if (total_ms) total_ms[n] = g_timer.total_ms[n];
+        if (launches) launches[n] = g_timer.launches[n];
+    }
+    return n;
+}
+
+const char *gsr_stage_name(int stage) { return (stage >= 0 && stage < GSR_STAGE_COUNT) ? kStageNames[stage] : ""; }
 
 }  // extern "C"

@@ -49,6 +49,7 @@ EXPORTED = (
     "gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr_accum_bytes",
     "gsr_forward_preprocess", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
     "gsr_geom_layout", "gsr_binning_layout", "gsr_img_layout", "gsr_last_error", "gsr_abi_version",
+    "gsr_timing_enable", "gsr_timing_read", "gsr_stage_name",
 )
 ABI_VERSION = 1
 
@@ -93,6 +94,12 @@ def load_library():
     lib.gsr_geom_layout.argtypes = [i32, i32, i32, ctypes.POINTER(sz), ctypes.c_int]
     lib.gsr_binning_layout.argtypes = [i64, i32, i32, ctypes.POINTER(sz), ctypes.c_int]
     lib.gsr_img_layout.argtypes = [i32, i32, ctypes.POINTER(sz), ctypes.c_int]
+    lib.gsr_timing_enable.argtypes = [ctypes.c_int]
+    lib.gsr_timing_enable.restype = ctypes.c_int
+    lib.gsr_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    lib.gsr_timing_read.restype = ctypes.c_int
+    lib.gsr_stage_name.argtypes = [ctypes.c_int]
+    lib.gsr_stage_name.restype = ctypes.c_char_p
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_abi_version.restype = ctypes.c_int
     if lib.gsr_abi_version() != ABI_VERSION:
@@ -226,6 +233,22 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     p = _prep(projmatrix, "projmatrix", device)
     _check(lib.gsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(device)), "mark_visible")
     return present
+
+
+# ------------------------------------------------------------------ timing hooks
+def timing_enable(on: bool = True):
+    load_library().gsr_timing_enable(int(on))
+
+
+def timing_read() -> dict:
+    """{stage: (total_ms, launches)} accumulated since timing_enable (waits for events)."""
+    lib = load_library()
+    ms = (ctypes.c_double * 16)()
+    n_ = (ctypes.c_int64 * 16)()
+    n = lib.gsr_timing_read(ms, n_, 16)
+    if n < 0:
+        _check(-n, "gsr_timing_read")
+    return {lib.gsr_stage_name(i).decode(): (ms[i], n_[i]) for i in range(n)}
 
 
 # ------------------------------------------------------------------ test hooks

@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Headline benchmark: differentiable Gaussian rasterizer training iterations on MI355X.
+
+Metric (BASELINE.json): train iters/sec (fwd+bwd) + Mpix/sec at 1080p with 1M
+Gaussians, 1/2/4/8 GPUs.  One step = one view per GPU of the reference's training
+unit (train.py:98-105): render() through diff_gaussian_rasterization
+-> L1 loss against a target -> loss.backward() (all leaf gradients); with N > 1
+GPUs the views shard across ranks (view = rank) over replicated Gaussians and the
+leaf gradients are summed with one RCCL all-reduce per step (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  Besides the contract fields it carries
+  * roofline: the dominant stage's algorithmic bytes per launch ÷ its
+    average launch time, measured with HIP events on the launch stream inside the
+    timed region, against the 8 TB/s HBM peak; `traffic` = PMC-measured HBM bytes
+    per launch from profiles/pmc_summary.json when present (else null);
+  * cpu_baseline: the CPU oracle (oracle/, C port of the upstream algorithm)
+    timed on this host for one full view of the same workload (rank 0, N = 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "3dgs_study_amd"))
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+WORKLOADS = {
+    "C": "1M Gaussians, 1920x1080, SH deg 3, render->L1->backward, one view per GPU per step",
+    "B": "100k Gaussians, 800x800, SH deg 3, render->L1->backward, one view per GPU per step",
+    "A": "10k Gaussians, 256x256, SH deg 0, render->L1->backward, one view per GPU per step",
+}
+
+
+def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, M: int) -> float:
+    """Bytes a launch must move at minimum (SURVEY.md §8d per-unit figures)."""
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    HW = W * H
+    return {
+        "preprocess": P * (44 + 12 * M) + P * 75.0,          # means/scale/rot/opacity/SH in; geometry out
+        "scan": P * 8.0,
+        "tile_count": P * 12.0 + T * 8.0,
+        "tile_scatter": P * 20.0 + I * 12.0,                  # duplicateWithKeys: per-G read, per-instance key
+        "tile_sort": I * 24.0,                                # one read + one write of 12-B pairs
+        "render_fwd": I * 40.0 + T * 16.0 + HW * 20.0,
+        "render_bwd": I * 40.0 + HW * 20.0 + T * 8.0 + P * 44.0,
+        "preprocess_bwd": P * (92.0 + 147 + 24 * M),
+    }.get(stage, 0.0)
+
+
+def pmc_traffic(stage: str):
+    f = ROOT / "profiles" / "pmc_summary.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        v = d.get("stages", {}).get(stage, {}).get("hbm_bytes_per_launch")
+        return float(v) if v is not None else None
+    except Exception:
+        return None
+
+
+def cpu_baseline(P: int, W: int, H: int, deg: int, budget_s: float = 30.0) -> dict:
+    """Time the C oracle (single thread) on full views of the same workload."""
+    import numpy as np
+
+    import synthetic
+    from oracle import oracle
+
+    oracle.build()
+    cam = synthetic.make_camera(W, H, 0)
+    g = synthetic.make_gaussians(P, deg, seed=0)
+    target = synthetic.make_target(W, H).numpy()
+    args = (g.get_xyz.detach().numpy(), g.get_opacity.detach().numpy(), cam.world_view_transform.numpy(),
+            cam.full_proj_transform.numpy(), cam.camera_center.numpy(), np.zeros(3, np.float32), H, W,
+            np.tan(cam.FoVx / 2), np.tan(cam.FoVy / 2), 1.0, deg)
+    kw = dict(shs=g.get_features.detach().numpy(), scales=g.get_scaling.detach().numpy(),
+              rotations=g.get_rotation.detach().numpy())
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        f = oracle.forward(*args, **kw)
+        dL = (np.sign(f["color"] - target) / f["color"].size).astype(np.float32)  # L1 backward
+        oracle.backward(f, dL)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s / 2 or len(times) >= 3:
+            break
+    med = sorted(times)[len(times) // 2]
+    return {"value": 1.0 / med, "unit": "train-iters/s", "cores": 1, "kind": "port",
+            "sample": f"{len(times)} full view(s) of the same workload (P={P}, {W}x{H}, SH{deg}) through the C oracle "
+                      f"(forward + L1 grad + backward), single thread; median {med:.2f} s/view"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="C", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lambda-dssim", type=float, default=0.0,
+                    help="0 = L1-only headline unit; 0.2 = the reference's L1+SSIM loss")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import synthetic
+    import train_step
+    from diff_gaussian_rasterization import _C
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = synthetic.CONFIGS[args.config]
+    P, W, H, deg = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
+    M = (deg + 1) ** 2
+    cam = synthetic.make_camera(W, H, view=rank % 8).to(dev)
+    g = synthetic.make_gaussians(P, deg, seed=0).to(dev, requires_grad=True)
+    target = synthetic.make_target(W, H, seed=1).to(dev)
+    bg = torch.zeros(3, device=dev)
+    params = g.params()
+    nparam = sum(p.numel() for p in params)
+
+    def one_step():
+        for p in params:
+            p.grad = None
+        out = train_step.train_step(cam, g, target, bg, lambda_dssim=args.lambda_dssim)
+        if world > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            dist.all_reduce(flat)
+        return out
+
+    for _ in range(args.warmup):
+        out = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _C.timing_enable(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    stages = _C.timing_read()
+    _C.timing_enable(False)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    I = _last_num_rendered(cam, g, bg)  # measured instances of this rank's view (byte model)
+
+    if rank == 0:
+        steps = args.steps
+        value = world * steps / elapsed
+        per_stage = {k: (ms / n if n else 0.0, n) for k, (ms, n) in stages.items()}
+        dom = max(per_stage, key=lambda k: per_stage[k][0] * per_stage[k][1])
+        dom_ms = per_stage[dom][0]
+        ab = algorithmic_bytes(dom, P, I, W, H, M)
+        achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        traffic = pmc_traffic(dom)
+        line = {
+            "metric": "train iters/sec (fwd+bwd) + Mpix/sec, 1080p, 1M Gaussians @1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "train-iters/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded Gaussians in a radius-2 ball, camera at distance 6, SURVEY.md §8d)",
+            "config": {
+                "workload": f"{args.config}: {WORKLOADS[args.config]}",
+                "gaussians": P, "width": W, "height": H, "sh_degree": deg,
+                "num_rendered": I, "views_per_step": world,
+                "loss": "L1" if not args.lambda_dssim else f"L1+{args.lambda_dssim}*(1-SSIM)",
+                "parallelism": f"view-parallel x{world}" + (f", RCCL all-reduce {nparam * 4 / 1e6:.0f} MB/step"
+                                                            if world > 1 else ""),
+            },
+            "mpix_per_s": round(value * W * H / 1e6, 2),
+            "stages_ms": {k: round(v[0], 4) for k, v in per_stage.items()},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": ab,
+                "avg_launch_ms": round(dom_ms, 4),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(P, W, H, deg)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _last_num_rendered(cam, g, bg) -> int:
+    """num_rendered of the benchmarked view (forward only, outside the timed region)."""
+    import math
+
+    import torch
+    from diff_gaussian_rasterization import _C
+
+    with torch.no_grad():
+        res = _C.rasterize_gaussians(bg, g.get_xyz, torch.empty(0, device=bg.device), g.get_opacity, g.get_scaling,
+                                     g.get_rotation, 1.0, torch.empty(0, device=bg.device), cam.world_view_transform,
+                                     cam.full_proj_transform, math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5),
+                                     cam.image_height, cam.image_width, g.get_features, g.active_sh_degree,
+                                     cam.camera_center, False, False)
+    return int(res[0])
+
+
+if __name__ == "__main__":
+    main()

@@ -146,6 +146,26 @@ int gsr_geom_layout(int32_t P, int32_t W, int32_t H, size_t *offsets, int cap);
 int gsr_binning_layout(int64_t num_rendered, int32_t W, int32_t H, size_t *offsets, int cap);
 int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap);
 
+/* Per-stage device timing (HIP events on the launch stream), for benchmarks.
+ * gsr_timing_enable(1) resets the accumulators and starts recording;
+ * gsr_timing_read() waits for the recorded events and returns, per stage,
+ * the summed milliseconds and the launch count (returns the number of stages,
+ * negative on error).  A stage is one launch_* group of kernels. */
+enum gsr_stage {
+    GSR_STAGE_PREPROCESS = 0, /* FORWARD::preprocessCUDA */
+    GSR_STAGE_SCAN,           /* InclusiveSum of tiles_touched */
+    GSR_STAGE_TILE_COUNT,     /* per-tile counts + ranges (identifyTileRanges output) */
+    GSR_STAGE_TILE_SCATTER,   /* duplicateWithKeys into tile buckets */
+    GSR_STAGE_TILE_SORT,      /* per-tile depth sort (SortPairs) */
+    GSR_STAGE_RENDER_FWD,     /* FORWARD::renderCUDA */
+    GSR_STAGE_RENDER_BWD,     /* BACKWARD::renderCUDA */
+    GSR_STAGE_PREPROCESS_BWD, /* BACKWARD::computeCov2DCUDA + preprocessCUDA */
+    GSR_STAGE_COUNT
+};
+int gsr_timing_enable(int on);
+int gsr_timing_read(double *total_ms, int64_t *launches, int cap);
+const char *gsr_stage_name(int stage);
+
 const char *gsr_last_error(void);
 int gsr_abi_version(void);
 
