@@ -1,0 +1,132 @@
+"""The C ABI library loads without a GPU, exports every symbol include/gsr.h
+declares, and its host-side logic (argument validation, scratch layouts, error
+strings) behaves — no kernel is launched here."""
+import ctypes
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def header_functions():
+    text = (ROOT / "include" / "gsr.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gsr_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from diff_gaussian_rasterization import _C
+
+    return _C.load_library()
+
+
+def test_every_declared_symbol_is_exported(lib):
+    from diff_gaussian_rasterization import _C
+
+    names = header_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), f"libgsr.so lacks {n}"
+    assert sorted(_C.EXPORTED) == names
+
+
+def test_abi_version_and_struct_layout(lib):
+    from diff_gaussian_rasterization import _C
+
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 1
+    # 10 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
+    assert ctypes.sizeof(_C.GsrInputs) == 40 + 11 * 8
+    assert _C.GsrInputs.bg.offset == 40
+
+
+def test_scratch_layouts_are_aligned_and_disjoint(lib):
+    from diff_gaussian_rasterization import _C
+
+    for P, W, H, I in ((1, 16, 16, 1), (10_000, 256, 256, 18_267), (1_000_000, 1920, 1080, 8_023_099),
+                       (5_000_000, 3840, 2160, 110_000_000)):
+        g, b, im = _C.layouts(P, W, H, I)
+        for d in (g, b, im):
+            offs = list(d.values())
+            assert all(o % 256 == 0 for o in offs)
+            assert offs == sorted(offs) and len(set(offs)) == len(offs)
+        assert lib.gsr_geom_bytes(P, W, H) > g["ctrl"]
+        assert lib.gsr_binning_bytes(I, W, H) >= I * 12
+        assert lib.gsr_img_bytes(W, H) >= W * H * 8
+        assert lib.gsr_accum_bytes(P) == P * 64
+        # per-Gaussian sub-arrays hold P entries each
+        assert g["means2D"] - g["depths"] >= 4 * P
+        assert g["splats"] - g["means2D"] >= 8 * P
+
+
+def _inputs(**kw):
+    from diff_gaussian_rasterization import _C
+
+    base = dict(P=4, D=0, M=1, W=16, H=16, tan_fovx=0.5, tan_fovy=0.5, scale_modifier=1.0, prefiltered=0, debug=0,
+                bg=1, means3D=1, opacities=1, viewmatrix=1, projmatrix=1, campos=1, sh=1, scales=1, rotations=1)
+    base.update(kw)
+    return _C.GsrInputs(**base)
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(colors_precomp=1), "excatly one of either SHs or precomputed colors"),
+    (dict(sh=None), "excatly one of either SHs or precomputed colors"),
+    (dict(cov3D_precomp=1), "exactly one of either scale/rotation pair or precomputed 3D covariance"),
+    (dict(scales=None), "exactly one of either scale/rotation pair or precomputed 3D covariance"),
+    (dict(D=3, M=4), "degree 3 needs 16"),
+    (dict(D=4, M=25), "sh_degree must be in [0, 3]"),
+    (dict(P=-1), "num_points, 3"),
+    (dict(W=0), "image size"),
+])
+def test_argument_validation_mirrors_upstream_errors(lib, kw, msg):
+    s = _inputs(**kw)
+    n = ctypes.c_int64(-1)
+    rc = lib.gsr_forward_preprocess(ctypes.byref(s), None, None, ctypes.byref(n), None, None)
+    assert rc != 0
+    assert msg in lib.gsr_last_error().decode()
+
+
+def test_zero_gaussians_is_a_host_side_no_op(lib):
+    s = _inputs(P=0)
+    n = ctypes.c_int64(-1)
+    mt = ctypes.c_uint32(7)
+    assert lib.gsr_forward_preprocess(ctypes.byref(s), None, None, ctypes.byref(n), ctypes.byref(mt), None) == 0
+    assert n.value == 0 and mt.value == 0
+    assert lib.gsr_backward(ctypes.byref(s), None, None, None, None, 0, *([None] * 11)) == 0
+    assert lib.gsr_mark_visible(0, None, None, None, None, None) == 0
+
+
+def test_stage_names(lib):
+    from diff_gaussian_rasterization import _C
+
+    names = [lib.gsr_stage_name(i).decode() for i in range(8)]
+    assert names == ["preprocess", "scan", "tile_count", "tile_scatter", "tile_sort", "render_fwd", "render_bwd",
+                     "preprocess_bwd"]
+    assert lib.gsr_stage_name(99).decode() == ""
+    _C.timing_enable(True)
+    assert _C.timing_read() == {n: (0.0, 0) for n in names}
+    _C.timing_enable(False)
+
+
+def test_cpu_tensors_are_rejected_loudly():
+    import torch
+    from diff_gaussian_rasterization import _C
+
+    with pytest.raises(RuntimeError, match="no CPU implementation"):
+        _C.rasterize_gaussians(torch.zeros(3), torch.zeros(2, 3), torch.empty(0), torch.ones(2, 1), torch.ones(2, 3),
+                               torch.ones(2, 4), 1.0, torch.empty(0), torch.eye(4), torch.eye(4), 0.5, 0.5, 8, 8,
+                               torch.zeros(2, 1, 3), 0, torch.zeros(3), False, False)
+    with pytest.raises(RuntimeError, match="num_points, 3"):
+        _C.rasterize_gaussians(torch.zeros(3), torch.zeros(2, 4), torch.empty(0), torch.ones(2, 1), torch.ones(2, 3),
+                               torch.ones(2, 4), 1.0, torch.empty(0), torch.eye(4), torch.eye(4), 0.5, 0.5, 8, 8,
+                               torch.zeros(2, 1, 3), 0, torch.zeros(3), False, False)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from diff_gaussian_rasterization import _C
+
+    monkeypatch.setattr(_C, "_lib", None)
+    monkeypatch.setenv("GSR_LIBRARY", str(tmp_path / "nope.so"))
+    with pytest.raises(ImportError, match="not found"):
+        _C.load_library()
