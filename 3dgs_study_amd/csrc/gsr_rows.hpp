@@ -1,0 +1,73 @@
+// gsr_rows.hpp — coalesced staging of per-Gaussian rows through LDS.
+//
+// The SH block of a Gaussian is a 12·M-byte row (192 B at SH degree 3).  A
+// thread-per-Gaussian kernel that reads its own row directly issues 48 dword
+// loads per lane whose 64 addresses sit 192 B apart: every wave-instruction
+// touches 64 cache lines.  Instead the workgroup streams its contiguous slice
+// of rows with 16-byte-per-lane loads into LDS rows padded to an odd number
+// of dwords (bank-conflict-free per-lane row reads), and writes gradients back
+// the same way.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsr {
+
+// row r, column c of a [rows][RW] block -> padded LDS index
+__device__ __forceinline__ int lds_row_index(int e, int RW, float invRW) {
+    int r = (int)((float)e * invRW);
+    r += ((r + 1) * RW <= e) ? 1 : 0;
+    r -= (r * RW > e) ? 1 : 0;
+    return r * (RW + 1) + (e - r * RW);
+}
+
+// Copy rows [g0, g0 + n) of a row-major float [*, RW] array into LDS rows of
+// stride RW + 1.  All threads of the workgroup must call it.
+template <int THREADS>
+__device__ inline void rows_to_lds(const float *__restrict__ src, int g0, int n, int RW, float *lds) {
+    const int total = n * RW;
+    const float invRW = 1.0f / (float)RW;
+    const float *base = src + (size_t)g0 * RW;
+    if ((((uintptr_t)base) & 15u) == 0) {
+        const float4 *b4 = reinterpret_cast<const float4 *>(base);
+        const int n4 = total >> 2;
+        for (int i = threadIdx.x; i < n4; i += THREADS) {
+            const float4 v = b4[i];
+            const int e = i << 2;
+            lds[lds_row_index(e, RW, invRW)] = v.x;
+            lds[lds_row_index(e + 1, RW, invRW)] = v.y;
+            lds[lds_row_index(e + 2, RW, invRW)] = v.z;
+            lds[lds_row_index(e + 3, RW, invRW)] = v.w;
+        }
+        for (int e = (n4 << 2) + threadIdx.x; e < total; e += THREADS) lds[lds_row_index(e, RW, invRW)] = base[e];
+    } else {
+        for (int e = threadIdx.x; e < total; e += THREADS) lds[lds_row_index(e, RW, invRW)] = base[e];
+    }
+}
+
+// The reverse: LDS rows (stride RW + 1) -> global rows [g0, g0 + n).
+template <int THREADS>
+__device__ inline void lds_to_rows(const float *lds, int g0, int n, int RW, float *__restrict__ dst) {
+    const int total = n * RW;
+    const float invRW = 1.0f / (float)RW;
+    float *base = dst + (size_t)g0 * RW;
+    if ((((uintptr_t)base) & 15u) == 0) {
+        float4 *b4 = reinterpret_cast<float4 *>(base);
+        const int n4 = total >> 2;
+        for (int i = threadIdx.x; i < n4; i += THREADS) {
+            const int e = i << 2;
+            float4 v;
+            v.x = lds[lds_row_index(e, RW, invRW)];
+            v.y = lds[lds_row_index(e + 1, RW, invRW)];
+            v.z = lds[lds_row_index(e + 2, RW, invRW)];
+            v.w = lds[lds_row_index(e + 3, RW, invRW)];
+            b4[i] = v;
+        }
+        for (int e = (n4 << 2) + threadIdx.x; e < total; e += THREADS) base[e] = lds[lds_row_index(e, RW, invRW)];
+    } else {
+        for (int e = threadIdx.x; e < total; e += THREADS) base[e] = lds[lds_row_index(e, RW, invRW)];
+    }
+}
+
+}  // namespace gsr

@@ -12,6 +12,7 @@
 
 #include "gsr_kernels.hpp"
 #include "gsr_math.hpp"
+#include "gsr_rows.hpp"
 #include "gsr_wave.hpp"
 
 namespace gsr {
@@ -59,8 +60,16 @@ __device__ inline float sh_channel(const float *sh, int c, int deg, float x, flo
 
 __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) {
     __shared__ uint32_t wsum[PRE_THREADS / 64];
+    extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
     const gsr_inputs &in = a.in;
-    const int idx = blockIdx.x * PRE_THREADS + threadIdx.x;
+    const int g0 = blockIdx.x * PRE_THREADS;
+    const int idx = g0 + threadIdx.x;
+    const int RW = 3 * in.M;
+    const bool use_sh = in.sh != nullptr && in.colors_precomp == nullptr;
+    if (use_sh) {
+        rows_to_lds<PRE_THREADS>(in.sh, g0, min(PRE_THREADS, in.P - g0), RW, sh_lds);
+        __syncthreads();
+    }
     uint32_t touched = 0;
     if (idx < in.P) {
         int radius_out = 0;
@@ -116,7 +125,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                     const float dx = p.x - in.campos[0], dy = p.y - in.campos[1], dz = p.z - in.campos[2];
                     const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
                     const float x = dx / len, y = dy / len, z = dz / len;
-                    const float *sh = in.sh + (size_t)idx * in.M * 3;
+                    const float *sh = sh_lds + threadIdx.x * (RW + 1);
 #pragma unroll
                     for (int c = 0; c < 3; c++) {
                         const float v = sh_channel(sh, c, in.D, x, y, z);
@@ -214,7 +223,8 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, h
     hipError_t e = hipMemsetAsync(a.ctrl, 0, CTRL_WORDS * 4, s);
     if (e != hipSuccess) return e;
     const int nb = pre_blocks(in.P);
-    hipLaunchKernelGGL(preprocess_fwd_kernel, dim3(nb), dim3(PRE_THREADS), 0, s, a);
+    const size_t lds = (in.sh && !in.colors_precomp) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
+    hipLaunchKernelGGL(preprocess_fwd_kernel, dim3(nb), dim3(PRE_THREADS), lds, s, a);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 
 #include "gsr_kernels.hpp"
 #include "gsr_math.hpp"
+#include "gsr_rows.hpp"
 
 namespace gsr {
 
@@ -23,6 +24,8 @@ struct PreBwdArgs {
     BwdOutputs o;
 };
 
+// backward.cu computeColorFromSH (backward).  `sh` and `dsh` may alias (the
+// same LDS row): every SH coefficient is read before any gradient is written.
 __device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, float ox, float oy, float oz,
                                    const float dRGB[3], f3 &dmean) {
     const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
@@ -33,34 +36,17 @@ __device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, 
 #pragma unroll
     for (int c = 0; c < 3; c++) {
 #define SH(k) sh[3 * (k) + c]
-        const float d = dRGB[c];
-        dsh[c] = SH_C0 * d;
         if (deg > 0) {
-            dsh[3 * 1 + c] = (-SH_C1 * y) * d;
-            dsh[3 * 2 + c] = (SH_C1 * z) * d;
-            dsh[3 * 3 + c] = (-SH_C1 * x) * d;
             dRGBdx[c] = -SH_C1 * SH(3);
             dRGBdy[c] = -SH_C1 * SH(1);
             dRGBdz[c] = SH_C1 * SH(2);
             if (deg > 1) {
-                dsh[3 * 4 + c] = (SH_C2_0 * xy) * d;
-                dsh[3 * 5 + c] = (SH_C2_1 * yz) * d;
-                dsh[3 * 6 + c] = (SH_C2_2 * (2.f * zz - xx - yy)) * d;
-                dsh[3 * 7 + c] = (SH_C2_3 * xz) * d;
-                dsh[3 * 8 + c] = (SH_C2_4 * (xx - yy)) * d;
                 dRGBdx[c] += SH_C2_0 * y * SH(4) + SH_C2_2 * 2.f * -x * SH(6) + SH_C2_3 * z * SH(7) +
                              SH_C2_4 * 2.f * x * SH(8);
                 dRGBdy[c] += SH_C2_0 * x * SH(4) + SH_C2_1 * z * SH(5) + SH_C2_2 * 2.f * -y * SH(6) +
                              SH_C2_4 * 2.f * -y * SH(8);
                 dRGBdz[c] += SH_C2_1 * y * SH(5) + SH_C2_2 * 2.f * 2.f * z * SH(6) + SH_C2_3 * x * SH(7);
                 if (deg > 2) {
-                    dsh[3 * 9 + c] = (SH_C3_0 * y * (3.f * xx - yy)) * d;
-                    dsh[3 * 10 + c] = (SH_C3_1 * xy * z) * d;
-                    dsh[3 * 11 + c] = (SH_C3_2 * y * (4.f * zz - xx - yy)) * d;
-                    dsh[3 * 12 + c] = (SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy)) * d;
-                    dsh[3 * 13 + c] = (SH_C3_4 * x * (4.f * zz - xx - yy)) * d;
-                    dsh[3 * 14 + c] = (SH_C3_5 * z * (xx - yy)) * d;
-                    dsh[3 * 15 + c] = (SH_C3_6 * x * (xx - 3.f * yy)) * d;
                     dRGBdx[c] += (SH_C3_0 * SH(9) * 3.f * 2.f * xy + SH_C3_1 * SH(10) * yz +
                                   SH_C3_2 * SH(11) * -2.f * xy + SH_C3_3 * SH(12) * -3.f * 2.f * xz +
                                   SH_C3_4 * SH(13) * (-3.f * xx + 4.f * zz - yy) + SH_C3_5 * SH(14) * 2.f * xz +
@@ -76,6 +62,32 @@ __device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, 
             }
         }
 #undef SH
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const float d = dRGB[c];
+        dsh[c] = SH_C0 * d;
+        if (deg > 0) {
+            dsh[3 * 1 + c] = (-SH_C1 * y) * d;
+            dsh[3 * 2 + c] = (SH_C1 * z) * d;
+            dsh[3 * 3 + c] = (-SH_C1 * x) * d;
+            if (deg > 1) {
+                dsh[3 * 4 + c] = (SH_C2_0 * xy) * d;
+                dsh[3 * 5 + c] = (SH_C2_1 * yz) * d;
+                dsh[3 * 6 + c] = (SH_C2_2 * (2.f * zz - xx - yy)) * d;
+                dsh[3 * 7 + c] = (SH_C2_3 * xz) * d;
+                dsh[3 * 8 + c] = (SH_C2_4 * (xx - yy)) * d;
+                if (deg > 2) {
+                    dsh[3 * 9 + c] = (SH_C3_0 * y * (3.f * xx - yy)) * d;
+                    dsh[3 * 10 + c] = (SH_C3_1 * xy * z) * d;
+                    dsh[3 * 11 + c] = (SH_C3_2 * y * (4.f * zz - xx - yy)) * d;
+                    dsh[3 * 12 + c] = (SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy)) * d;
+                    dsh[3 * 13 + c] = (SH_C3_4 * x * (4.f * zz - xx - yy)) * d;
+                    dsh[3 * 14 + c] = (SH_C3_5 * z * (xx - yy)) * d;
+                    dsh[3 * 15 + c] = (SH_C3_6 * x * (xx - 3.f * yy)) * d;
+                }
+            }
+        }
     }
     for (int k = ncoef; k < M; k++) {
         dsh[3 * k + 0] = 0.f;
@@ -93,13 +105,39 @@ __device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, 
     dmean.z += (-ox * oz * ddx - oy * oz * ddy + (sum2 - oz * oz) * ddz) * invsum32;
 }
 
-__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreBwdArgs a) {
+constexpr int PB_THREADS = 256;
+
+__device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh_row, float *dsh_row);
+
+// One workgroup = PB_THREADS consecutive Gaussians.  SH rows are staged in LDS
+// (coalesced 16-B loads), each thread overwrites its row with dL/dSH, and the
+// rows are streamed back out coalesced.
+__global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PB_THREADS][3M + 1]
     const gsr_inputs &in = a.in;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= in.P) return;
+    const int g0 = blockIdx.x * PB_THREADS;
+    const int n = min(PB_THREADS, in.P - g0);
+    const int RW = 3 * in.M;
+    const bool stage = in.sh != nullptr && a.o.dsh != nullptr && in.M > 0;
+    if (stage) {
+        rows_to_lds<PB_THREADS>(in.sh, g0, n, RW, sh_lds);
+        __syncthreads();
+    }
+    if ((int)threadIdx.x < n) {
+        float *row = stage ? sh_lds + threadIdx.x * (RW + 1) : nullptr;
+        preprocess_bwd_one(a, g0 + threadIdx.x, row, row);
+    }
+    if (stage) {
+        __syncthreads();
+        lds_to_rows<PB_THREADS>(sh_lds, g0, n, RW, a.o.dsh);
+    }
+}
+
+__device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh_row, float *dsh_row) {
+    const gsr_inputs &in = a.in;
     const BwdOutputs &o = a.o;
     const bool vis = a.radii[idx] > 0;
-    float *dsh = (o.dsh && in.M > 0) ? o.dsh + (size_t)idx * in.M * 3 : nullptr;
+    float *dsh = dsh_row;  // LDS row (streamed to o.dsh by the caller) or nullptr
     if (!vis) {
         for (int k = 0; k < 3; k++) {
             o.dmeans2D[3 * (size_t)idx + k] = 0.f;
@@ -225,8 +263,8 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreBwdArgs a) {
         const uint8_t cl = a.clamped[idx];
         const float dRGB[3] = {dcol[0] * ((cl & 1) ? 0.f : 1.f), dcol[1] * ((cl & 2) ? 0.f : 1.f),
                                dcol[2] * ((cl & 4) ? 0.f : 1.f)};
-        sh_backward(in.sh + (size_t)idx * in.M * 3, dsh, in.D, in.M, mean.x - in.campos[0], mean.y - in.campos[1],
-                    mean.z - in.campos[2], dRGB, dmean);
+        sh_backward(sh_row, dsh, in.D, in.M, mean.x - in.campos[0], mean.y - in.campos[1], mean.z - in.campos[2],
+                    dRGB, dmean);
     }
     o.dmeans3D[3 * (size_t)idx + 0] = dmean.x;
     o.dmeans3D[3 * (size_t)idx + 1] = dmean.y;
@@ -284,7 +322,9 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     a.clamped = at<uint8_t>(geom, G.off[GSR_GEOM_CLAMPED]);
     a.accum = accum;
     a.o = o;
-    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, a);
+    const bool stage = in.sh && o.dsh && in.M > 0;
+    const size_t lds = stage ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
+    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + PB_THREADS - 1) / PB_THREADS), dim3(PB_THREADS), lds, s, a);
     return hipGetLastError();
 }
 
