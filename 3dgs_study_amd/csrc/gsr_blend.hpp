@@ -1,0 +1,60 @@
+// gsr_blend.hpp — pieces shared by the forward and backward blend kernels.
+//
+// Work unit: one wave64 = one 8x8 pixel quadrant of a 16x16 tile (lane l ->
+// pixel (l & 7, l >> 3)).  A wave streams the tile's depth-sorted list in
+// chunks of 64 entries, one entry per lane: the lane gathers the entry's 48-B
+// splat record, tests in parallel whether the Gaussian can reach ANY pixel of
+// the quadrant, and a ballot turns the chunk into a bit mask.  The wave then
+// walks only the set bits; each Gaussian's parameters are broadcast from the
+// owning lane with v_readlane into SGPRs, so the per-pixel math reads scalar
+// operands and no LDS or workgroup barrier is involved.
+#pragma once
+
+#include "gsr_common.hpp"
+#include "gsr_wave.hpp"
+
+namespace gsr {
+
+constexpr int BLEND_THREADS = 256;  // 4 waves = the 4 quadrants of one tile
+
+// Exact cull: min over the quadrant's pixel centres [x0, x0+7] x [y0, y0+7] of
+// q(d) = ca dx^2 + 2 cb dx dy + cc dy^2 (d = pixel - mean) against qmax.  The
+// forward/backward reject a pixel when o*exp(-q/2) < 1/255, i.e. q > 2 ln(255 o);
+// qmax is that bound widened in preprocess, so a skipped Gaussian is one that
+// every pixel of the quadrant would have skipped.  A NaN bound keeps the entry.
+__device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb, float cc, float qmax, float x0,
+                                         float y0) {
+    const float dx0 = x0 - mx, dx1 = x0 + 7.0f - mx;
+    const float dy0 = y0 - my, dy1 = y0 + 7.0f - my;
+    if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return true;  // mean inside: q_min = 0
+    // convex q: with the minimum outside the box, the box minimum lies on an edge
+    const float icc = 1.0f / cc, ica = 1.0f / ca;
+    float q = INFINITY;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const float dx = e ? dx1 : dx0;
+        const float dy = fminf(fmaxf(-cb * dx * icc, dy0), dy1);
+        q = fminf(q, ca * dx * dx + 2.0f * cb * dx * dy + cc * dy * dy);
+        const float ey = e ? dy1 : dy0;
+        const float ex = fminf(fmaxf(-cb * ey * ica, dx0), dx1);
+        q = fminf(q, ca * ex * ex + 2.0f * cb * ex * ey + cc * ey * ey);
+    }
+    return !(q > qmax);
+}
+
+__device__ __forceinline__ float bcast(float v, int k) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
+}
+__device__ __forceinline__ uint32_t bcast_u(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+
+// blockIdx -> tile: consecutive tiles (which share most Gaussians) go to
+// workgroups with the same blockIdx % 8, i.e. to one XCD and its L2 under the
+// round-robin dispatch (placement is a speed hint only, never relied upon).
+__device__ __forceinline__ int xcd_tile(int b, int tiles) {
+    const int per = (tiles + 7) >> 3;
+    const int t = (b & 7) * per + (b >> 3);
+    return t < tiles ? t : -1;
+}
+__host__ __device__ inline int xcd_grid(int tiles) { return ((tiles + 7) >> 3) * 8; }
+
+}  // namespace gsr

@@ -133,23 +133,17 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                         rgb[c] = fmaxf(v, 0.0f);
                     }
                 }
-                // Conservative box of the alpha >= 1/255 region: power >= -ln(255 o)
-                // <=> d^T Sigma^-1 d <= 2 ln(255 o); half-extents sqrt(2 ln(255 o) Sigma_ii),
-                // widened for rounding.  Used only to skip work that the blend
-                // would reject anyway (alpha < 1/255), never to change a result.
+                // Cull bound for the blend kernels: alpha = o*exp(-q/2) >= 1/255 needs
+                // q = d^T conic d <= 2 ln(255 o).  Stored widened (0.1% + 0.002) so a
+                // wave may skip a Gaussian only when every pixel would reject it.
                 const float opac = in.opacities[idx];
-                const float lnr = logf(255.0f * opac) + 1e-3f;  // 0.1% slack on the threshold
-                float ex = -1.0f, ey = -1.0f;
-                if (lnr > 0.0f) {
-                    ex = sqrtf(2.0f * lnr * cov.x) * 1.01f + 0.5f;
-                    ey = sqrtf(2.0f * lnr * cov.z) * 1.01f + 0.5f;
-                }
+                const float qmax = 2.0f * logf(255.0f * opac) * 1.001f + 0.002f;
                 a.depths[idx] = p_view.z;
                 a.means2D[idx] = make_float2(px, py);
                 float4 *sp = a.splats + 3 * (size_t)idx;
                 sp[0] = make_float4(px, py, conic_x, conic_y);
                 sp[1] = make_float4(conic_z, opac, rgb[0], rgb[1]);
-                sp[2] = make_float4(rgb[2], ex, ey, 0.0f);
+                sp[2] = make_float4(rgb[2], qmax, 0.0f, 0.0f);
                 a.clamped[idx] = clampbits;
                 radius_out = r;
                 touched = area;

@@ -6,52 +6,65 @@
 // n_contrib, recompute alpha, divide T by (1 - alpha), keep accum_rec /
 // last_alpha / last_color, and produce 9 partial gradients per (pixel, Gaussian).
 //
-// CDNA4 mapping:
-//  * the walk starts at the tile's max n_contrib (written by the forward), not
-//    at the end of the list: entries past it are skipped by every pixel anyway;
-//  * 8x8 quadrant per wave + the conservative alpha box give a wave-uniform
-//    skip (all pixels of the quadrant would `continue` on alpha < 1/255);
-//  * upstream issues ~9 float atomics per contributing (pixel, Gaussian) pair.
-//    Here the 9 partials are summed over the wave's 64 pixels with DPP row
-//    reductions (no LDS), and ONE wave-instruction of 9 lanes adds the sums to
-//    the Gaussian's 64-byte accumulator row: one memory-side atomic request per
-//    (wave, Gaussian) instead of up to 576.
+// CDNA4 mapping (gsr_blend.hpp): one independent wave64 per 8x8 quadrant.  The
+// wave starts at the largest n_contrib among its own 64 pixels (entries past it
+// are skipped by every pixel), streams 64-entry chunks backwards with the same
+// lane-parallel exact cull as the forward, and walks the surviving Gaussians
+// from the back.  Upstream issues ~9 float atomics per contributing
+// (pixel, Gaussian) pair; here the 9 partials are summed over the wave's 64
+// pixels by a reduce-scatter (v_permlane32_swap, v_permlane16_swap, then DPP row
+// shifts: 28 VALU for all nine sums instead of 63) and ONE 9-lane atomic
+// wave-instruction adds them to the Gaussian's 64-byte accumulator row.
+#include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
-#include "gsr_wave.hpp"
 
 namespace gsr {
 
-constexpr int RB_THREADS = 256;
-constexpr int RB_BATCH = 256;
-
 struct RenderBwdArgs {
-    int W, H, gx;
+    int W, H, gx, tiles;
     const uint2 *ranges;
     const uint32_t *point_list;
     const float4 *splats;
     const float *bg;
     const float *final_T;
     const uint32_t *n_contrib;
-    const uint32_t *tile_maxc;
     const float *dL_dpix;
     float *accum;
 };
 
-__global__ void __launch_bounds__(RB_THREADS) render_bwd_kernel(RenderBwdArgs a) {
-    __shared__ float4 sA[RB_BATCH];
-    __shared__ float4 sB[RB_BATCH];
-    __shared__ float4 sC[RB_BATCH];
-    __shared__ uint32_t sId[RB_BATCH];
-    const int tile = blockIdx.x;
+// NB: copy the builtin's pair into scalars before bit-casting: with ROCm 7.2's
+// clang, __builtin_bit_cast(float, r[1]) on the returned vector silently reads
+// element 0 (caught by tests/test_gpu_parity.py; see tests/hip/permlane_probe.hip).
+__device__ __forceinline__ float swap32_sum(float a, float b) {  // -> [a_lo + a_hi | b_lo + b_hi]
+    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                                                    false, false);
+    const uint32_t x = r[0], y = r[1];
+    return __builtin_bit_cast(float, x) + __builtin_bit_cast(float, y);
+}
+__device__ __forceinline__ float swap16_sum(float a, float b) {  // rows: [a0+a1 | b0+b1 | a2+a3 | b2+b3]
+    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                                                    false, false);
+    const uint32_t x = r[0], y = r[1];
+    return __builtin_bit_cast(float, x) + __builtin_bit_cast(float, y);
+}
+__device__ __forceinline__ float row_sum_to_lane15(float v) {  // sum of each 16-lane row lands in its lane 15
+    v += dpp_f32<DPP_ROW_SHR1>(v);
+    v += dpp_f32<DPP_ROW_SHR2>(v);
+    v += dpp_f32<DPP_ROW_SHR4, 0xf, 0xe>(v);
+    v += dpp_f32<DPP_ROW_SHR8, 0xf, 0xc>(v);
+    return v;
+}
+
+__global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs a) {
+    const int tile = xcd_tile(blockIdx.x, a.tiles);
+    if (tile < 0) return;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float fx = (float)px, fy = (float)py;
-    const float qxlo = (float)qx0, qxhi = (float)(qx0 + 7), qylo = (float)qy0, qyhi = (float)(qy0 + 7);
     const uint2 r = a.ranges[tile];
-    const int maxc = (int)a.tile_maxc[tile];
 
     const size_t HW = (size_t)a.W * a.H;
     const size_t pix = inside ? (size_t)a.W * py + px : 0;
@@ -65,66 +78,74 @@ __global__ void __launch_bounds__(RB_THREADS) render_bwd_kernel(RenderBwdArgs a)
     }
     const float bg_dot = a.bg[0] * dpx0 + a.bg[1] * dpx1 + a.bg[2] * dpx2;
     const float ddelx_dx = 0.5f * (float)a.W, ddely_dy = 0.5f * (float)a.H;
-    // wave-level upper bound of the list positions any of its pixels replays
-    int wave_maxc = last_contrib;
+    int end = last_contrib;  // wave max: the first (from the back) entry any pixel replays
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) wave_maxc = max(wave_maxc, __shfl_xor(wave_maxc, o));
+    for (int o = 32; o >= 1; o >>= 1) end = max(end, __shfl_xor(end, o));
+    if (end <= 0) return;
 
     float T = T_final;
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
     float last_alpha = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;
+    const uint32_t *list = a.point_list + r.x;
 
-    for (int end = maxc; end > 0; end -= RB_BATCH) {
-        const int cnt = min(RB_BATCH, end);
-        const int lo = end - cnt;
-        __syncthreads();
-        if ((int)threadIdx.x < cnt) {
-            const uint32_t id = a.point_list[r.x + lo + threadIdx.x];
-            const float4 *sp = a.splats + 3 * (size_t)id;
-            sA[threadIdx.x] = sp[0];
-            sB[threadIdx.x] = sp[1];
-            sC[threadIdx.x] = sp[2];
-            sId[threadIdx.x] = id;
+    // chunk c covers entries [lo, lo + 64) with lo = end - 64 (c + 1); lane l <-> entry lo + l
+    int lo = end - 64;
+    uint32_t id = (lo + lane >= 0) ? list[lo + lane] : 0u;
+    uint32_t id_next = (lo - 64 + lane >= 0) ? list[lo - 64 + lane] : 0u;
+    float4 A, B, C;
+    {
+        const float4 *sp = a.splats + 3 * (size_t)id;
+        A = sp[0];
+        B = sp[1];
+        C = sp[2];
+    }
+    for (; lo + 64 > 0; lo -= 64) {
+        const int nlo = lo - 64;
+        const uint32_t id_next2 = (nlo - 64 + lane >= 0) ? list[nlo - 64 + lane] : 0u;
+        float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+        if (nlo + 64 > 0) {
+            const float4 *nsp = a.splats + 3 * (size_t)id_next;
+            nA = nsp[0];
+            nB = nsp[1];
+            nC = nsp[2];
         }
-        __syncthreads();
-        const int jstart = min(cnt, wave_maxc - lo) - 1;
-        for (int j = jstart; j >= 0; j--) {
-            const int k = lo + j;  // upstream `contributor` for this entry
-            const float4 A = sA[j];
-            const float4 E = sC[j];
-            if (A.x + E.y < qxlo || A.x - E.y > qxhi || A.y + E.z < qylo || A.y - E.z > qyhi) continue;
-            const float4 B = sB[j];
+        const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.y, (float)qx0, (float)qy0);
+        uint64_t mask = __ballot(rel);
+        while (mask) {
+            const int k = 63 - __builtin_clzll(mask);
+            mask &= ~(1ull << k);
+            const int entry = lo + k;  // upstream `contributor` for this entry
+            const float gx_ = bcast(A.x, k), gy_ = bcast(A.y, k);
+            const float cx = bcast(A.z, k), cy = bcast(A.w, k), cz = bcast(B.x, k), op = bcast(B.y, k);
+            const float cr = bcast(B.z, k), cg = bcast(B.w, k), cb = bcast(C.x, k);
+            const uint32_t gid = bcast_u(id, k);
             float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
-            bool valid = k < last_contrib;
-            const float dx = A.x - fx, dy = A.y - fy;
-            const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-            valid = valid && !(power > 0.0f);
+            const float dx = gx_ - fx, dy = gy_ - fy;
+            const float power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
             const float G = __expf(power);
-            const float alpha = fminf(0.99f, B.y * G);
-            valid = valid && !(alpha < 1.0f / 255.0f);
+            const float alpha = fminf(0.99f, op * G);
+            const bool valid = entry < last_contrib && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
             if (valid) {
-                T = T / (1.f - alpha);
+                const float inv_1ma = __builtin_amdgcn_rcpf(1.f - alpha);
+                T = T * inv_1ma;
                 const float dchannel_dcolor = alpha * T;
-                float dL_dalpha = 0.0f;
                 acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
                 acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
                 acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-                lc0 = B.z;
-                lc1 = B.w;
-                lc2 = E.x;
-                dL_dalpha += (B.z - acc0) * dpx0;
-                dL_dalpha += (B.w - acc1) * dpx1;
-                dL_dalpha += (E.x - acc2) * dpx2;
+                lc0 = cr;
+                lc1 = cg;
+                lc2 = cb;
+                float dL_dalpha = (cr - acc0) * dpx0 + (cg - acc1) * dpx1 + (cb - acc2) * dpx2;
                 g6 = dchannel_dcolor * dpx0;
                 g7 = dchannel_dcolor * dpx1;
                 g8 = dchannel_dcolor * dpx2;
                 dL_dalpha *= T;
                 last_alpha = alpha;
-                dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                const float dL_dG = B.y * dL_dalpha;
+                dL_dalpha += (-T_final * inv_1ma) * bg_dot;
+                const float dL_dG = op * dL_dalpha;
                 const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * A.z - gdy * A.w;
-                const float dG_ddely = -gdy * B.x - gdx * A.w;
+                const float dG_ddelx = -gdx * cx - gdy * cy;
+                const float dG_ddely = -gdy * cz - gdx * cy;
                 g0 = dL_dG * dG_ddelx * ddelx_dx;
                 g1 = dL_dG * dG_ddely * ddely_dy;
                 g2 = -0.5f * gdx * dx * dL_dG;
@@ -132,20 +153,19 @@ __global__ void __launch_bounds__(RB_THREADS) render_bwd_kernel(RenderBwdArgs a)
                 g4 = -0.5f * gdy * dy * dL_dG;
                 g5 = G * dL_dalpha;
             }
-#ifdef GSR_BWD_LANE_ATOMICS
-            if (valid) {
-                float *row = a.accum + (size_t)sId[j] * ACCUM_STRIDE;
-                atomicAdd(row + 0, g0); atomicAdd(row + 1, g1); atomicAdd(row + 2, g2);
-                atomicAdd(row + 3, g3); atomicAdd(row + 4, g4); atomicAdd(row + 5, g5);
-                atomicAdd(row + 6, g6); atomicAdd(row + 7, g7); atomicAdd(row + 8, g8);
-            }
-            continue;
-#endif
             if (__any(valid)) {
-                // all nine reductions complete in convergent code before any lane selects
-                const float s0 = wave_sum(g0), s1 = wave_sum(g1), s2 = wave_sum(g2);
-                const float s3 = wave_sum(g3), s4 = wave_sum(g4), s5 = wave_sum(g5);
-                const float s6 = wave_sum(g6), s7 = wave_sum(g7), s8 = wave_sum(g8);
+                // reduce-scatter of the nine sums over 64 lanes (convergent: all lanes active)
+                const float h0 = swap32_sum(g0, g1);  // lanes 0-31: g0, 32-63: g1
+                const float h1 = swap32_sum(g2, g3);
+                const float h2 = swap32_sum(g4, g5);
+                const float h3 = swap32_sum(g6, g7);
+                const float h4 = swap32_sum(g8, 0.f);
+                const float k0 = row_sum_to_lane15(swap16_sum(h0, h1));   // lanes 15/31/47/63: g0 g2 g1 g3
+                const float k1 = row_sum_to_lane15(swap16_sum(h2, h3));   //                    g4 g6 g5 g7
+                const float k2 = row_sum_to_lane15(swap16_sum(h4, 0.f));  //                    g8
+                const float s0 = bcast(k0, 15), s2 = bcast(k0, 31), s1 = bcast(k0, 47), s3 = bcast(k0, 63);
+                const float s4 = bcast(k1, 15), s6 = bcast(k1, 31), s5 = bcast(k1, 47), s7 = bcast(k1, 63);
+                const float s8 = bcast(k2, 15);
                 float v = s0;
                 v = lane == 1 ? s1 : v;
                 v = lane == 2 ? s2 : v;
@@ -155,9 +175,14 @@ __global__ void __launch_bounds__(RB_THREADS) render_bwd_kernel(RenderBwdArgs a)
                 v = lane == 6 ? s6 : v;
                 v = lane == 7 ? s7 : v;
                 v = lane == 8 ? s8 : v;
-                if (lane < ACC_NVALS) atomicAdd(a.accum + (size_t)sId[j] * ACCUM_STRIDE + lane, v);
+                if (lane < ACC_NVALS) atomicAdd(a.accum + (size_t)gid * ACCUM_STRIDE + lane, v);
             }
         }
+        A = nA;
+        B = nB;
+        C = nC;
+        id = id_next;
+        id_next = id_next2;
     }
 }
 
@@ -170,16 +195,16 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.W = in.W;
     a.H = in.H;
     a.gx = g.gx;
+    a.tiles = g.tiles;
     a.ranges = at<uint2>(geom, G.off[GSR_GEOM_RANGES]);
     a.point_list = at<uint32_t>(binning, binning_layout(I, in.W, in.H).off[GSR_BIN_POINT_LIST]);
     a.splats = at<float4>(geom, G.off[GSR_GEOM_SPLATS]);
     a.bg = in.bg;
     a.final_T = at<float>(img, Im.off[GSR_IMG_FINAL_T]);
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
-    a.tile_maxc = at<uint32_t>(img, Im.off[GSR_IMG_TILE_MAX_CONTRIB]);
     a.dL_dpix = dL_dpix;
     a.accum = accum;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(g.tiles), dim3(RB_THREADS), 0, s, a);
+    hipLaunchKernelGGL(render_bwd_kernel, dim3(xcd_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

@@ -6,24 +6,20 @@
 // below 1e-4 (that Gaussian is not blended), record n_contrib = list position
 // of the last blended Gaussian and final_T.
 //
-// CDNA4 mapping: one 256-thread workgroup (4 wave64) per tile; wave w owns an
-// 8x8 pixel quadrant so that a Gaussian's alpha>=1/255 box (precomputed by
-// preprocess, conservative) can be tested once per wave: a wave-uniform skip
-// of a Gaussian whose box misses the quadrant changes no pixel, because every
-// pixel of the quadrant would reject it with alpha < 1/255.  Splat records
-// (48 B, gathered through point_list) are staged 256 at a time in LDS; the
-// workgroup stops staging once every pixel is saturated, and each wave stops
-// iterating once its own 64 pixels are.
+// CDNA4 mapping (gsr_blend.hpp): each wave64 owns an 8x8 quadrant and runs on
+// its own — no LDS, no workgroup barrier — so a quadrant that saturates early
+// retires its wave at once.  Chunks of 64 list entries are gathered one per
+// lane (ids two chunks ahead, 48-B splat records one chunk ahead, hiding the
+// dependent-load latency behind the current chunk's blending), culled exactly
+// against the quadrant in parallel, and the surviving Gaussians are blended in
+// list order with their parameters broadcast to SGPRs by v_readlane.
+#include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
-#include "gsr_wave.hpp"
 
 namespace gsr {
 
-constexpr int RF_THREADS = 256;
-constexpr int RF_BATCH = 256;
-
 struct RenderFwdArgs {
-    int W, H, gx;
+    int W, H, gx, tiles;
     const uint2 *ranges;
     const uint32_t *point_list;
     const float4 *splats;
@@ -34,60 +30,82 @@ struct RenderFwdArgs {
     uint32_t *tile_maxc;
 };
 
-__global__ void __launch_bounds__(RF_THREADS) render_fwd_kernel(RenderFwdArgs a) {
-    __shared__ float4 sA[RF_BATCH];  // x, y, conic.x, conic.y
-    __shared__ float4 sB[RF_BATCH];  // conic.z, opacity, r, g
-    __shared__ float4 sC[RF_BATCH];  // b, ext_x, ext_y, -
-    __shared__ uint32_t smax;
-    const int tile = blockIdx.x;
+__global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs a) {
+    const int tile = xcd_tile(blockIdx.x, a.tiles);
+    if (tile < 0) return;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float fx = (float)px, fy = (float)py;
-    const float qxlo = (float)qx0, qxhi = (float)(qx0 + 7), qylo = (float)qy0, qyhi = (float)(qy0 + 7);
     const uint2 r = a.ranges[tile];
     const int n = (int)(r.y - r.x);
-    if (threadIdx.x == 0) smax = 0;
 
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
     uint32_t last = 0;
     bool done = !inside;
-    for (int base = 0; base < n; base += RF_BATCH) {
-        if (__syncthreads_count(done) == RF_THREADS) break;
-        const int k = base + (int)threadIdx.x;
-        if (k < n) {
-            const uint32_t id = a.point_list[r.x + k];
+    if (__any(!done) && n > 0) {
+        const uint32_t *list = a.point_list + r.x;
+        // chunk c: entries [64c, 64c + 64); lane l holds entry 64c + l
+        uint32_t id_next = (64 + lane < n) ? list[64 + lane] : 0u;  // ids of chunk c+1
+        float4 A, B, C;                                             // splats of chunk c
+        {
+            const uint32_t id = lane < n ? list[lane] : 0u;
             const float4 *sp = a.splats + 3 * (size_t)id;
-            sA[threadIdx.x] = sp[0];
-            sB[threadIdx.x] = sp[1];
-            sC[threadIdx.x] = sp[2];
+            A = sp[0];
+            B = sp[1];
+            C = sp[2];
         }
-        __syncthreads();
-        const int cnt = min(RF_BATCH, n - base);
-        for (int j = 0; j < cnt; j++) {
-            if (!__any(!done)) break;
-            const float4 A = sA[j];
-            const float4 E = sC[j];
-            if (A.x + E.y < qxlo || A.x - E.y > qxhi || A.y + E.z < qylo || A.y - E.z > qyhi) continue;
-            if (done) continue;
-            const float4 B = sB[j];
-            const float dx = A.x - fx, dy = A.y - fy;
-            const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-            if (power > 0.0f) continue;
-            const float alpha = fminf(0.99f, B.y * __expf(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1 - alpha);
-            if (test_T < 0.0001f) {
-                done = true;
-                continue;
+        for (int pos = 0; pos < n; pos += 64) {
+            // prefetch: ids of chunk c+2, splats of chunk c+1
+            const uint32_t id_next2 = (pos + 128 + lane < n) ? a.point_list[r.x + pos + 128 + lane] : 0u;
+            const float4 *nsp = a.splats + 3 * (size_t)id_next;
+            const bool has_next = pos + 64 < n;
+            float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+            if (has_next) {
+                nA = nsp[0];
+                nB = nsp[1];
+                nC = nsp[2];
             }
-            C0 += B.z * alpha * T;
-            C1 += B.w * alpha * T;
-            C2 += E.x * alpha * T;
-            T = test_T;
-            last = (uint32_t)(base + j + 1);
+            const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.y, (float)qx0, (float)qy0);
+            uint64_t mask = __ballot(rel);
+            bool stop = false;
+            while (mask) {
+                const int k = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const float gx_ = bcast(A.x, k), gy_ = bcast(A.y, k);
+                const float cx = bcast(A.z, k), cy = bcast(A.w, k), cz = bcast(B.x, k), op = bcast(B.y, k);
+                const float cr = bcast(B.z, k), cg = bcast(B.w, k), cb = bcast(C.x, k);
+                if (!done) {
+                    const float dx = gx_ - fx, dy = gy_ - fy;
+                    const float power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
+                    if (!(power > 0.0f)) {
+                        const float alpha = fminf(0.99f, op * __expf(power));
+                        if (!(alpha < 1.0f / 255.0f)) {
+                            const float test_T = T * (1 - alpha);
+                            if (test_T < 0.0001f) {
+                                done = true;
+                            } else {
+                                C0 += cr * alpha * T;
+                                C1 += cg * alpha * T;
+                                C2 += cb * alpha * T;
+                                T = test_T;
+                                last = (uint32_t)(pos + k + 1);
+                            }
+                        }
+                    }
+                }
+                if (!__any(!done)) {
+                    stop = true;
+                    break;
+                }
+            }
+            if (stop) break;
+            A = nA;
+            B = nB;
+            C = nC;
+            id_next = id_next2;
         }
     }
     if (inside) {
@@ -99,9 +117,11 @@ __global__ void __launch_bounds__(RF_THREADS) render_fwd_kernel(RenderFwdArgs a)
         a.out_color[HW + pix] = C1 + T * a.bg[1];
         a.out_color[2 * HW + pix] = C2 + T * a.bg[2];
     }
-    atomicMax(&smax, last);
-    __syncthreads();
-    if (threadIdx.x == 0) a.tile_maxc[tile] = smax;
+    // per-quadrant max n_contrib -> tile max (the backward starts its walk there)
+    uint32_t m = last;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if (lane == 0) atomicMax(&a.tile_maxc[tile], m);
 }
 
 hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,
@@ -113,6 +133,7 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
     a.W = in.W;
     a.H = in.H;
     a.gx = g.gx;
+    a.tiles = g.tiles;
     a.ranges = at<uint2>(geom, G.off[GSR_GEOM_RANGES]);
     a.point_list = binning ? at<uint32_t>(binning, binning_layout(I, in.W, in.H).off[GSR_BIN_POINT_LIST]) : nullptr;
     a.splats = at<float4>(geom, G.off[GSR_GEOM_SPLATS]);
@@ -121,7 +142,9 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
     a.final_T = at<float>(img, Im.off[GSR_IMG_FINAL_T]);
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
     a.tile_maxc = at<uint32_t>(img, Im.off[GSR_IMG_TILE_MAX_CONTRIB]);
-    hipLaunchKernelGGL(render_fwd_kernel, dim3(g.tiles), dim3(RF_THREADS), 0, s, a);
+    hipError_t e = hipMemsetAsync(a.tile_maxc, 0, (size_t)g.tiles * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(render_fwd_kernel, dim3(xcd_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
 
