@@ -28,7 +28,9 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
     const float dy0 = y0 - my, dy1 = y0 + 7.0f - my;
     if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return true;  // mean inside: q_min = 0
     // convex q: with the minimum outside the box, the box minimum lies on an edge
-    const float icc = 1.0f / cc, ica = 1.0f / ca;
+    // approximate reciprocals only move the edge minimiser by an ulp: q changes at
+    // second order, far inside the preprocess margin
+    const float icc = __builtin_amdgcn_rcpf(cc), ica = __builtin_amdgcn_rcpf(ca);
     float q = INFINITY;
 #pragma unroll
     for (int e = 0; e < 2; e++) {
@@ -42,19 +44,30 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
     return !(q > qmax);
 }
 
+// s_waitcnt vmcnt(4) expcnt(7) lgkmcnt(15): everything but the 4 youngest
+// vector-memory ops (the chunk prefetch) has completed.  Issued as the builtin so
+// that the compiler's waitcnt pass sees it and marks the older loads as landed.
+__device__ __forceinline__ void wait_vmcnt_4() { __builtin_amdgcn_s_waitcnt(0x0F74); }
+
 __device__ __forceinline__ float bcast(float v, int k) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
 }
 __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
 
-// blockIdx -> tile: consecutive tiles (which share most Gaussians) go to
-// workgroups with the same blockIdx % 8, i.e. to one XCD and its L2 under the
-// round-robin dispatch (placement is a speed hint only, never relied upon).
+// blockIdx -> tile.  Workgroups are dealt round-robin over the 8 XCDs
+// (blockIdx % 8 share one; a speed hint only, never relied upon), so strips of
+// XCD_STRIP consecutive tiles (which share most of their Gaussians) are given
+// to one XCD's L2, and the strips are dealt round-robin over the XCDs so that
+// every XCD gets an even share of the heavy centre of the image.
+constexpr int XCD_STRIP = 4;
 __device__ __forceinline__ int xcd_tile(int b, int tiles) {
-    const int per = (tiles + 7) >> 3;
-    const int t = (b & 7) * per + (b >> 3);
+    const int x = b & 7, j = b >> 3;
+    const int t = ((j / XCD_STRIP) * 8 + x) * XCD_STRIP + (j % XCD_STRIP);
     return t < tiles ? t : -1;
 }
-__host__ __device__ inline int xcd_grid(int tiles) { return ((tiles + 7) >> 3) * 8; }
+__host__ __device__ inline int xcd_grid(int tiles) {
+    const int strips = (tiles + XCD_STRIP - 1) / XCD_STRIP;
+    return ((strips + 7) / 8) * 8 * XCD_STRIP;
+}
 
 }  // namespace gsr

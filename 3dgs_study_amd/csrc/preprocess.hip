@@ -135,7 +135,8 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 }
                 // Cull bound for the blend kernels: alpha = o*exp(-q/2) >= 1/255 needs
                 // q = d^T conic d <= 2 ln(255 o).  Stored widened (0.1% + 0.002) so a
-                // wave may skip a Gaussian only when every pixel would reject it.
+                // wave may skip a Gaussian only when every pixel would reject it.  The
+                // record also carries the Gaussian's index (the backward's atomic target).
                 const float opac = in.opacities[idx];
                 const float qmax = 2.0f * logf(255.0f * opac) * 1.001f + 0.002f;
                 a.depths[idx] = p_view.z;
@@ -143,7 +144,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 float4 *sp = a.splats + 3 * (size_t)idx;
                 sp[0] = make_float4(px, py, conic_x, conic_y);
                 sp[1] = make_float4(conic_z, opac, rgb[0], rgb[1]);
-                sp[2] = make_float4(rgb[2], qmax, 0.0f, 0.0f);
+                sp[2] = make_float4(rgb[2], qmax, __uint_as_float((uint32_t)idx), 0.0f);
                 a.clamped[idx] = clampbits;
                 radius_out = r;
                 touched = area;

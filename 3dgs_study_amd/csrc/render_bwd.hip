@@ -50,8 +50,8 @@ __device__ __forceinline__ float swap16_sum(float a, float b) {  // rows: [a0+a1
 __device__ __forceinline__ float row_sum_to_lane15(float v) {  // sum of each 16-lane row lands in its lane 15
     v += dpp_f32<DPP_ROW_SHR1>(v);
     v += dpp_f32<DPP_ROW_SHR2>(v);
-    v += dpp_f32<DPP_ROW_SHR4, 0xf, 0xe>(v);
-    v += dpp_f32<DPP_ROW_SHR8, 0xf, 0xc>(v);
+    v += dpp_f32<DPP_ROW_SHR4>(v);  // only lane 15 is consumed: no bank masks needed,
+    v += dpp_f32<DPP_ROW_SHR8>(v);  // so each step is one v_add_f32_dpp
     return v;
 }
 
@@ -84,31 +84,14 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     if (end <= 0) return;
 
     float T = T_final;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
-    float last_alpha = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;
+    float R0 = 0.f, R1 = 0.f, R2 = 0.f;
+    const bool row_last = (lane & 15) == 15;
+    // accumulator slot of the sum each row-last lane holds: lanes 15/31/47/63 -> +0/+2/+1/+3
+    const int slot = ((lane >> 4) & 1) * 2 + (lane >> 5);
     const uint32_t *list = a.point_list + r.x;
 
-    // chunk c covers entries [lo, lo + 64) with lo = end - 64 (c + 1); lane l <-> entry lo + l
-    int lo = end - 64;
-    uint32_t id = (lo + lane >= 0) ? list[lo + lane] : 0u;
-    uint32_t id_next = (lo - 64 + lane >= 0) ? list[lo - 64 + lane] : 0u;
-    float4 A, B, C;
-    {
-        const float4 *sp = a.splats + 3 * (size_t)id;
-        A = sp[0];
-        B = sp[1];
-        C = sp[2];
-    }
-    for (; lo + 64 > 0; lo -= 64) {
-        const int nlo = lo - 64;
-        const uint32_t id_next2 = (nlo - 64 + lane >= 0) ? list[nlo - 64 + lane] : 0u;
-        float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-        if (nlo + 64 > 0) {
-            const float4 *nsp = a.splats + 3 * (size_t)id_next;
-            nA = nsp[0];
-            nB = nsp[1];
-            nC = nsp[2];
-        }
+    // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l).
+    auto replay_chunk = [&](int lo, const float4 &A, const float4 &B, const float4 &C) {
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.y, (float)qx0, (float)qy0);
         uint64_t mask = __ballot(rel);
         while (mask) {
@@ -117,72 +100,88 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
             const int entry = lo + k;  // upstream `contributor` for this entry
             const float gx_ = bcast(A.x, k), gy_ = bcast(A.y, k);
             const float cx = bcast(A.z, k), cy = bcast(A.w, k), cz = bcast(B.x, k), op = bcast(B.y, k);
-            const float cr = bcast(B.z, k), cg = bcast(B.w, k), cb = bcast(C.x, k);
-            const uint32_t gid = bcast_u(id, k);
-            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
             const float dx = gx_ - fx, dy = gy_ - fy;
             const float power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
             const float G = __expf(power);
             const float alpha = fminf(0.99f, op * G);
             const bool valid = entry < last_contrib && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-            if (valid) {
-                const float inv_1ma = __builtin_amdgcn_rcpf(1.f - alpha);
-                T = T * inv_1ma;
-                const float dchannel_dcolor = alpha * T;
-                acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-                acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-                acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-                lc0 = cr;
-                lc1 = cg;
-                lc2 = cb;
-                float dL_dalpha = (cr - acc0) * dpx0 + (cg - acc1) * dpx1 + (cb - acc2) * dpx2;
-                g6 = dchannel_dcolor * dpx0;
-                g7 = dchannel_dcolor * dpx1;
-                g8 = dchannel_dcolor * dpx2;
-                dL_dalpha *= T;
-                last_alpha = alpha;
-                dL_dalpha += (-T_final * inv_1ma) * bg_dot;
-                const float dL_dG = op * dL_dalpha;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * cx - gdy * cy;
-                const float dG_ddely = -gdy * cz - gdx * cy;
-                g0 = dL_dG * dG_ddelx * ddelx_dx;
-                g1 = dL_dG * dG_ddely * ddely_dy;
-                g2 = -0.5f * gdx * dx * dL_dG;
-                g3 = -0.5f * gdx * dy * dL_dG;
-                g4 = -0.5f * gdy * dy * dL_dG;
-                g5 = G * dL_dalpha;
-            }
-            if (__any(valid)) {
-                // reduce-scatter of the nine sums over 64 lanes (convergent: all lanes active)
-                const float h0 = swap32_sum(g0, g1);  // lanes 0-31: g0, 32-63: g1
-                const float h1 = swap32_sum(g2, g3);
-                const float h2 = swap32_sum(g4, g5);
-                const float h3 = swap32_sum(g6, g7);
-                const float h4 = swap32_sum(g8, 0.f);
-                const float k0 = row_sum_to_lane15(swap16_sum(h0, h1));   // lanes 15/31/47/63: g0 g2 g1 g3
-                const float k1 = row_sum_to_lane15(swap16_sum(h2, h3));   //                    g4 g6 g5 g7
-                const float k2 = row_sum_to_lane15(swap16_sum(h4, 0.f));  //                    g8
-                const float s0 = bcast(k0, 15), s2 = bcast(k0, 31), s1 = bcast(k0, 47), s3 = bcast(k0, 63);
-                const float s4 = bcast(k1, 15), s6 = bcast(k1, 31), s5 = bcast(k1, 47), s7 = bcast(k1, 63);
-                const float s8 = bcast(k2, 15);
-                float v = s0;
-                v = lane == 1 ? s1 : v;
-                v = lane == 2 ? s2 : v;
-                v = lane == 3 ? s3 : v;
-                v = lane == 4 ? s4 : v;
-                v = lane == 5 ? s5 : v;
-                v = lane == 6 ? s6 : v;
-                v = lane == 7 ? s7 : v;
-                v = lane == 8 ? s8 : v;
-                if (lane < ACC_NVALS) atomicAdd(a.accum + (size_t)gid * ACCUM_STRIDE + lane, v);
+            if (!__any(valid)) continue;
+            const float cr = bcast(B.z, k), cg = bcast(B.w, k), cb = bcast(C.x, k);
+            const uint32_t gid = __float_as_uint(bcast(C.z, k));
+            // Branch-free replay step: a skipped pixel sees alpha = 0 (T and the
+            // running colour R unchanged) and zero gradients.  R is upstream's
+            // accum_rec advanced eagerly: after a blended Gaussian it already holds
+            // last_alpha * last_color + (1 - last_alpha) * accum_rec.
+            const float av = valid ? alpha : 0.0f;
+            const float Gv = valid ? G : 0.0f;
+            const float om = 1.f - av;
+            const float inv_1ma = __builtin_amdgcn_rcpf(om);
+            T = T * inv_1ma;
+            const float dchannel_dcolor = av * T;
+            const float e0 = cr - R0, e1 = cg - R1, e2 = cb - R2;
+            const float dot = e0 * dpx0 + e1 * dpx1 + e2 * dpx2;
+            R0 = av * cr + om * R0;
+            R1 = av * cg + om * R1;
+            R2 = av * cb + om * R2;
+            const float dL_dalpha = valid ? dot * T + (-T_final * inv_1ma) * bg_dot : 0.0f;
+            const float g6 = dchannel_dcolor * dpx0;
+            const float g7 = dchannel_dcolor * dpx1;
+            const float g8 = dchannel_dcolor * dpx2;
+            const float dL_dG = op * dL_dalpha;
+            const float gdx = Gv * dx, gdy = Gv * dy;
+            const float dG_ddelx = -gdx * cx - gdy * cy;
+            const float dG_ddely = -gdy * cz - gdx * cy;
+            const float g0 = dL_dG * dG_ddelx * ddelx_dx;
+            const float g1 = dL_dG * dG_ddely * ddely_dy;
+            const float hG = -0.5f * dL_dG;
+            const float g2 = gdx * dx * hG;
+            const float g3 = gdx * dy * hG;
+            const float g4 = gdy * dy * hG;
+            const float g5 = Gv * dL_dalpha;
+            // reduce-scatter of the nine sums over 64 lanes (convergent: all lanes active)
+            const float h0 = swap32_sum(g0, g1);  // lanes 0-31: g0, 32-63: g1
+            const float h1 = swap32_sum(g2, g3);
+            const float h2 = swap32_sum(g4, g5);
+            const float h3 = swap32_sum(g6, g7);
+            const float h4 = swap32_sum(g8, 0.f);
+            const float k0 = row_sum_to_lane15(swap16_sum(h0, h1));   // lanes 15/31/47/63: g0 g2 g1 g3
+            const float k1 = row_sum_to_lane15(swap16_sum(h2, h3));   //                    g4 g6 g5 g7
+            const float k2 = row_sum_to_lane15(swap16_sum(h4, 0.f));  //                    g8
+            // three atomic wave-instructions straight from the lanes holding the sums
+            // (uniform row base in SGPRs, per-lane slot offset), no gather into lanes 0-8
+            float *row = a.accum + (size_t)gid * ACCUM_STRIDE;
+            if (row_last) {
+                atomicAdd(row + slot, k0);
+                atomicAdd(row + slot + 4, k1);
+                if (lane == 15) atomicAdd(row + slot + 8, k2);  // slot = 0 here; a lane-dependent
+                // address keeps the compiler's atomic optimizer (a wave-scan loop) out
             }
         }
-        A = nA;
-        B = nB;
-        C = nC;
-        id = id_next;
-        id_next = id_next2;
+    };
+    // Double-buffered backwards stream, unrolled by two so the buffers swap roles
+    // instead of being copied (see render_fwd.hip).  Indices are clamped so every
+    // load is unconditional; the one wait per chunk also drains the previous
+    // chunk's accumulator atomics, none are waited for inside the Gaussian loop.
+    const float4 *sp = a.splats + 3 * (size_t)list[max(end - 64 + lane, 0)];
+    float4 A0 = sp[0], B0 = sp[1], C0 = sp[2], A1, B1, C1;
+    uint32_t idx_a, idx_b = list[max(end - 128 + lane, 0)];
+    for (int lo = end - 64;;) {
+        idx_a = list[max(lo - 128 + lane, 0)];
+        sp = a.splats + 3 * (size_t)idx_b;
+        A1 = sp[0];
+        B1 = sp[1];
+        C1 = sp[2];
+        wait_vmcnt_4();
+        replay_chunk(lo, A0, B0, C0);
+        if ((lo -= 64) + 64 <= 0) break;
+        idx_b = list[max(lo - 128 + lane, 0)];
+        sp = a.splats + 3 * (size_t)idx_a;
+        A0 = sp[0];
+        B0 = sp[1];
+        C0 = sp[2];
+        wait_vmcnt_4();
+        replay_chunk(lo, A1, B1, C1);
+        if ((lo -= 64) + 64 <= 0) break;
     }
 }
 

@@ -10,7 +10,8 @@
 // its own — no LDS, no workgroup barrier — so a quadrant that saturates early
 // retires its wave at once.  Chunks of 64 list entries are gathered one per
 // lane (ids two chunks ahead, 48-B splat records one chunk ahead, hiding the
-// dependent-load latency behind the current chunk's blending), culled exactly
+// dependent-load latency behind the current chunk's blending; one vmcnt wait per
+// chunk, none in the per-Gaussian loop), culled exactly
 // against the quadrant in parallel, and the surviving Gaussians are blended in
 // list order with their parameters broadcast to SGPRs by v_readlane.
 #include "gsr_blend.hpp"
@@ -47,65 +48,62 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
     bool done = !inside;
     if (__any(!done) && n > 0) {
         const uint32_t *list = a.point_list + r.x;
-        // chunk c: entries [64c, 64c + 64); lane l holds entry 64c + l
-        uint32_t id_next = (64 + lane < n) ? list[64 + lane] : 0u;  // ids of chunk c+1
-        float4 A, B, C;                                             // splats of chunk c
-        {
-            const uint32_t id = lane < n ? list[lane] : 0u;
-            const float4 *sp = a.splats + 3 * (size_t)id;
-            A = sp[0];
-            B = sp[1];
-            C = sp[2];
-        }
-        for (int pos = 0; pos < n; pos += 64) {
-            // prefetch: ids of chunk c+2, splats of chunk c+1
-            const uint32_t id_next2 = (pos + 128 + lane < n) ? a.point_list[r.x + pos + 128 + lane] : 0u;
-            const float4 *nsp = a.splats + 3 * (size_t)id_next;
-            const bool has_next = pos + 64 < n;
-            float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-            if (has_next) {
-                nA = nsp[0];
-                nB = nsp[1];
-                nC = nsp[2];
-            }
+        const int nm1 = n - 1;
+        // Blend one 64-entry chunk starting at list position pos (lane l <-> entry
+        // pos + l); returns true once every pixel of the quadrant is saturated.
+        auto blend_chunk = [&](int pos, const float4 &A, const float4 &B, const float4 &C) -> bool {
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.y, (float)qx0, (float)qy0);
             uint64_t mask = __ballot(rel);
-            bool stop = false;
             while (mask) {
                 const int k = __builtin_ctzll(mask);
                 mask &= mask - 1;
                 const float gx_ = bcast(A.x, k), gy_ = bcast(A.y, k);
                 const float cx = bcast(A.z, k), cy = bcast(A.w, k), cz = bcast(B.x, k), op = bcast(B.y, k);
                 const float cr = bcast(B.z, k), cg = bcast(B.w, k), cb = bcast(C.x, k);
-                if (!done) {
-                    const float dx = gx_ - fx, dy = gy_ - fy;
-                    const float power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-                    if (!(power > 0.0f)) {
-                        const float alpha = fminf(0.99f, op * __expf(power));
-                        if (!(alpha < 1.0f / 255.0f)) {
-                            const float test_T = T * (1 - alpha);
-                            if (test_T < 0.0001f) {
-                                done = true;
-                            } else {
-                                C0 += cr * alpha * T;
-                                C1 += cg * alpha * T;
-                                C2 += cb * alpha * T;
-                                T = test_T;
-                                last = (uint32_t)(pos + k + 1);
-                            }
-                        }
-                    }
-                }
-                if (!__any(!done)) {
-                    stop = true;
-                    break;
-                }
+                // branch-free per-pixel step (selects, not exec-mask branches: the
+                // loop is VALU-issue bound and every branch costs SALU + exec traffic)
+                const float dx = gx_ - fx, dy = gy_ - fy;
+                const float power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
+                const float alpha = fminf(0.99f, op * __expf(power));
+                const float test_T = T * (1 - alpha);
+                const bool ok = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const bool sat = ok && test_T < 0.0001f;  // this Gaussian is not blended
+                const bool blend = ok && !sat;
+                done = done || sat;
+                const float wgt = blend ? alpha * T : 0.0f;
+                C0 += cr * wgt;
+                C1 += cg * wgt;
+                C2 += cb * wgt;
+                T = blend ? test_T : T;
+                last = blend ? (uint32_t)(pos + k + 1) : last;
+                if (!__any(!done)) return true;
             }
-            if (stop) break;
-            A = nA;
-            B = nB;
-            C = nC;
-            id_next = id_next2;
+            return false;
+        };
+        // Double-buffered stream, unrolled by two so the buffers swap roles instead
+        // of being copied (a register copy of an in-flight load would force a full
+        // vmcnt drain).  Indices are clamped: every load is unconditional, so the
+        // single wait per chunk keeps exactly the 4 prefetch loads in flight.
+        const float4 *sp = a.splats + 3 * (size_t)list[min(lane, nm1)];
+        float4 A0 = sp[0], B0 = sp[1], C0_ = sp[2], A1, B1, C1_;
+        uint32_t idx_a, idx_b = list[min(64 + lane, nm1)];
+        for (int pos = 0;;) {
+            idx_a = list[min(pos + 128 + lane, nm1)];
+            sp = a.splats + 3 * (size_t)idx_b;
+            A1 = sp[0];
+            B1 = sp[1];
+            C1_ = sp[2];
+            wait_vmcnt_4();
+            if (blend_chunk(pos, A0, B0, C0_)) break;
+            if ((pos += 64) >= n) break;
+            idx_b = list[min(pos + 128 + lane, nm1)];
+            sp = a.splats + 3 * (size_t)idx_a;
+            A0 = sp[0];
+            B0 = sp[1];
+            C0_ = sp[2];
+            wait_vmcnt_4();
+            if (blend_chunk(pos, A1, B1, C1_)) break;
+            if ((pos += 64) >= n) break;
         }
     }
     if (inside) {
