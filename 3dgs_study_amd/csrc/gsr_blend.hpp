@@ -49,6 +49,20 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
 // that the compiler's waitcnt pass sees it and marks the older loads as landed.
 __device__ __forceinline__ void wait_vmcnt_4() { __builtin_amdgcn_s_waitcnt(0x0F74); }
 
+// Per-wave LDS image of the current chunk: entry k's 48-B splat record at
+// byte 48k (lane-contiguous b128 stores are conflict-free at this stride).  The
+// per-Gaussian loop reads the record back with uniform-address ds_reads
+// (broadcast) — LDS-pipe work instead of nine or ten VALU v_readlanes.
+struct ChunkStage {
+    float4 rec[64][3];
+};
+__device__ __forceinline__ void stage_chunk(ChunkStage &st, int lane, const float4 &A, const float4 &B,
+                                            const float4 &C) {
+    st.rec[lane][0] = A;
+    st.rec[lane][1] = B;
+    st.rec[lane][2] = C;
+}
+
 __device__ __forceinline__ float bcast(float v, int k) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
 }

@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 float4 *sp = a.splats + 3 * (size_t)idx;
                 sp[0] = make_float4(px, py, conic_x, conic_y);
                 sp[1] = make_float4(conic_z, opac, rgb[0], rgb[1]);
-                sp[2] = make_float4(rgb[2], qmax, __uint_as_float((uint32_t)idx), 0.0f);
+                sp[2] = make_float4(rgb[2], __uint_as_float((uint32_t)idx), qmax, 0.0f);
                 a.clamped[idx] = clampbits;
                 radius_out = r;
                 touched = area;

@@ -83,6 +83,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     for (int o = 32; o >= 1; o >>= 1) end = max(end, __shfl_xor(end, o));
     if (end <= 0) return;
 
+    __shared__ ChunkStage stage[BLEND_THREADS / 64];
+    ChunkStage &st = stage[w];
     float T = T_final;
     float R0 = 0.f, R1 = 0.f, R2 = 0.f;
     const bool row_last = (lane & 15) == 15;
@@ -91,23 +93,26 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     const uint32_t *list = a.point_list + r.x;
 
     // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l).
-    auto replay_chunk = [&](int lo, const float4 &A, const float4 &B, const float4 &C) {
-        const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.y, (float)qx0, (float)qy0);
+    auto replay_chunk = [&](int lo, float4 A, float4 B, float4 C) {
+        stage_chunk(st, lane, A, B, C);
+        const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         uint64_t mask = __ballot(rel);
         while (mask) {
             const int k = 63 - __builtin_clzll(mask);
             mask &= ~(1ull << k);
             const int entry = lo + k;  // upstream `contributor` for this entry
-            const float gx_ = bcast(A.x, k), gy_ = bcast(A.y, k);
-            const float cx = bcast(A.z, k), cy = bcast(A.w, k), cz = bcast(B.x, k), op = bcast(B.y, k);
+            const float4 p0 = st.rec[k][0], p1 = st.rec[k][1];
+            const float2 p2 = *reinterpret_cast<const float2 *>(&st.rec[k][2]);
+            const float gx_ = p0.x, gy_ = p0.y, cx = p0.z, cy = p0.w;
+            const float cz = p1.x, op = p1.y;
             const float dx = gx_ - fx, dy = gy_ - fy;
             const float power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
             const float G = __expf(power);
             const float alpha = fminf(0.99f, op * G);
             const bool valid = entry < last_contrib && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
             if (!__any(valid)) continue;
-            const float cr = bcast(B.z, k), cg = bcast(B.w, k), cb = bcast(C.x, k);
-            const uint32_t gid = __float_as_uint(bcast(C.z, k));
+            const float cr = p1.z, cg = p1.w, cb = p2.x;
+            const uint32_t gid = __float_as_uint(p2.y);
             // Branch-free replay step: a skipped pixel sees alpha = 0 (T and the
             // running colour R unchanged) and zero gradients.  R is upstream's
             // accum_rec advanced eagerly: after a blended Gaussian it already holds

@@ -13,7 +13,7 @@
 // dependent-load latency behind the current chunk's blending; one vmcnt wait per
 // chunk, none in the per-Gaussian loop), culled exactly
 // against the quadrant in parallel, and the surviving Gaussians are blended in
-// list order with their parameters broadcast to SGPRs by v_readlane.
+// list order with their parameters broadcast from a per-wave LDS image.
 #include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
 
@@ -46,20 +46,24 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
     uint32_t last = 0;
     bool done = !inside;
+    __shared__ ChunkStage stage[BLEND_THREADS / 64];
+    ChunkStage &st = stage[w];
     if (__any(!done) && n > 0) {
         const uint32_t *list = a.point_list + r.x;
         const int nm1 = n - 1;
         // Blend one 64-entry chunk starting at list position pos (lane l <-> entry
         // pos + l); returns true once every pixel of the quadrant is saturated.
-        auto blend_chunk = [&](int pos, const float4 &A, const float4 &B, const float4 &C) -> bool {
-            const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.y, (float)qx0, (float)qy0);
+        auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
+            stage_chunk(st, lane, A, B, C);
+            const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
             uint64_t mask = __ballot(rel);
             while (mask) {
                 const int k = __builtin_ctzll(mask);
                 mask &= mask - 1;
-                const float gx_ = bcast(A.x, k), gy_ = bcast(A.y, k);
-                const float cx = bcast(A.z, k), cy = bcast(A.w, k), cz = bcast(B.x, k), op = bcast(B.y, k);
-                const float cr = bcast(B.z, k), cg = bcast(B.w, k), cb = bcast(C.x, k);
+                const float4 p0 = st.rec[k][0], p1 = st.rec[k][1];
+                const float cb = st.rec[k][2].x;
+                const float gx_ = p0.x, gy_ = p0.y, cx = p0.z, cy = p0.w;
+                const float cz = p1.x, op = p1.y, cr = p1.z, cg = p1.w;
                 // branch-free per-pixel step (selects, not exec-mask branches: the
                 // loop is VALU-issue bound and every branch costs SALU + exec traffic)
                 const float dx = gx_ - fx, dy = gy_ - fy;
