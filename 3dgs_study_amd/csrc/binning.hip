@@ -145,23 +145,57 @@ __device__ __forceinline__ int next_pow2(int n) {
     return p;
 }
 
+// Bitonic sort of s[0, np) in LDS (np a power of two).  The participating waves
+// each own a contiguous region of R = np / nw elements; every stage whose stride
+// j is below R pairs elements inside one region, so that wave runs it on its
+// own: a wave's LDS operations execute in issue order, so only a compiler fence
+// separates such stages.  Only the log2(nw) * (log2(nw) + 1) / 2 stages with
+// j >= R need a workgroup barrier (6 of 78 for np = 4096 on 8 waves).
 template <int THREADS>
 __device__ __forceinline__ void bitonic_lds(uint64_t *s, int np) {
+    constexpr int NW = THREADS / 64;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int nw = np >> 7;  // keep >= 128 elements (64 pairs) per wave
+    nw = nw < 1 ? 1 : (nw > NW ? NW : nw);
+    const int R = np / nw, half = R >> 1;
+    bool synced = true;  // all waves' previous writes are visible
     for (int k = 2; k <= np; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < (np >> 1); i += THREADS) {
-                const int lo = 2 * i - (i & (j - 1));
-                const int hi = lo + j;
-                const bool asc = (lo & k) == 0;
-                const uint64_t x = s[lo], y = s[hi];
-                if ((x > y) == asc) {
-                    s[lo] = y;
-                    s[hi] = x;
+            if (j >= R) {
+                if (!synced) __syncthreads();
+                for (int i = threadIdx.x; i < (np >> 1); i += THREADS) {
+                    const int lo = 2 * i - (i & (j - 1));
+                    const int hi = lo + j;
+                    const bool asc = (lo & k) == 0;
+                    const uint64_t x = s[lo], y = s[hi];
+                    if ((x > y) == asc) {
+                        s[lo] = y;
+                        s[hi] = x;
+                    }
                 }
+                __syncthreads();
+                synced = true;
+            } else {
+                if (w < nw) {
+                    for (int q = lane; q < half; q += 64) {
+                        const int i = w * half + q;
+                        const int lo = 2 * i - (i & (j - 1));
+                        const int hi = lo + j;
+                        const bool asc = (lo & k) == 0;
+                        const uint64_t x = s[lo], y = s[hi];
+                        if ((x > y) == asc) {
+                            s[lo] = y;
+                            s[hi] = x;
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                synced = false;
             }
-            __syncthreads();
         }
     }
+    if (!synced) __syncthreads();
 }
 
 template <int CAP, int THREADS>
