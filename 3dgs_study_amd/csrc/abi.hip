@@ -21,6 +21,7 @@ namespace {
 
 thread_local std::string g_err;
 thread_local uint32_t *g_pinned = nullptr;  // 16 control words read back per forward
+thread_local hipEvent_t g_ctrl_ready = nullptr;
 
 int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -40,7 +41,7 @@ int check_hip(hipError_t e, const char *what) {
 // Optional per-stage timing with HIP events recorded on the launch stream
 // (bench.py reads it to price the dominant kernel against the HBM roofline).
 struct StageTimer {
-    bool on = false;
+    int mask = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
     std::vector<int> stage;  // stage of each used pair
     size_t used = 0;
@@ -49,12 +50,12 @@ struct StageTimer {
 };
 StageTimer g_timer;  // the ABI is driven from one host thread per process
 
-const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess", "scan",       "tile_count",    "tile_scatter",
-                                            "tile_sort",  "render_fwd", "render_bwd",    "preprocess_bwd"};
+const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess", "scan",       "depth_sort", "duplicate",
+                                            "tile_sort",  "render_fwd", "render_bwd", "preprocess_bwd"};
 
 template <typename F>
 hipError_t timed(int st, hipStream_t s, F &&launch) {
-    if (!g_timer.on) return launch();
+    if (!(g_timer.mask & (1 << st))) return launch();
     if (g_timer.used == g_timer.pool.size()) {
         hipEvent_t a, b;
         hipError_t e = hipEventCreate(&a);
@@ -84,7 +85,8 @@ int validate(const gsr_inputs *in, bool forward) {
     if (!in) return fail(GSR_ERR_ARGS, "inputs is NULL");
     if (in->P < 0) return fail(GSR_ERR_ARGS, "means3D must have dimensions (num_points, 3)");
     if (in->W <= 0 || in->H <= 0) return fail(GSR_ERR_ARGS, "image size must be positive (got %dx%d)", in->W, in->H);
-    if ((int64_t)in->W * in->H > (int64_t)1 << 30) return fail(GSR_ERR_CAPACITY, "image too large");
+    if ((int64_t)in->W * in->H > (int64_t)1 << 30 || in->W > 65535 * TILE_X || in->H > 65535 * TILE_Y)
+        return fail(GSR_ERR_CAPACITY, "image too large");
     if (in->P == 0) return GSR_OK;
     if (!in->means3D || !in->viewmatrix || !in->projmatrix || !in->bg || (forward && !in->opacities))
         return fail(GSR_ERR_ARGS, "missing required input (means3D/opacities/viewmatrix/projmatrix/bg)");
@@ -137,21 +139,20 @@ int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap) {
 const char *gsr_last_error(void) { return g_err.c_str(); }
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 
-int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered,
-                           uint32_t *max_tile_len, void *stream) {
+int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered, void *stream) {
     if (int rc = validate(in, true)) return rc;
     if (!num_rendered) return fail(GSR_ERR_ARGS, "num_rendered is NULL");
     *num_rendered = 0;
-    if (max_tile_len) *max_tile_len = 0;
     if (in->P == 0) return GSR_OK;
     if (!geom || !radii) return fail(GSR_ERR_ARGS, "geom/radii buffers are NULL");
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
     if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, s); }), "preprocess", dbg, s)) return rc;
     if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_scan(in->P, geom, in->W, in->H, s); }), "inclusive scan", dbg, s)) return rc;
-    if (int rc = step(timed(GSR_STAGE_TILE_COUNT, s, [&] { return launch_bin_count(in->P, in->W, in->H, geom, radii, s); }), "tile count", dbg, s)) return rc;
     if (!g_pinned) {
         if (int rc = check_hip(hipHostMalloc((void **)&g_pinned, CTRL_WORDS * 4, hipHostMallocDefault), "hipHostMalloc"))
+            return rc;
+        if (int rc = check_hip(hipEventCreateWithFlags(&g_ctrl_ready, hipEventDisableTiming), "hipEventCreate"))
             return rc;
     }
     const GeomLayout L = geom_layout(in->P, in->W, in->H);
@@ -159,21 +160,20 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
                                           hipMemcpyDeviceToHost, s),
                            "num_rendered read-back"))
         return rc;
-    if (int rc = check_hip(hipStreamSynchronize(s), "num_rendered read-back")) return rc;
+    if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
+    // the depth sort does not depend on num_rendered: it runs while the host waits
+    if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] { return launch_depth_sort(in->P, in->W, in->H, geom, s); }), "depth sort", dbg, s)) return rc;
+    if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;
     if (g_pinned[CTRL_PREFILTER_ERR])
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     const int64_t I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
     if (I > 0xFFFFFFFFll) return fail(GSR_ERR_CAPACITY, "num_rendered %lld exceeds 32-bit list indexing", (long long)I);
-    if ((uint32_t)I != g_pinned[CTRL_TILE_TOTAL_LO])
-        return fail(GSR_ERR_HIP, "internal: scan total %u != tile bucket total %u", (uint32_t)I,
-                    g_pinned[CTRL_TILE_TOTAL_LO]);
     *num_rendered = I;
-    if (max_tile_len) *max_tile_len = g_pinned[CTRL_MAX_TILE];
     return GSR_OK;
 }
 
 int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
-                       uint32_t max_tile_len, const int32_t *radii, float *out_color, void *stream) {
+                       const int32_t *radii, float *out_color, void *stream) {
     if (int rc = validate(in, true)) return rc;
     if (!out_color) return fail(GSR_ERR_ARGS, "out_color is NULL");
     hipStream_t s = (hipStream_t)stream;
@@ -182,11 +182,17 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
         return check_hip(hipMemsetAsync(out_color, 0, (size_t)3 * in->W * in->H * sizeof(float), s), "memset");
     if (!geom || !img || (num_rendered > 0 && !binning)) return fail(GSR_ERR_ARGS, "scratch buffers are NULL");
     if (num_rendered > 0) {
-        if (int rc = step(timed(GSR_STAGE_TILE_SCATTER, s, [&] { return launch_bin_scatter(in->P, in->W, in->H, geom, radii, binning, num_rendered, s); }),
-                          "duplicateWithKeys (tile scatter)", dbg, s))
+        if (int rc = step(timed(GSR_STAGE_DUPLICATE, s, [&] { return launch_emit(in->P, in->W, in->H, geom, radii, binning, num_rendered, s); }),
+                          "duplicateWithKeys", dbg, s))
             return rc;
-        if (int rc = step(timed(GSR_STAGE_TILE_SORT, s, [&] { return launch_tile_sort(in->P, in->W, in->H, geom, binning, num_rendered, max_tile_len, s); }),
-                          "per-tile sort", dbg, s))
+        if (int rc = step(timed(GSR_STAGE_TILE_SORT, s, [&] { return launch_tile_sort(in->P, in->W, in->H, geom, binning, num_rendered, s); }),
+                          "tile sort", dbg, s))
+            return rc;
+    } else {
+        const GeomLayout L = geom_layout(in->P, in->W, in->H);
+        if (int rc = check_hip(hipMemsetAsync(at<uint2>(geom, L.off[GSR_GEOM_RANGES]), 0,
+                                              (size_t)grid_dims(in->W, in->H).tiles * sizeof(uint2), s),
+                               "ranges memset"))
             return rc;
     }
     return step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s); }), "render", dbg, s);
@@ -227,8 +233,8 @@ int gsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, c
     return check_hip(launch_mark_visible(P, means3D, viewmatrix, present, s), "mark_visible");
 }
 
-int gsr_timing_enable(int on) {
-    g_timer.on = on != 0;
+int gsr_timing_enable(int mask) {
+    g_timer.mask = mask;
     g_timer.used = 0;
     for (int k = 0; k < GSR_STAGE_COUNT; k++) {
         g_timer.total_ms[k] = 0;

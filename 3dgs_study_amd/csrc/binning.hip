@@ -1,26 +1,33 @@
-// binning.hip — tile bucketing and per-tile depth sort.
+// binning.hip — depth-ordered tile binning.
 //
 // Replaces upstream duplicateWithKeys + cub::DeviceRadixSort::SortPairs +
 // identifyTileRanges (rasterizer_impl.cu).
-// Upstream emits one (tile<<32 | depth_bits, id) pair per touched tile and
-// radix-sorts all I pairs over 32+log2(T) bits (~6 passes of 24 B/pair).
-// Here the same order is produced with one pass over the instances:
+// Upstream emits one (tile << 32 | depth_bits, id) pair per touched tile, in
+// Gaussian-index order, and stably radix-sorts all I pairs over 32 + log2(T)
+// bits (~6 passes over 12-B pairs).  The resulting order inside a tile is
+// (depth_bits, id).  Here the same order comes from two much cheaper sorts:
 //
-//  1. bin_count   — workgroup b owns a contiguous slice of Gaussians and counts
-//                   its instances per tile in LDS -> counts[b][t] (no global
-//                   atomics; the rect is recomputed exactly as preprocess did).
-//  2. bin_colscan — per tile, exclusive scan over b -> counts[b][t] becomes the
-//                   slice's write offset inside the tile's bucket.
-//  3. bin_tilescan— exclusive scan over tiles -> ranges[t] (identifyTileRanges'
-//                   output, available before any key exists) and max tile length.
-//  4. bin_scatter — each workgroup re-walks its slice and drops the 64-bit key
-//                   (depth_bits << 32 | id) into the tile bucket via LDS cursors.
-//  5. tile sort   — one workgroup per tile sorts its bucket in LDS.  Ascending
-//                   (depth_bits, id) is exactly the stable radix order upstream
-//                   gets (equal depth bits keep emission = index order), so
-//                   point_list and ranges match upstream bit for bit.
+//  1. depth sort  — stable LSD radix sort of the P depth bit patterns with the
+//                   index as value (4 passes over P, not I): order[rank] = id in
+//                   (depth_bits, id) order.  Invisible Gaussians sort anywhere:
+//                   they emit nothing.
+//  2. rank scan   — exclusive scan of tiles_touched gathered in rank order.
+//  3. emit        — each Gaussian, in rank order, writes (tile, id) for every
+//                   tile of its rect (row-major, as upstream) at its offset.
+//  4. tile sort   — stable LSD radix sort of the I instances by tile index
+//                   (ceil(log2 T / 8) passes: 2 at 1080p and 4K).  Stability
+//                   keeps rank order inside a tile, i.e. (depth_bits, id).
+//  5. ranges      — identifyTileRanges on the sorted tile keys.
 //
-// Steps 1-3 run before the num_rendered host read-back, overlapping it.
+// Steps 1-2 run in gsr_forward_preprocess while the host reads num_rendered;
+// 3-5 run in gsr_forward_render once the caller has sized the binning buffer.
+//
+// One radix pass = upsweep (per-block digit histogram), digit scan (one
+// workgroup per digit over the blocks), downsweep (stable scatter).  Inside a
+// workgroup each wave owns a contiguous quarter of the block's items and walks
+// it in rounds of 64; lanes holding the same digit are found with 8 ballots
+// (wave "match"), ranked with mbcnt, and a per-wave LDS counter per digit
+// carries the running count from round to round — no atomics anywhere.
 #pragma clang fp contract(off)
 
 #include "gsr_kernels.hpp"
@@ -29,324 +36,344 @@
 
 namespace gsr {
 
-struct BinArgs {
-    int P, gpb, gx, gy, T;
-    const float2 *means2D;
-    const int32_t *radii;
-    const float *depths;
-    uint32_t *counts;  // [NB][T]
-    const uint2 *ranges;
-    uint64_t *keys;
+constexpr int RX_WAVES = RX_THREADS / 64;
+static_assert(RX_THREADS == RADIX, "one thread per digit in the per-block digit loops");
+
+// Lanes of the wave whose digit equals this lane's (restricted to `live`);
+// only the pass's nbits significant digit bits are compared.
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t live, int nbits) {
+    uint64_t m = live;
+#pragma unroll
+    for (int b = 0; b < RADIX_BITS; b++) {
+        if (b < nbits) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(bit);
+            m &= bit ? bal : ~bal;
+        }
+    }
+    return m;
+}
+// number of set bits of m below this lane
+__device__ __forceinline__ uint32_t count_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+struct RadixPass {
+    const uint32_t *kin;   // keys (the digit source)
+    const uint32_t *vin;   // values; nullptr = the item index
+    uint32_t *kout;        // nullptr = keys not needed after this pass
+    uint32_t *vout;
+    uint32_t n;
+    int shift;
+    int nbits;             // significant bits of this pass's digit (<= RADIX_BITS)
+    uint32_t *hist;        // [RADIX][NB] block counts -> block offsets within each digit
+    uint32_t *totals;      // [RADIX]
+    int NB;
 };
 
-__global__ void __launch_bounds__(BIN_THREADS) bin_count_kernel(BinArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    const int b = blockIdx.x;
-    const int c0 = blockIdx.y * BIN_TILE_CHUNK;
-    const int clen = min(BIN_TILE_CHUNK, a.T - c0);
-    for (int j = threadIdx.x; j < clen; j += BIN_THREADS) hist[j] = 0;
-    __syncthreads();
-    const int g0 = b * a.gpb, g1 = min(a.P, g0 + a.gpb);
-    for (int i = g0 + threadIdx.x; i < g1; i += BIN_THREADS) {
-        const int r = a.radii[i];
-        if (r <= 0) continue;
-        const float2 m = a.means2D[i];
-        const TileRect rc = get_rect(m.x, m.y, r, a.gx, a.gy);
-        for (unsigned y = rc.y0; y < rc.y1; y++) {
-            const int row = (int)(y * a.gx);
-            const int t0 = max(row + (int)rc.x0, c0), t1 = min(row + (int)rc.x1, c0 + clen);
-            for (int t = t0; t < t1; t++) atomicAdd(&hist[t - c0], 1u);
-        }
-    }
-    __syncthreads();
-    uint32_t *dst = a.counts + (size_t)b * a.T + c0;
-    for (int j = threadIdx.x; j < clen; j += BIN_THREADS) dst[j] = hist[j];
-}
-
-__global__ void __launch_bounds__(256) bin_colscan_kernel(uint32_t *counts, int NB, int T, uint32_t *tile_total) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= T) return;
-    uint32_t run = 0;
-    int b = 0;
-    for (; b + 8 <= NB; b += 8) {
-        uint32_t c[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) c[k] = counts[(size_t)(b + k) * T + t];
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            counts[(size_t)(b + k) * T + t] = run;
-            run += c[k];
-        }
-    }
-    for (; b < NB; b++) {
-        const uint32_t c = counts[(size_t)b * T + t];
-        counts[(size_t)b * T + t] = run;
-        run += c;
-    }
-    tile_total[t] = run;
-}
-
-constexpr int TS_THREADS = 1024;
-__global__ void __launch_bounds__(TS_THREADS)
-    bin_tilescan_kernel(const uint32_t *tile_total, int T, uint2 *ranges, uint32_t *ctrl) {
-    __shared__ uint32_t wsum[TS_THREADS / 64];
-    __shared__ uint32_t smax;
-    if (threadIdx.x == 0) smax = 0;
-    __syncthreads();
-    uint32_t carry = 0, mx = 0;
-    for (int base = 0; base < T; base += TS_THREADS) {
-        const int t = base + threadIdx.x;
-        const uint32_t v = t < T ? tile_total[t] : 0u;
-        uint32_t tot;
-        const uint32_t inc = block_inclusive_scan<TS_THREADS>(v, wsum, &tot);
-        // identifyTileRanges leaves empty tiles at the memset value (0, 0)
-        if (t < T) ranges[t] = v ? make_uint2(carry + inc - v, carry + inc) : make_uint2(0u, 0u);
-        carry += tot;
-        mx = max(mx, v);
-    }
-    atomicMax(&smax, mx);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        ctrl[CTRL_MAX_TILE] = smax;
-        ctrl[CTRL_TILE_TOTAL_LO] = carry;
-    }
-}
-
-__global__ void __launch_bounds__(BIN_THREADS) bin_scatter_kernel(BinArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
-    const int b = blockIdx.x;
-    const int c0 = blockIdx.y * BIN_TILE_CHUNK;
-    const int clen = min(BIN_TILE_CHUNK, a.T - c0);
-    const uint32_t *offs = a.counts + (size_t)b * a.T + c0;
-    for (int j = threadIdx.x; j < clen; j += BIN_THREADS) cur[j] = a.ranges[c0 + j].x + offs[j];
-    __syncthreads();
-    const int g0 = b * a.gpb, g1 = min(a.P, g0 + a.gpb);
-    for (int i = g0 + threadIdx.x; i < g1; i += BIN_THREADS) {
-        const int r = a.radii[i];
-        if (r <= 0) continue;
-        const float2 m = a.means2D[i];
-        const TileRect rc = get_rect(m.x, m.y, r, a.gx, a.gy);
-        const uint64_t key = ((uint64_t)__float_as_uint(a.depths[i]) << 32) | (uint32_t)i;
-        for (unsigned y = rc.y0; y < rc.y1; y++) {
-            const int row = (int)(y * a.gx);
-            const int t0 = max(row + (int)rc.x0, c0), t1 = min(row + (int)rc.x1, c0 + clen);
-            for (int t = t0; t < t1; t++) {
-                const uint32_t slot = atomicAdd(&cur[t - c0], 1u);
-                a.keys[slot] = key;
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------- tile sort
-__device__ __forceinline__ int next_pow2(int n) {
-    int p = 1;
-    while (p < n) p <<= 1;
-    return p;
-}
-
-// Bitonic sort of s[0, np) in LDS (np a power of two).  The participating waves
-// each own a contiguous region of R = np / nw elements; every stage whose stride
-// j is below R pairs elements inside one region, so that wave runs it on its
-// own: a wave's LDS operations execute in issue order, so only a compiler fence
-// separates such stages.  Only the log2(nw) * (log2(nw) + 1) / 2 stages with
-// j >= R need a workgroup barrier (6 of 78 for np = 4096 on 8 waves).
-template <int THREADS>
-__device__ __forceinline__ void bitonic_lds(uint64_t *s, int np) {
-    constexpr int NW = THREADS / 64;
+// ITEMS per thread: fewer for short inputs (more workgroups, shorter serial
+// rank chains), more for long ones (fewer blocks in the digit scan).
+template <int ITEMS>
+__global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) {
+    constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
+    __shared__ uint32_t h[RX_WAVES][RADIX];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int nw = np >> 7;  // keep >= 128 elements (64 pairs) per wave
-    nw = nw < 1 ? 1 : (nw > NW ? NW : nw);
-    const int R = np / nw, half = R >> 1;
-    bool synced = true;  // all waves' previous writes are visible
-    for (int k = 2; k <= np; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= R) {
-                if (!synced) __syncthreads();
-                for (int i = threadIdx.x; i < (np >> 1); i += THREADS) {
-                    const int lo = 2 * i - (i & (j - 1));
-                    const int hi = lo + j;
-                    const bool asc = (lo & k) == 0;
-                    const uint64_t x = s[lo], y = s[hi];
-                    if ((x > y) == asc) {
-                        s[lo] = y;
-                        s[hi] = x;
-                    }
-                }
-                __syncthreads();
-                synced = true;
-            } else {
-                if (w < nw) {
-                    for (int q = lane; q < half; q += 64) {
-                        const int i = w * half + q;
-                        const int lo = 2 * i - (i & (j - 1));
-                        const int hi = lo + j;
-                        const bool asc = (lo & k) == 0;
-                        const uint64_t x = s[lo], y = s[hi];
-                        if ((x > y) == asc) {
-                            s[lo] = y;
-                            s[hi] = x;
-                        }
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                synced = false;
-            }
-        }
-    }
-    if (!synced) __syncthreads();
-}
-
-template <int CAP, int THREADS>
-__global__ void __launch_bounds__(THREADS)
-    sort_tiles_lds_kernel(const uint2 *ranges, uint64_t *keys, uint32_t *point_list) {
-    __shared__ uint64_t s[CAP];
-    const uint2 r = ranges[blockIdx.x];
-    const int n = (int)(r.y - r.x);
-    if (n <= 0 || n > CAP) return;
-    if (n == 1) {
-        if (threadIdx.x == 0) point_list[r.x] = (uint32_t)keys[r.x];
-        return;
-    }
-    const int np = next_pow2(n);
-    for (int i = threadIdx.x; i < np; i += THREADS) s[i] = i < n ? keys[r.x + i] : ~0ull;
+#pragma unroll
+    for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
     __syncthreads();
-    bitonic_lds<THREADS>(s, np);
-    for (int i = threadIdx.x; i < n; i += THREADS) {
-        const uint64_t k = s[i];
-        keys[r.x + i] = k;
-        point_list[r.x + i] = (uint32_t)k;
+    const uint32_t base = blockIdx.x * (uint32_t)TILE_N + w * (uint32_t)WAVE_N + lane;
+    uint32_t kk[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const uint32_t idx = base + 64u * r;
+        kk[r] = idx < a.n ? a.kin[idx] : 0u;
     }
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++)
+        if (base + 64u * r < a.n) atomicAdd(&h[w][(kk[r] >> a.shift) & (RADIX - 1)], 1u);  // order-free count
+    __syncthreads();
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < RX_WAVES; k++) c += h[k][threadIdx.x];
+    a.hist[(size_t)threadIdx.x * a.NB + blockIdx.x] = c;
 }
 
-// Tiles longer than SORT_MAX_LDS: sort LDS-sized chunks, then merge runs
-// pairwise in global memory (merge path, ping-pong with tmp).
-constexpr int BIG_THREADS = 1024;
-__device__ inline int merge_corank(int d, const uint64_t *A, int na, const uint64_t *B, int nb) {
-    int lo = max(0, d - nb), hi = min(d, na);
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (A[mid] < B[d - mid - 1])
-            lo = mid + 1;
-        else
-            hi = mid;
+// One workgroup per digit: exclusive scan of that digit's block counts.
+__global__ void __launch_bounds__(256) radix_digit_scan_kernel(RadixPass a) {
+    __shared__ uint32_t wsum[4];
+    uint32_t *row = a.hist + (size_t)blockIdx.x * a.NB;
+    uint32_t carry = 0;
+    for (int base = 0; base < a.NB; base += 256) {
+        const int i = base + threadIdx.x;
+        const uint32_t v = i < a.NB ? row[i] : 0u;
+        uint32_t tot;
+        const uint32_t inc = block_inclusive_scan<256>(v, wsum, &tot);
+        if (i < a.NB) row[i] = carry + inc - v;
+        carry += tot;
     }
-    return lo;
+    if (threadIdx.x == 0) a.totals[blockIdx.x] = carry;
 }
 
-__global__ void __launch_bounds__(BIG_THREADS)
-    sort_tiles_big_kernel(const uint2 *ranges, uint64_t *keys, uint64_t *tmp, uint32_t *point_list) {
-    __shared__ uint64_t s[SORT_MAX_LDS];
-    const uint2 r = ranges[blockIdx.x];
-    const int n = (int)(r.y - r.x);
-    if (n <= SORT_MAX_LDS) return;
-    uint64_t *src = keys + r.x, *dst = tmp + r.x;
-    for (int c = 0; c < n; c += SORT_MAX_LDS) {
-        const int m = min(SORT_MAX_LDS, n - c);
-        const int np = next_pow2(m);
-        for (int i = threadIdx.x; i < np; i += BIG_THREADS) s[i] = i < m ? src[c + i] : ~0ull;
-        __syncthreads();
-        bitonic_lds<BIG_THREADS>(s, np);
-        for (int i = threadIdx.x; i < m; i += BIG_THREADS) src[c + i] = s[i];
-        __syncthreads();
+template <int ITEMS>
+__global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a) {
+    constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
+    __shared__ uint32_t cnt[RX_WAVES][RADIX];
+    __shared__ uint32_t lstart[RADIX];   // block-local start of each digit's run
+    __shared__ uint32_t gstart[RADIX];   // global start of this block's run of each digit
+    __shared__ uint32_t wsum[RX_WAVES];
+    __shared__ uint32_t stage_k[TILE_N], stage_v[TILE_N];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t b0 = blockIdx.x * (uint32_t)TILE_N;
+    const uint32_t base = b0 + w * (uint32_t)WAVE_N + lane;
+    uint32_t kk[ITEMS], vv[ITEMS], rk[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const uint32_t idx = base + 64u * r;
+        const bool ok = idx < a.n;
+        kk[r] = ok ? a.kin[idx] : 0u;
+        vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
     }
-    for (int w = SORT_MAX_LDS; w < n; w <<= 1) {
-        for (int s0 = 0; s0 < n; s0 += 2 * w) {
-            const int na = min(w, n - s0);
-            const int nb = max(0, min(w, n - s0 - na));
-            const uint64_t *A = src + s0, *B = src + s0 + na;
-            uint64_t *out = dst + s0;
-            const int total = na + nb;
-            const int per = (total + BIG_THREADS - 1) / BIG_THREADS;
-            const int d0 = threadIdx.x * per;
-            if (d0 < total) {
-                const int d1 = min(d0 + per, total);
-                int i = merge_corank(d0, A, na, B, nb);
-                int j = d0 - i;
-                for (int d = d0; d < d1; d++) {
-                    const bool takeA = (j >= nb) || (i < na && A[i] <= B[j]);
-                    out[d] = takeA ? A[i++] : B[j++];
-                }
-            }
+    {  // where this block's items of digit d go: all smaller digits + earlier blocks
+        const uint32_t t = a.totals[threadIdx.x];
+        uint32_t tot;
+        const uint32_t inc = block_inclusive_scan<RX_THREADS>(t, wsum, &tot);
+        gstart[threadIdx.x] = inc - t + a.hist[(size_t)threadIdx.x * a.NB + blockIdx.x];
+    }
+#pragma unroll
+    for (int k = 0; k < RX_WAVES; k++) cnt[k][threadIdx.x] = 0;
+    __syncthreads();
+    // stable ranks inside each wave's quarter
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const bool ok = base + 64u * r < a.n;
+        const uint64_t live = __ballot(ok);
+        if (!live) break;
+        const uint32_t d = (kk[r] >> a.shift) & (RADIX - 1);
+        const uint64_t peers = match_digit(d, live, a.nbits);
+        const uint32_t below = count_below(peers);
+        const uint32_t c = cnt[w][d];
+        rk[r] = c + below;
+        if (ok && below == 0) cnt[w][d] = c + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    __syncthreads();
+    {  // block-local digit runs, and each wave's start inside its digit's run
+        uint32_t c[RX_WAVES], sum = 0;
+#pragma unroll
+        for (int k = 0; k < RX_WAVES; k++) {
+            c[k] = cnt[k][threadIdx.x];
+            sum += c[k];
         }
-        __syncthreads();
-        uint64_t *t = src;
-        src = dst;
-        dst = t;
+        uint32_t tot;
+        const uint32_t start = block_inclusive_scan<RX_THREADS>(sum, wsum, &tot) - sum;
+        lstart[threadIdx.x] = start;
+        uint32_t off = start;
+#pragma unroll
+        for (int k = 0; k < RX_WAVES; k++) {
+            cnt[k][threadIdx.x] = off;
+            off += c[k];
+        }
     }
-    for (int i = threadIdx.x; i < n; i += BIG_THREADS) {
-        const uint64_t k = src[i];
-        if (src != keys + r.x) keys[r.x + i] = k;
-        point_list[r.x + i] = (uint32_t)k;
+    __syncthreads();
+    // block-sorted image in LDS ...
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        if (base + 64u * r < a.n) {
+            const uint32_t d = (kk[r] >> a.shift) & (RADIX - 1);
+            const uint32_t p = cnt[w][d] + rk[r];
+            stage_k[p] = kk[r];
+            stage_v[p] = vv[r];
+        }
+    }
+    __syncthreads();
+    // ... written out in order: each digit's run is contiguous in the output too
+    const uint32_t nb = min((uint32_t)TILE_N, a.n - b0);
+    for (uint32_t i = threadIdx.x; i < nb; i += RX_THREADS) {
+        const uint32_t k = stage_k[i];
+        const uint32_t d = (k >> a.shift) & (RADIX - 1);
+        const uint32_t pos = gstart[d] + (i - lstart[d]);
+        if (a.kout) a.kout[pos] = k;
+        a.vout[pos] = stage_v[i];
     }
 }
 
-// ---------------------------------------------------------------- launchers
-static BinArgs make_args(int P, int W, int H, void *geom, const int32_t *radii) {
-    const GeomLayout L = geom_layout(P, W, H);
-    const GridDims g = grid_dims(W, H);
-    BinArgs a;
-    a.P = P;
-    a.gpb = bin_gpb(P);
-    a.gx = g.gx;
-    a.gy = g.gy;
-    a.T = g.tiles;
-    a.means2D = at<float2>(geom, L.off[GSR_GEOM_MEANS2D]);
-    a.radii = radii;
-    a.depths = at<float>(geom, L.off[GSR_GEOM_DEPTHS]);
-    a.counts = at<uint32_t>(geom, L.bin_counts);
-    a.ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
-    a.keys = nullptr;
-    return a;
-}
-
-static int nchunks(int T) { return (T + BIN_TILE_CHUNK - 1) / BIN_TILE_CHUNK; }
-static size_t chunk_lds(int T) { return (size_t)min(T, BIN_TILE_CHUNK) * 4; }
-
-hipError_t launch_bin_count(int P, int W, int H, void *geom, const int32_t *radii, hipStream_t s) {
-    const BinArgs a = make_args(P, W, H, geom, radii);
-    const GeomLayout L = geom_layout(P, W, H);
-    const int NB = bin_blocks(P);
-    uint32_t *tile_total = at<uint32_t>(geom, L.tile_total);
-    hipLaunchKernelGGL(bin_count_kernel, dim3(NB, nchunks(a.T)), dim3(BIN_THREADS), chunk_lds(a.T), s, a);
-    hipLaunchKernelGGL(bin_colscan_kernel, dim3((a.T + 255) / 256), dim3(256), 0, s, a.counts, NB, a.T, tile_total);
-    hipLaunchKernelGGL(bin_tilescan_kernel, dim3(1), dim3(TS_THREADS), 0, s, (const uint32_t *)tile_total, a.T,
-                       at<uint2>(geom, L.off[GSR_GEOM_RANGES]), at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]));
+template <int ITEMS>
+static hipError_t radix_pass(const RadixPass &a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(radix_upsweep_kernel<ITEMS>, dim3(a.NB), dim3(RX_THREADS), 0, s, a);
+    hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(RADIX), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(radix_downsweep_kernel<ITEMS>, dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_bin_scatter(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
-                              hipStream_t s) {
-    BinArgs a = make_args(P, W, H, geom, radii);
-    a.keys = at<uint64_t>(binning, binning_layout(I, W, H).off[GSR_BIN_KEYS]);
-    const int NB = bin_blocks(P);
-    hipLaunchKernelGGL(bin_scatter_kernel, dim3(NB, nchunks(a.T)), dim3(BIN_THREADS), chunk_lds(a.T), s, a);
+// ------------------------------------------------------------ rank-order scan
+
+__device__ __forceinline__ uint32_t rect_area(uint2 q) {
+    return ((q.x >> 16) - (q.x & 0xffffu)) * ((q.y >> 16) - (q.y & 0xffffu));
+}
+
+__global__ void __launch_bounds__(EMIT_BLOCK)
+    rank_sums_kernel(const uint32_t *order, const uint2 *rects, int P, uint32_t *sums) {
+    __shared__ uint32_t wsum[EMIT_BLOCK / 64];
+    const int r = blockIdx.x * EMIT_BLOCK + threadIdx.x;
+    const uint32_t v = r < P ? rect_area(rects[order[r]]) : 0u;
+    const uint32_t tot = block_sum<EMIT_BLOCK>(v, wsum);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+constexpr int TOPSCAN_THREADS = 1024;
+__global__ void __launch_bounds__(TOPSCAN_THREADS) exclusive_scan_one_block_kernel(uint32_t *v, int n) {
+    __shared__ uint32_t wsum[TOPSCAN_THREADS / 64];
+    uint32_t carry = 0;
+    for (int base = 0; base < n; base += TOPSCAN_THREADS) {
+        const int i = base + threadIdx.x;
+        const uint32_t x = i < n ? v[i] : 0u;
+        uint32_t tot;
+        const uint32_t inc = block_inclusive_scan<TOPSCAN_THREADS>(x, wsum, &tot);
+        if (i < n) v[i] = carry + inc - x;
+        carry += tot;
+    }
+}
+
+// duplicateWithKeys in rank order: (tile, id) for every tile of the rect.
+// The workgroup's 256 Gaussians own one contiguous run of instances; threads
+// take consecutive instances (coalesced stores) and find their Gaussian by a
+// binary search over the LDS offsets.
+struct EmitArgs {
+    int P, gx;
+    const uint32_t *order;
+    const uint2 *rects;
+    const uint32_t *block_prefix;
+    uint32_t *tile_keys;
+    uint32_t *ids;
+};
+__global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
+    __shared__ uint32_t wsum[EMIT_BLOCK / 64];
+    __shared__ uint32_t loff[EMIT_BLOCK + 1];
+    __shared__ uint4 rect[EMIT_BLOCK];  // x0, width, y0, id
+    const int r = blockIdx.x * EMIT_BLOCK + threadIdx.x;
+    const uint32_t id = r < a.P ? a.order[r] : 0u;
+    const uint2 q = r < a.P ? a.rects[id] : make_uint2(0u, 0u);
+    const uint32_t v = rect_area(q);
+    uint32_t tot;
+    const uint32_t inc = block_inclusive_scan<EMIT_BLOCK>(v, wsum, &tot);
+    loff[threadIdx.x] = inc - v;
+    if (threadIdx.x == EMIT_BLOCK - 1) loff[EMIT_BLOCK] = tot;
+    if (v) rect[threadIdx.x] = make_uint4(q.x & 0xffffu, (q.x >> 16) - (q.x & 0xffffu), q.y & 0xffffu, id);
+    __syncthreads();
+    const uint32_t base = a.block_prefix[blockIdx.x];
+    for (uint32_t j = threadIdx.x; j < tot; j += EMIT_BLOCK) {
+        int lo = 0, hi = EMIT_BLOCK;  // largest k with loff[k] <= j (it has v > 0)
+#pragma unroll
+        for (int step = 0; step < 8; step++) {
+            const int mid = (lo + hi) >> 1;
+            if (loff[mid] <= j) lo = mid; else hi = mid;
+        }
+        const uint4 rc = rect[lo];
+        const uint32_t q = j - loff[lo];
+        uint32_t y = (uint32_t)((float)q * __builtin_amdgcn_rcpf((float)rc.y));
+        if (y * rc.y > q) y--;
+        if ((y + 1) * rc.y <= q) y++;
+        const uint32_t x = q - y * rc.y;
+        a.tile_keys[base + j] = (rc.z + y) * (uint32_t)a.gx + rc.x + x;
+        a.ids[base + j] = rc.w;
+    }
+}
+
+// identifyTileRanges: ranges were zeroed; empty tiles stay (0, 0).
+__global__ void identify_ranges_kernel(const uint32_t *tile_keys, uint32_t n, uint2 *ranges) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = tile_keys[i];
+    if (i == 0 || tile_keys[i - 1] != t) ranges[t].x = i;
+    if (i == n - 1 || tile_keys[i + 1] != t) ranges[t].y = i + 1;
+}
+
+// ------------------------------------------------------------ launchers
+hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
+    const GeomLayout L = geom_layout(P, W, H);
+    RadixPass a;
+    a.n = (uint32_t)P;
+    a.NB = radix_blocks(P, DSORT_ITEMS);
+    a.hist = at<uint32_t>(geom, L.dsort_hist);
+    a.totals = at<uint32_t>(geom, L.dsort_totals);
+    const uint32_t *depth_bits = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTHS]);
+    uint32_t *ka = at<uint32_t>(geom, L.dsort_keys_a), *kb = at<uint32_t>(geom, L.dsort_keys_b);
+    uint32_t *va = at<uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), *vb = at<uint32_t>(geom, L.dsort_vals_b);
+    // (depth, index) -> b -> a -> b -> a(order); the last pass drops the keys
+    const uint32_t *kin[4] = {depth_bits, kb, ka, kb};
+    const uint32_t *vin[4] = {nullptr, vb, va, vb};
+    uint32_t *kout[4] = {kb, ka, kb, nullptr};
+    uint32_t *vout[4] = {vb, va, vb, va};
+    for (int p = 0; p < 4; p++) {
+        a.kin = kin[p];
+        a.vin = vin[p];
+        a.kout = kout[p];
+        a.vout = vout[p];
+        a.shift = 8 * p;
+        a.nbits = RADIX_BITS;
+        hipError_t e = radix_pass<DSORT_ITEMS>(a, s);
+        if (e != hipSuccess) return e;
+    }
+    // rank-order exclusive offsets of the instances, per EMIT block
+    const int nb = emit_blocks(P);
+    uint32_t *sums = at<uint32_t>(geom, L.emit_sums);
+    hipLaunchKernelGGL(rank_sums_kernel, dim3(nb), dim3(EMIT_BLOCK), 0, s, (const uint32_t *)va,
+                       at<const uint2>(geom, L.rects), P, sums);
+    hipLaunchKernelGGL(exclusive_scan_one_block_kernel, dim3(1), dim3(TOPSCAN_THREADS), 0, s, sums, nb);
     return hipGetLastError();
 }
 
-hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, uint32_t max_tile,
-                            hipStream_t s) {
-    const GridDims g = grid_dims(W, H);
+hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
+                       hipStream_t s) {
+    const GeomLayout L = geom_layout(P, W, H);
     const BinningLayout B = binning_layout(I, W, H);
-    const uint2 *ranges = at<uint2>(geom, geom_layout(P, W, H).off[GSR_GEOM_RANGES]);
-    uint64_t *keys = at<uint64_t>(binning, B.off[GSR_BIN_KEYS]);
-    uint32_t *pl = at<uint32_t>(binning, B.off[GSR_BIN_POINT_LIST]);
-    const dim3 grid(g.tiles);
-    const uint32_t m = max_tile < (uint32_t)SORT_MAX_LDS ? max_tile : (uint32_t)SORT_MAX_LDS;
-    if (m <= 256)
-        hipLaunchKernelGGL((sort_tiles_lds_kernel<256, 128>), grid, dim3(128), 0, s, ranges, keys, pl);
-    else if (m <= 1024)
-        hipLaunchKernelGGL((sort_tiles_lds_kernel<1024, 256>), grid, dim3(256), 0, s, ranges, keys, pl);
-    else if (m <= 2048)
-        hipLaunchKernelGGL((sort_tiles_lds_kernel<2048, 256>), grid, dim3(256), 0, s, ranges, keys, pl);
-    else if (m <= 4096)
-        hipLaunchKernelGGL((sort_tiles_lds_kernel<4096, 512>), grid, dim3(512), 0, s, ranges, keys, pl);
-    else
-        hipLaunchKernelGGL((sort_tiles_lds_kernel<SORT_MAX_LDS, 1024>), grid, dim3(1024), 0, s, ranges, keys, pl);
-    if (max_tile > (uint32_t)SORT_MAX_LDS)
-        hipLaunchKernelGGL(sort_tiles_big_kernel, grid, dim3(BIG_THREADS), 0, s, ranges, keys,
-                           at<uint64_t>(binning, B.tmp_keys), pl);
+    const GridDims g = grid_dims(W, H);
+    EmitArgs a;
+    a.P = P;
+    a.gx = g.gx;
+    a.order = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]);
+    a.rects = at<const uint2>(geom, L.rects);
+    a.block_prefix = at<const uint32_t>(geom, L.emit_sums);
+    // emit into the buffer pair that the tile passes will end in KEYS/POINT_LIST
+    const bool odd = tile_sort_passes(g.tiles) & 1;
+    a.tile_keys = at<uint32_t>(binning, odd ? B.keys_b : B.off[GSR_BIN_KEYS]);
+    a.ids = at<uint32_t>(binning, odd ? B.vals_b : B.off[GSR_BIN_POINT_LIST]);
+    hipLaunchKernelGGL(emit_kernel, dim3(emit_blocks(P)), dim3(EMIT_BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, hipStream_t s) {
+    const GeomLayout L = geom_layout(P, W, H);
+    const BinningLayout B = binning_layout(I, W, H);
+    const GridDims g = grid_dims(W, H);
+    const int npass = tile_sort_passes(g.tiles);
+    uint32_t *keys[2] = {at<uint32_t>(binning, B.off[GSR_BIN_KEYS]), at<uint32_t>(binning, B.keys_b)};
+    uint32_t *vals[2] = {at<uint32_t>(binning, B.off[GSR_BIN_POINT_LIST]), at<uint32_t>(binning, B.vals_b)};
+    int bits = 0;
+    while (bits < 32 && ((uint32_t)(g.tiles - 1) >> bits) != 0u) bits++;
+    int cur = npass & 1;
+    RadixPass a;
+    a.n = (uint32_t)I;
+    a.NB = radix_blocks(I, TSORT_ITEMS);
+    a.hist = at<uint32_t>(binning, B.hist);
+    a.totals = at<uint32_t>(binning, B.totals);
+    for (int p = 0; p < npass; p++) {
+        a.kin = keys[cur];
+        a.vin = vals[cur];
+        a.kout = keys[cur ^ 1];
+        a.vout = vals[cur ^ 1];
+        a.shift = RADIX_BITS * p;
+        a.nbits = min(RADIX_BITS, bits - a.shift);
+        hipError_t e = radix_pass<TSORT_ITEMS>(a, s);
+        if (e != hipSuccess) return e;
+        cur ^= 1;
+    }
+    uint2 *ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
+    hipError_t e = hipMemsetAsync(ranges, 0, (size_t)g.tiles * sizeof(uint2), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(identify_ranges_kernel, dim3((unsigned)((I + 255) / 256)), dim3(256), 0, s,
+                       (const uint32_t *)keys[0], (uint32_t)I, ranges);
     return hipGetLastError();
 }
 

@@ -19,12 +19,14 @@ constexpr int TILE_Y = 16;  // BLOCK_Y
 constexpr int TILE_PIX = TILE_X * TILE_Y;
 constexpr int WAVE = 64;
 
-// Binning: Gaussians per binning block and tile-histogram chunk (LDS words).
-constexpr int BIN_THREADS = 512;
-constexpr int BIN_MAX_BLOCKS = 256;       // one block per CU on MI355X
-constexpr int BIN_MIN_GPB = 1024;
-constexpr int BIN_TILE_CHUNK = 16384;     // 64 KiB of LDS counters per pass
-constexpr int SORT_MAX_LDS = 8192;        // tiles up to this length sort in LDS
+// Binning radix passes (binning.hip): 8-bit digits, 256-thread workgroups with
+// ITEMS keys per thread (depth sort over P: 4, tile sort over I: 8).
+constexpr int RADIX_BITS = 8;
+constexpr int RADIX = 1 << RADIX_BITS;
+constexpr int RX_THREADS = 256;
+constexpr int DSORT_ITEMS = 4;
+constexpr int TSORT_ITEMS = 8;
+constexpr int EMIT_BLOCK = 256;  // Gaussians per rank-order emit workgroup
 constexpr int PRE_THREADS = 256;          // preprocess block (scan granule)
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -40,16 +42,17 @@ __host__ __device__ inline GridDims grid_dims(int W, int H) {
     return g;
 }
 
-// Gaussians per binning block (multiple of BIN_THREADS), and number of blocks.
-__host__ __device__ inline int bin_gpb(int P) {
-    int gpb = (P + BIN_MAX_BLOCKS - 1) / BIN_MAX_BLOCKS;
-    if (gpb < BIN_MIN_GPB) gpb = BIN_MIN_GPB;
-    return (int)align_up((size_t)gpb, BIN_THREADS);
+__host__ __device__ inline int radix_blocks(int64_t n, int items) {
+    const int64_t tile = (int64_t)RX_THREADS * items;
+    const int64_t nb = (n + tile - 1) / tile;
+    return nb < 1 ? 1 : (int)nb;
 }
-__host__ __device__ inline int bin_blocks(int P) {
-    int gpb = bin_gpb(P);
-    int nb = (P + gpb - 1) / gpb;
-    return nb < 1 ? 1 : nb;
+__host__ __device__ inline int emit_blocks(int P) { return (P + EMIT_BLOCK - 1) / EMIT_BLOCK; }
+// LSD passes of the tile sort: enough 8-bit digits to cover tile indices [0, T)
+__host__ __device__ inline int tile_sort_passes(int T) {
+    int bits = 0;
+    while (bits < 32 && ((uint32_t)(T - 1) >> bits) != 0u) bits++;
+    return (bits + RADIX_BITS - 1) / RADIX_BITS;
 }
 __host__ __device__ inline int pre_blocks(int P) { return (P + PRE_THREADS - 1) / PRE_THREADS; }
 
@@ -58,16 +61,19 @@ enum CtrlWord {
     CTRL_NUM_RENDERED_LO = 0,
     CTRL_NUM_RENDERED_HI = 1,
     CTRL_PREFILTER_ERR = 2,
-    CTRL_MAX_TILE = 3,
-    CTRL_TILE_TOTAL_LO = 4,  // Σ tile counts (must equal num_rendered)
     CTRL_WORDS = 16
 };
 
 struct GeomLayout {
     size_t off[GSR_GEOM_NFIELDS];
-    size_t scan_sums;   // uint32 [pre_blocks(P)] block sums -> exclusive block prefixes
-    size_t bin_counts;  // uint32 [bin_blocks(P)][T] per (block, tile) counts -> offsets
-    size_t tile_total;  // uint32 [T]
+    size_t scan_sums;     // uint32 [pre_blocks(P)] block sums -> exclusive block prefixes
+    size_t rects;         // uint2 [P] tile rect {x0 | x1 << 16, y0 | y1 << 16}; 0 when not visible
+    size_t dsort_keys_a;  // uint32 [P] depth-sort ping-pong (the order lands in GSR_GEOM_DEPTH_ORDER)
+    size_t dsort_keys_b;
+    size_t dsort_vals_b;
+    size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, DSORT_ITEMS)]
+    size_t dsort_totals;  // uint32 [RADIX]
+    size_t emit_sums;     // uint32 [emit_blocks(P)] rank-order instance offsets per emit block
     size_t bytes;
 };
 __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
@@ -83,16 +89,25 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.off[GSR_GEOM_POINT_OFFSETS] = take((size_t)P * 4);
     L.off[GSR_GEOM_RANGES] = take((size_t)g.tiles * 8);
     L.off[GSR_GEOM_CTRL] = take(CTRL_WORDS * 4);
+    L.off[GSR_GEOM_DEPTH_ORDER] = take((size_t)P * 4);
     L.scan_sums = take((size_t)pre_blocks(P) * 4 + 4);
-    L.bin_counts = take((size_t)bin_blocks(P) * g.tiles * 4);
-    L.tile_total = take((size_t)g.tiles * 4);
+    L.rects = take((size_t)P * 8);
+    L.dsort_keys_a = take((size_t)P * 4);
+    L.dsort_keys_b = take((size_t)P * 4);
+    L.dsort_vals_b = take((size_t)P * 4);
+    L.dsort_hist = take((size_t)RADIX * radix_blocks(P, DSORT_ITEMS) * 4);
+    L.dsort_totals = take((size_t)RADIX * 4);
+    L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
     L.bytes = o;
     return L;
 }
 
 struct BinningLayout {
     size_t off[GSR_BIN_NFIELDS];
-    size_t tmp_keys;  // uint64 [I] merge scratch for tiles longer than SORT_MAX_LDS
+    size_t keys_b;  // uint32 [I] tile-sort ping-pong
+    size_t vals_b;  // uint32 [I]
+    size_t hist;    // uint32 [RADIX][radix_blocks(I, TSORT_ITEMS)]
+    size_t totals;  // uint32 [RADIX]
     size_t bytes;
 };
 __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H) {
@@ -100,9 +115,12 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H)
     size_t n = (size_t)(I > 0 ? I : 1);
     size_t o = 0;
     auto take = [&](size_t b) { size_t r = o; o = align_up(o + b, 256); return r; };
-    L.off[GSR_BIN_KEYS] = take(n * 8);
+    L.off[GSR_BIN_KEYS] = take(n * 4);
     L.off[GSR_BIN_POINT_LIST] = take(n * 4);
-    L.tmp_keys = take(n * 8);
+    L.keys_b = take(n * 4);
+    L.vals_b = take(n * 4);
+    L.hist = take((size_t)RADIX * radix_blocks((int64_t)n, TSORT_ITEMS) * 4);
+    L.totals = take((size_t)RADIX * 4);
     L.bytes = o;
     return L;
 }

@@ -14,11 +14,10 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
                                hipStream_t s);
 
 // binning.hip
-hipError_t launch_bin_count(int P, int W, int H, void *geom, const int32_t *radii, hipStream_t s);
-hipError_t launch_bin_scatter(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
-                              hipStream_t s);
-hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, uint32_t max_tile,
-                            hipStream_t s);
+hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s);
+hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
+                       hipStream_t s);
+hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, hipStream_t s);
 
 // render_fwd.hip
 hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,

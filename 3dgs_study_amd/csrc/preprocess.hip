@@ -26,6 +26,7 @@ struct PreArgs {
     float4 *splats;  // [P][3]
     uint8_t *clamped;
     uint32_t *tiles_touched;
+    uint2 *rects;  // packed tile rect per Gaussian (binning.hip)
     uint32_t *scan_sums;
     uint32_t *ctrl;
     int32_t *radii;
@@ -73,6 +74,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     uint32_t touched = 0;
     if (idx < in.P) {
         int radius_out = 0;
+        uint2 rect_out = make_uint2(0u, 0u);
         const f3 p = {in.means3D[3 * idx], in.means3D[3 * idx + 1], in.means3D[3 * idx + 2]};
         const Mat4 V = load_mat4(in.viewmatrix);
         const Mat4 Pm = load_mat4(in.projmatrix);
@@ -148,10 +150,12 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 a.clamped[idx] = clampbits;
                 radius_out = r;
                 touched = area;
+                rect_out = make_uint2(rc.x0 | (rc.x1 << 16), rc.y0 | (rc.y1 << 16));
             }
         }
         a.radii[idx] = radius_out;
         a.tiles_touched[idx] = touched;
+        a.rects[idx] = rect_out;
     }
     const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
     if (threadIdx.x == 0) a.scan_sums[blockIdx.x] = tot;
@@ -212,6 +216,7 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, h
     a.splats = at<float4>(geom, L.off[GSR_GEOM_SPLATS]);
     a.clamped = at<uint8_t>(geom, L.off[GSR_GEOM_CLAMPED]);
     a.tiles_touched = at<uint32_t>(geom, L.off[GSR_GEOM_TILES_TOUCHED]);
+    a.rects = at<uint2>(geom, L.rects);
     a.scan_sums = at<uint32_t>(geom, L.scan_sums);
     a.ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
     a.radii = radii;

@@ -51,7 +51,7 @@ EXPORTED = (
     "gsr_geom_layout", "gsr_binning_layout", "gsr_img_layout", "gsr_last_error", "gsr_abi_version",
     "gsr_timing_enable", "gsr_timing_read", "gsr_stage_name",
 )
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 
@@ -81,9 +81,9 @@ def load_library():
     lib.gsr_accum_bytes.argtypes = [i32]
     lib.gsr_accum_bytes.restype = sz
     pin = ctypes.POINTER(GsrInputs)
-    lib.gsr_forward_preprocess.argtypes = [pin, vp, vp, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_uint32), vp]
+    lib.gsr_forward_preprocess.argtypes = [pin, vp, vp, ctypes.POINTER(i64), vp]
     lib.gsr_forward_preprocess.restype = ctypes.c_int
-    lib.gsr_forward_render.argtypes = [pin, vp, vp, vp, i64, ctypes.c_uint32, vp, vp, vp]
+    lib.gsr_forward_render.argtypes = [pin, vp, vp, vp, i64, vp, vp, vp]
     lib.gsr_forward_render.restype = ctypes.c_int
     lib.gsr_backward.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward.restype = ctypes.c_int
@@ -178,12 +178,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     img = torch.empty((lib.gsr_img_bytes(W, H),), **u8)
     stream = _stream(device)
     num_rendered = ctypes.c_int64(0)
-    max_tile = ctypes.c_uint32(0)
     _check(lib.gsr_forward_preprocess(ctypes.byref(s), geom.data_ptr(), _ptr(radii), ctypes.byref(num_rendered),
-                                      ctypes.byref(max_tile), stream), "rasterize_gaussians (preprocess)")
+                                      stream), "rasterize_gaussians (preprocess)")
     binning = torch.empty((lib.gsr_binning_bytes(num_rendered.value, W, H),), **u8)
     _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
-                                  num_rendered.value, max_tile.value, _ptr(radii), out_color.data_ptr(), stream),
+                                  num_rendered.value, _ptr(radii), out_color.data_ptr(), stream),
            "rasterize_gaussians (render)")
     return num_rendered.value, out_color, radii, geom, binning, img
 
@@ -236,8 +235,18 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 
 
 # ------------------------------------------------------------------ timing hooks
-def timing_enable(on: bool = True):
-    load_library().gsr_timing_enable(int(on))
+def timing_enable(on=True):
+    """Start per-stage event timing: True = every stage, False = off, or an
+    iterable of stage names (only those stages get events)."""
+    lib = load_library()
+    if isinstance(on, bool):
+        mask = -1 if on else 0
+    else:
+        names = [lib.gsr_stage_name(i).decode() for i in range(16)]
+        mask = 0
+        for n in on:
+            mask |= 1 << names.index(n)
+    lib.gsr_timing_enable(mask)
 
 
 def timing_read() -> dict:
@@ -261,6 +270,7 @@ def layouts(P, W, H, num_rendered):
     nb = lib.gsr_binning_layout(num_rendered, W, H, b, 16)
     im = (ctypes.c_size_t * 16)()
     ni = lib.gsr_img_layout(W, H, im, 16)
-    geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "point_offsets", "ranges", "ctrl")
+    geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "point_offsets", "ranges", "ctrl",
+                  "depth_order")
     return (dict(zip(geom_names, list(g)[:n])), dict(zip(("keys", "point_list"), list(b)[:nb])),
             dict(zip(("final_T", "n_contrib", "tile_max_contrib"), list(im)[:ni])))

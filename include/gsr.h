@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 1
+#define GSR_ABI_VERSION 2
 
 enum gsr_status {
     GSR_OK = 0,
@@ -90,18 +90,17 @@ size_t gsr_img_bytes(int32_t W, int32_t H);
 size_t gsr_accum_bytes(int32_t P);
 
 /* Replaces the first half of RasterizeGaussiansCUDA -> Rasterizer::forward
- * (preprocess + InclusiveSum + the num_rendered cudaMemcpy), and also runs the
- * per-tile counting that yields the tile ranges (identifyTileRanges' output).
- * Writes radii [P] int32, *num_rendered and *max_tile_len (host pointers;
- * max_tile_len may be NULL). */
-int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered,
-                           uint32_t *max_tile_len, void *stream);
+ * (preprocess + InclusiveSum + the num_rendered cudaMemcpy).  While the host
+ * waits for num_rendered the device also sorts the P Gaussians by depth (the
+ * first half of the binning, see 3dgs_study_amd/csrc/binning.hip).
+ * Writes radii [P] int32 and *num_rendered (host pointer). */
+int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered, void *stream);
 
 /* Replaces the second half of Rasterizer::forward (duplicateWithKeys,
- * SortPairs, FORWARD::render).  out_color is [3,H,W]; radii as written by
- * gsr_forward_preprocess; max_tile_len as returned by it. */
+ * SortPairs, identifyTileRanges, FORWARD::render).  out_color is [3,H,W];
+ * radii as written by gsr_forward_preprocess. */
 int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
-                       uint32_t max_tile_len, const int32_t *radii, float *out_color, void *stream);
+                       const int32_t *radii, float *out_color, void *stream);
 
 /* Replaces RasterizeGaussiansBackwardCUDA -> Rasterizer::backward.
  * Every output is fully written (no pre-zeroing needed); dsh may be NULL when
@@ -128,11 +127,12 @@ enum gsr_geom_field {
     GSR_GEOM_TILES_TOUCHED,  /* uint32 [P] */
     GSR_GEOM_POINT_OFFSETS,  /* uint32 [P]  inclusive scan of tiles_touched */
     GSR_GEOM_RANGES,         /* uint2  [T]  [start,end) of each tile in point_list */
-    GSR_GEOM_CTRL,           /* uint32 [16] num_rendered, status flags, max tile length */
+    GSR_GEOM_CTRL,           /* uint32 [16] num_rendered, status flags */
+    GSR_GEOM_DEPTH_ORDER,    /* uint32 [P]  Gaussian ids in (depth_bits, id) order */
     GSR_GEOM_NFIELDS
 };
 enum gsr_binning_field {
-    GSR_BIN_KEYS = 0,        /* uint64 [I]  per-tile bucketed (depth_bits<<32 | id), sorted in place */
+    GSR_BIN_KEYS = 0,        /* uint32 [I]  tile index of each point_list entry (sorted) */
     GSR_BIN_POINT_LIST,      /* uint32 [I]  Gaussian ids in (tile, depth, id) order */
     GSR_BIN_NFIELDS
 };
@@ -147,22 +147,23 @@ int gsr_binning_layout(int64_t num_rendered, int32_t W, int32_t H, size_t *offse
 int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap);
 
 /* Per-stage device timing (HIP events on the launch stream), for benchmarks.
- * gsr_timing_enable(1) resets the accumulators and starts recording;
+ * gsr_timing_enable(mask) resets the accumulators and starts recording the
+ * stages whose bit (1 << stage) is set in mask (-1: all; 0: off);
  * gsr_timing_read() waits for the recorded events and returns, per stage,
  * the summed milliseconds and the launch count (returns the number of stages,
  * negative on error).  A stage is one launch_* group of kernels. */
 enum gsr_stage {
     GSR_STAGE_PREPROCESS = 0, /* FORWARD::preprocessCUDA */
     GSR_STAGE_SCAN,           /* InclusiveSum of tiles_touched */
-    GSR_STAGE_TILE_COUNT,     /* per-tile counts + ranges (identifyTileRanges output) */
-    GSR_STAGE_TILE_SCATTER,   /* duplicateWithKeys into tile buckets */
-    GSR_STAGE_TILE_SORT,      /* per-tile depth sort (SortPairs) */
+    GSR_STAGE_DEPTH_SORT,     /* stable sort of the P depths + rank-order instance offsets */
+    GSR_STAGE_DUPLICATE,      /* duplicateWithKeys in depth order */
+    GSR_STAGE_TILE_SORT,      /* stable sort by tile (SortPairs) + identifyTileRanges */
     GSR_STAGE_RENDER_FWD,     /* FORWARD::renderCUDA */
     GSR_STAGE_RENDER_BWD,     /* BACKWARD::renderCUDA */
     GSR_STAGE_PREPROCESS_BWD, /* BACKWARD::computeCov2DCUDA + preprocessCUDA */
     GSR_STAGE_COUNT
 };
-int gsr_timing_enable(int on);
+int gsr_timing_enable(int mask);
 int gsr_timing_read(double *total_ms, int64_t *launches, int cap);
 const char *gsr_stage_name(int stage);
 

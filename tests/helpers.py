@@ -83,11 +83,12 @@ def read_intermediates(geom, binning, img, P, W, H, I):
     d["tiles_touched"] = _view(geom, go["tiles_touched"], P, torch.int32, np.uint32)
     d["point_offsets"] = _view(geom, go["point_offsets"], P, torch.int32, np.uint32)
     d["ranges"] = _view(geom, go["ranges"], 2 * T, torch.int32, np.uint32).reshape(T, 2)
+    d["depth_order"] = _view(geom, go["depth_order"], P, torch.int32, np.uint32)
     if I > 0:
-        d["keys"] = _view(binning, bo["keys"], I, torch.int64, np.uint64)
+        d["keys"] = _view(binning, bo["keys"], I, torch.int32, np.uint32)
         d["point_list"] = _view(binning, bo["point_list"], I, torch.int32, np.uint32)
     else:
-        d["keys"] = np.zeros(0, np.uint64)
+        d["keys"] = np.zeros(0, np.uint32)
         d["point_list"] = np.zeros(0, np.uint32)
     d["final_T"] = _view(img, io["final_T"], W * H, torch.float32, np.float32).reshape(H, W)
     d["n_contrib"] = _view(img, io["n_contrib"], W * H, torch.int32, np.uint32).reshape(H, W)

@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 1
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 2
     # 10 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 40 + 11 * 8
     assert _C.GsrInputs.bg.offset == 40
@@ -82,7 +82,7 @@ def _inputs(**kw):
 def test_argument_validation_mirrors_upstream_errors(lib, kw, msg):
     s = _inputs(**kw)
     n = ctypes.c_int64(-1)
-    rc = lib.gsr_forward_preprocess(ctypes.byref(s), None, None, ctypes.byref(n), None, None)
+    rc = lib.gsr_forward_preprocess(ctypes.byref(s), None, None, ctypes.byref(n), None)
     assert rc != 0
     assert msg in lib.gsr_last_error().decode()
 
@@ -90,9 +90,8 @@ def test_argument_validation_mirrors_upstream_errors(lib, kw, msg):
 def test_zero_gaussians_is_a_host_side_no_op(lib):
     s = _inputs(P=0)
     n = ctypes.c_int64(-1)
-    mt = ctypes.c_uint32(7)
-    assert lib.gsr_forward_preprocess(ctypes.byref(s), None, None, ctypes.byref(n), ctypes.byref(mt), None) == 0
-    assert n.value == 0 and mt.value == 0
+    assert lib.gsr_forward_preprocess(ctypes.byref(s), None, None, ctypes.byref(n), None) == 0
+    assert n.value == 0
     assert lib.gsr_backward(ctypes.byref(s), None, None, None, None, 0, *([None] * 11)) == 0
     assert lib.gsr_mark_visible(0, None, None, None, None, None) == 0
 
@@ -101,7 +100,7 @@ def test_stage_names(lib):
     from diff_gaussian_rasterization import _C
 
     names = [lib.gsr_stage_name(i).decode() for i in range(8)]
-    assert names == ["preprocess", "scan", "tile_count", "tile_scatter", "tile_sort", "render_fwd", "render_bwd",
+    assert names == ["preprocess", "scan", "depth_sort", "duplicate", "tile_sort", "render_fwd", "render_bwd",
                      "preprocess_bwd"]
     assert lib.gsr_stage_name(99).decode() == ""
     _C.timing_enable(True)

@@ -42,9 +42,15 @@ def check_forward(h, r, rgb_from_sh=True, ncontrib_frac=0.999):
     np.testing.assert_array_equal(h["ranges"], r["ranges"])
     np.testing.assert_array_equal(h["point_list"], r["point_list"])
     if h["num_rendered"]:
-        hk = h["keys"]
-        np.testing.assert_array_equal((hk & 0xFFFFFFFF).astype(np.uint32), r["point_list"])
-        np.testing.assert_array_equal((hk >> 32).astype(np.uint32), (r["keys"] & 0xFFFFFFFF).astype(np.uint32))
+        # sorted tile index of every entry == the tile half of upstream's sorted 64-bit keys
+        np.testing.assert_array_equal(h["keys"], (r["keys"] >> 32).astype(np.uint32))
+    # depth order: the visible Gaussians appear in (depth_bits, index) order
+    order = h["depth_order"]
+    assert np.array_equal(np.sort(order), np.arange(order.size, dtype=np.uint32))
+    vis_order = order[vis[order]]
+    dbits = r["depths"].view(np.uint32)
+    expect = np.lexsort((np.nonzero(vis)[0], dbits[vis]))
+    np.testing.assert_array_equal(vis_order, np.nonzero(vis)[0][expect])
     err = np.abs(h["color"] - r["color"]).max()
     assert err <= IMG_TOL, f"image max abs err {err}"
     terr = np.abs(h["final_T"] - r["final_T"]).max()

@@ -19,7 +19,7 @@ for f in sorted(glob.glob(str(d / "**" / "*counter_collection.csv"), recursive=T
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 STAGE = {"gsr::preprocess_fwd_kernel": "preprocess", "gsr::render_fwd_kernel": "render_fwd",
          "gsr::render_bwd_kernel": "render_bwd", "gsr::preprocess_bwd_kernel": "preprocess_bwd",
-         "gsr::bin_scatter_kernel": "tile_scatter"}
+         "gsr::emit_kernel": "duplicate"}
 summary = {"note": "per-dispatch means; hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE "
                    "counts half of wide streaming reads, MI355X_MICROARCH.md §HBM)", "kernels": {}, "stages": {}}
 for k, cs in sorted(vals.items()):
