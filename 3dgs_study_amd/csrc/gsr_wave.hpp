@@ -10,6 +10,8 @@
 namespace gsr {
 
 // DPP control codes (GFX9 encoding)
+constexpr int DPP_ROW_SHL1 = 0x101;
+constexpr int DPP_ROW_SHL2 = 0x102;
 constexpr int DPP_ROW_SHR1 = 0x111;
 constexpr int DPP_ROW_SHR2 = 0x112;
 constexpr int DPP_ROW_SHR3 = 0x113;

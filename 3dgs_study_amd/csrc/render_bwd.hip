@@ -10,11 +10,13 @@
 // wave starts at the largest n_contrib among its own 64 pixels (entries past it
 // are skipped by every pixel), streams 64-entry chunks backwards with the same
 // lane-parallel exact cull as the forward, and walks the surviving Gaussians
-// from the back.  Upstream issues ~9 float atomics per contributing
-// (pixel, Gaussian) pair; here the 9 partials are summed over the wave's 64
-// pixels by a reduce-scatter (v_permlane32_swap, v_permlane16_swap, then DPP row
-// shifts: 28 VALU for all nine sums instead of 63) and ONE 9-lane atomic
-// wave-instruction adds them to the Gaussian's 64-byte accumulator row.
+// from the back, two Gaussians per iteration.  Upstream issues ~9 float atomics
+// per contributing (pixel, Gaussian) pair; here the 2 x 9 partials are summed
+// over the wave's 64 pixels by one reduce-scatter (v_permlane32_swap,
+// v_permlane16_swap, DPP row shifts: ~25 VALU per Gaussian) and ONE 9-lane
+// atomic wave-instruction per Gaussian adds them to its 64-byte accumulator
+// row — a single memory-side atomic request, the resource that bounds this
+// kernel (MI355X_MICROARCH.md §Global float atomics: ~20 G requests/s).
 #include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
 
@@ -77,7 +79,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         dpx2 = a.dL_dpix[2 * HW + pix];
     }
     const float bg_dot = a.bg[0] * dpx0 + a.bg[1] * dpx1 + a.bg[2] * dpx2;
-    const float ddelx_dx = 0.5f * (float)a.W, ddely_dy = 0.5f * (float)a.H;
+    const float nTbg = -T_final * bg_dot;
+    const float nhx = -0.5f * (float)a.W, nhy = -0.5f * (float)a.H;  // -ddelx_dx, -ddely_dy
     int end = last_contrib;  // wave max: the first (from the back) entry any pixel replays
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) end = max(end, __shfl_xor(end, o));
@@ -87,80 +90,127 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     ChunkStage &st = stage[w];
     float T = T_final;
     float R0 = 0.f, R1 = 0.f, R2 = 0.f;
-    const bool row_last = (lane & 15) == 15;
-    // accumulator slot of the sum each row-last lane holds: lanes 15/31/47/63 -> +0/+2/+1/+3
-    const int slot = ((lane >> 4) & 1) * 2 + (lane >> 5);
     const uint32_t *list = a.point_list + r.x;
 
-    // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l).
+    // After the paired reduce-scatter below the 18 sums sit in the row-last lanes
+    // (15/31/47/63, row rr = lane >> 4) of five registers.  Two DPP row shifts
+    // gather each Gaussian's nine sums into ONE register (lanes 13-15 of the
+    // rows), so each Gaussian costs one atomic wave-instruction: nine lanes into
+    // one 64-B accumulator row = ONE memory-side atomic request (the chip-wide
+    // atomic request rate, not VALU, bounds this kernel).
+    const int rr = lane >> 4, rl = lane & 15;
+    const bool act_a = rl == 15 || rl == 14 || lane == 13;
+    const int slot_a = rl == 15 ? (rr & 1) * 2 + (rr >> 1)          // k0: a0 a2 a1 a3
+                     : rl == 14 ? 4 + (rr & 1) * 2 + (rr >> 1)      // k1: a4 a6 a5 a7
+                                : 8;                                // k2 row 0: a8
+    const bool act_b = rl == 15 || (rl == 14 && rr != 0) || (rl == 13 && !(rr & 1));
+    const int slot_b = rl == 15 ? 2 + (rr & 1) * 2 + (rr >> 1)      // k3: b2 b4 b3 b5
+                     : rl == 14 ? (rr == 1 ? 0 : (rr == 2 ? 8 : 1)) // k2 rows 1-3: b0 b8 b1
+                                : (rr == 0 ? 6 : 7);                // k4 rows 0, 2: b6 b7
+
+    struct Pre {
+        float dx, dy, ux, uy, G, alpha;
+        bool valid;
+    };
+    auto prepare = [&](float4 p0, float4 p1, int entry, bool live) {
+        Pre q;
+        q.dx = p0.x - fx;
+        q.dy = p0.y - fy;
+        q.ux = p0.z * q.dx + p0.w * q.dy;  // conic * d
+        q.uy = p0.w * q.dx + p1.x * q.dy;
+        const float power = -0.5f * (q.dx * q.ux + q.dy * q.uy);  // == render_fwd.hip, bit for bit
+        q.G = __expf(power);
+        q.alpha = fminf(0.99f, p1.y * q.G);
+        q.valid = live && entry < last_contrib && !(power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
+        return q;
+    };
+    struct G9 {
+        float g0, g1, g2, g3, g4, g5, g6, g7, g8;
+    };
+    // Branch-free replay step: a skipped pixel sees alpha = 0 (T and the running
+    // colour R unchanged) and zero gradients.  R is upstream's accum_rec advanced
+    // eagerly: after a blended Gaussian it already holds
+    // last_alpha * last_color + (1 - last_alpha) * accum_rec.
+    auto replay = [&](const Pre &q, float op, float cr, float cg, float cb) {
+        const float av = q.valid ? q.alpha : 0.0f;
+        const float Gv = q.valid ? q.G : 0.0f;
+        const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
+        T = T * inv_1ma;
+        const float dchannel_dcolor = av * T;
+        const float e0 = cr - R0, e1 = cg - R1, e2 = cb - R2;
+        const float dot = e0 * dpx0 + e1 * dpx1 + e2 * dpx2;
+        R0 += av * e0;
+        R1 += av * e1;
+        R2 += av * e2;
+        // dL/dalpha (upstream: sum_c (c - accum_rec) dL_dpix_c * T - T_final/(1-alpha) * bg.dL_dpix)
+        const float dL_dalpha = q.valid ? dot * T + inv_1ma * nTbg : 0.0f;
+        // dG/d(delta) = -G conic d; with W = G * opacity * dL/dalpha:
+        //   dmean2D = -W (conic d) * (W/2, H/2),  dconic = -W/2 (dx^2, dx dy, dy^2)
+        const float Wg = Gv * op * dL_dalpha;
+        const float hw = -0.5f * Wg;
+        const float hdx = hw * q.dx;
+        G9 g;
+        g.g0 = q.ux * (Wg * nhx);
+        g.g1 = q.uy * (Wg * nhy);
+        g.g2 = hdx * q.dx;
+        g.g3 = hdx * q.dy;
+        g.g4 = hw * q.dy * q.dy;
+        g.g5 = Gv * dL_dalpha;
+        g.g6 = dchannel_dcolor * dpx0;
+        g.g7 = dchannel_dcolor * dpx1;
+        g.g8 = dchannel_dcolor * dpx2;
+        return g;
+    };
+
+    // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l),
+    // two Gaussians per iteration: independent LDS reads and exps (ILP), one
+    // fused reduce-scatter of their 18 sums (no half-empty permlane32 stage).
     auto replay_chunk = [&](int lo, float4 A, float4 B, float4 C) {
         stage_chunk(st, lane, A, B, C);
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         uint64_t mask = __ballot(rel);
         while (mask) {
-            const int k = 63 - __builtin_clzll(mask);
-            mask &= ~(1ull << k);
-            const int entry = lo + k;  // upstream `contributor` for this entry
-            const float4 p0 = st.rec[k][0], p1 = st.rec[k][1];
-            const float2 p2 = *reinterpret_cast<const float2 *>(&st.rec[k][2]);
-            const float gx_ = p0.x, gy_ = p0.y, cx = p0.z, cy = p0.w;
-            const float cz = p1.x, op = p1.y;
-            const float dx = gx_ - fx, dy = gy_ - fy;
-            const float power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-            const float G = __expf(power);
-            const float alpha = fminf(0.99f, op * G);
-            const bool valid = entry < last_contrib && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-            if (!__any(valid)) continue;
-            const float cr = p1.z, cg = p1.w, cb = p2.x;
-            const uint32_t gid = __float_as_uint(p2.y);
-            // Branch-free replay step: a skipped pixel sees alpha = 0 (T and the
-            // running colour R unchanged) and zero gradients.  R is upstream's
-            // accum_rec advanced eagerly: after a blended Gaussian it already holds
-            // last_alpha * last_color + (1 - last_alpha) * accum_rec.
-            const float av = valid ? alpha : 0.0f;
-            const float Gv = valid ? G : 0.0f;
-            const float om = 1.f - av;
-            const float inv_1ma = __builtin_amdgcn_rcpf(om);
-            T = T * inv_1ma;
-            const float dchannel_dcolor = av * T;
-            const float e0 = cr - R0, e1 = cg - R1, e2 = cb - R2;
-            const float dot = e0 * dpx0 + e1 * dpx1 + e2 * dpx2;
-            R0 = av * cr + om * R0;
-            R1 = av * cg + om * R1;
-            R2 = av * cb + om * R2;
-            const float dL_dalpha = valid ? dot * T + (-T_final * inv_1ma) * bg_dot : 0.0f;
-            const float g6 = dchannel_dcolor * dpx0;
-            const float g7 = dchannel_dcolor * dpx1;
-            const float g8 = dchannel_dcolor * dpx2;
-            const float dL_dG = op * dL_dalpha;
-            const float gdx = Gv * dx, gdy = Gv * dy;
-            const float dG_ddelx = -gdx * cx - gdy * cy;
-            const float dG_ddely = -gdy * cz - gdx * cy;
-            const float g0 = dL_dG * dG_ddelx * ddelx_dx;
-            const float g1 = dL_dG * dG_ddely * ddely_dy;
-            const float hG = -0.5f * dL_dG;
-            const float g2 = gdx * dx * hG;
-            const float g3 = gdx * dy * hG;
-            const float g4 = gdy * dy * hG;
-            const float g5 = Gv * dL_dalpha;
-            // reduce-scatter of the nine sums over 64 lanes (convergent: all lanes active)
-            const float h0 = swap32_sum(g0, g1);  // lanes 0-31: g0, 32-63: g1
-            const float h1 = swap32_sum(g2, g3);
-            const float h2 = swap32_sum(g4, g5);
-            const float h3 = swap32_sum(g6, g7);
-            const float h4 = swap32_sum(g8, 0.f);
-            const float k0 = row_sum_to_lane15(swap16_sum(h0, h1));   // lanes 15/31/47/63: g0 g2 g1 g3
-            const float k1 = row_sum_to_lane15(swap16_sum(h2, h3));   //                    g4 g6 g5 g7
-            const float k2 = row_sum_to_lane15(swap16_sum(h4, 0.f));  //                    g8
-            // three atomic wave-instructions straight from the lanes holding the sums
-            // (uniform row base in SGPRs, per-lane slot offset), no gather into lanes 0-8
-            float *row = a.accum + (size_t)gid * ACCUM_STRIDE;
-            if (row_last) {
-                atomicAdd(row + slot, k0);
-                atomicAdd(row + slot + 4, k1);
-                if (lane == 15) atomicAdd(row + slot + 8, k2);  // slot = 0 here; a lane-dependent
-                // address keeps the compiler's atomic optimizer (a wave-scan loop) out
-            }
+            const int ka = 63 - __builtin_clzll(mask);
+            mask ^= 1ull << ka;
+            const bool two = mask != 0;  // wave-uniform
+            const int kb = two ? 63 - __builtin_clzll(mask) : ka;
+            if (two) mask ^= 1ull << kb;
+            const float4 a0 = st.rec[ka][0], a1 = st.rec[ka][1];
+            const float4 b0 = st.rec[kb][0], b1 = st.rec[kb][1];
+            const float2 a2 = *reinterpret_cast<const float2 *>(&st.rec[ka][2]);
+            const float2 b2 = *reinterpret_cast<const float2 *>(&st.rec[kb][2]);
+            const Pre qa = prepare(a0, a1, lo + ka, true);  // entry index = upstream `contributor`
+            const Pre qb = prepare(b0, b1, lo + kb, two);
+            if (!__any(qa.valid || qb.valid)) continue;
+            const G9 ga = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: ka > kb
+            const G9 gb = replay(qb, b1.y, b1.z, b1.w, b2.x);
+            // reduce-scatter of the 18 sums over 64 lanes (convergent: all lanes active)
+            const float h0 = swap32_sum(ga.g0, ga.g1);  // lanes 0-31: first, 32-63: second
+            const float h1 = swap32_sum(ga.g2, ga.g3);
+            const float h2 = swap32_sum(ga.g4, ga.g5);
+            const float h3 = swap32_sum(ga.g6, ga.g7);
+            const float h4 = swap32_sum(ga.g8, gb.g8);
+            const float h5 = swap32_sum(gb.g0, gb.g1);
+            const float h6 = swap32_sum(gb.g2, gb.g3);
+            const float h7 = swap32_sum(gb.g4, gb.g5);
+            const float h8 = swap32_sum(gb.g6, gb.g7);
+            const float k0 = row_sum_to_lane15(swap16_sum(h0, h1));   // lanes 15/31/47/63: a0 a2 a1 a3
+            const float k1 = row_sum_to_lane15(swap16_sum(h2, h3));   //                    a4 a6 a5 a7
+            const float k2 = row_sum_to_lane15(swap16_sum(h4, h5));   //                    a8 b0 b8 b1
+            const float k3 = row_sum_to_lane15(swap16_sum(h6, h7));   //                    b2 b4 b3 b5
+            const float k4 = row_sum_to_lane15(swap16_sum(h8, 0.f));  //                    b6 -  b7 -
+            const float k1s = dpp_f32<DPP_ROW_SHL1>(k1);  // lane 14 of each row <- lane 15
+            const float k2s1 = dpp_f32<DPP_ROW_SHL1>(k2);
+            const float k2s2 = dpp_f32<DPP_ROW_SHL2>(k2);  // lane 13 of each row <- lane 15
+            const float k4s = dpp_f32<DPP_ROW_SHL2>(k4);
+            const float va = rl == 15 ? k0 : (rl == 14 ? k1s : k2s2);
+            const float vb = rl == 15 ? k3 : (rl == 14 ? k2s1 : k4s);
+            // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
+            // compiler's atomic optimizer (a wave-scan loop) out
+            const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.y));
+            const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.y));
+            if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, va);
+            if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, vb);
         }
     };
     // Double-buffered backwards stream, unrolled by two so the buffers swap roles

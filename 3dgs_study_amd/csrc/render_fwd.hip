@@ -57,29 +57,48 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
             stage_chunk(st, lane, A, B, C);
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
             uint64_t mask = __ballot(rel);
+            // Two Gaussians per iteration: their LDS reads, powers and exps are
+            // independent, so each wave has twice the instruction-level parallelism
+            // to cover LDS and transcendental latency; only the T recurrence is serial.
             while (mask) {
-                const int k = __builtin_ctzll(mask);
+                const int ka = __builtin_ctzll(mask);
                 mask &= mask - 1;
-                const float4 p0 = st.rec[k][0], p1 = st.rec[k][1];
-                const float cb = st.rec[k][2].x;
-                const float gx_ = p0.x, gy_ = p0.y, cx = p0.z, cy = p0.w;
-                const float cz = p1.x, op = p1.y, cr = p1.z, cg = p1.w;
-                // branch-free per-pixel step (selects, not exec-mask branches: the
-                // loop is VALU-issue bound and every branch costs SALU + exec traffic)
-                const float dx = gx_ - fx, dy = gy_ - fy;
-                const float power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-                const float alpha = fminf(0.99f, op * __expf(power));
-                const float test_T = T * (1 - alpha);
-                const bool ok = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const bool sat = ok && test_T < 0.0001f;  // this Gaussian is not blended
-                const bool blend = ok && !sat;
-                done = done || sat;
-                const float wgt = blend ? alpha * T : 0.0f;
-                C0 += cr * wgt;
-                C1 += cg * wgt;
-                C2 += cb * wgt;
-                T = blend ? test_T : T;
-                last = blend ? (uint32_t)(pos + k + 1) : last;
+                const bool two = mask != 0;  // wave-uniform
+                const int kb = two ? __builtin_ctzll(mask) : ka;
+                mask &= mask - 1;
+                const float4 a0 = st.rec[ka][0], a1 = st.rec[ka][1];
+                const float4 b0 = st.rec[kb][0], b1 = st.rec[kb][1];
+                const float acb = st.rec[ka][2].x, bcb = st.rec[kb][2].x;
+                float pa, pb, alpha_a, alpha_b;
+                {
+                    const float dx = a0.x - fx, dy = a0.y - fy;
+                    const float ux = a0.z * dx + a0.w * dy, uy = a0.w * dx + a1.x * dy;  // conic * d
+                    pa = -0.5f * (dx * ux + dy * uy);  // render_bwd.hip recomputes it identically
+                    alpha_a = fminf(0.99f, a1.y * __expf(pa));
+                }
+                {
+                    const float dx = b0.x - fx, dy = b0.y - fy;
+                    const float ux = b0.z * dx + b0.w * dy, uy = b0.w * dx + b1.x * dy;
+                    pb = -0.5f * (dx * ux + dy * uy);
+                    alpha_b = fminf(0.99f, b1.y * __expf(pb));
+                }
+                // upstream's front-to-back step, branch-free (selects, not exec-mask
+                // branches): skip power > 0 and alpha < 1/255, stop before T < 1e-4
+                auto step = [&](bool live, float power, float alpha, float cr, float cg, float cb, int k) {
+                    const float test_T = T * (1 - alpha);
+                    const bool ok = live && !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                    const bool sat = ok && test_T < 0.0001f;  // this Gaussian is not blended
+                    const bool blend = ok && !sat;
+                    done = done || sat;
+                    const float wgt = blend ? alpha * T : 0.0f;
+                    C0 += cr * wgt;
+                    C1 += cg * wgt;
+                    C2 += cb * wgt;
+                    T = blend ? test_T : T;
+                    last = blend ? (uint32_t)(pos + k + 1) : last;
+                };
+                step(true, pa, alpha_a, a1.z, a1.w, acb, ka);
+                step(two, pb, alpha_b, b1.z, b1.w, bcb, kb);
                 if (!__any(!done)) return true;
             }
             return false;
