@@ -32,13 +32,27 @@ __device__ inline void rows_to_lds(const float *__restrict__ src, int g0, int n,
     if ((((uintptr_t)base) & 15u) == 0) {
         const float4 *b4 = reinterpret_cast<const float4 *>(base);
         const int n4 = total >> 2;
-        for (int i = threadIdx.x; i < n4; i += THREADS) {
-            const float4 v = b4[i];
-            const int e = i << 2;
-            lds[lds_row_index(e, RW, invRW)] = v.x;
-            lds[lds_row_index(e + 1, RW, invRW)] = v.y;
-            lds[lds_row_index(e + 2, RW, invRW)] = v.z;
-            lds[lds_row_index(e + 3, RW, invRW)] = v.w;
+        // batches of BATCH loads in flight per lane before the first LDS store
+        // (a load-store-load loop would expose the full HBM latency per float4)
+        constexpr int BATCH = 12;
+        for (int i0 = threadIdx.x; i0 < n4; i0 += THREADS * BATCH) {
+            float4 v[BATCH];
+#pragma unroll
+            for (int b = 0; b < BATCH; b++) {
+                const int i = i0 + b * THREADS;
+                if (i < n4) v[b] = b4[i];
+            }
+#pragma unroll
+            for (int b = 0; b < BATCH; b++) {
+                const int i = i0 + b * THREADS;
+                if (i < n4) {
+                    const int e = i << 2;
+                    lds[lds_row_index(e, RW, invRW)] = v[b].x;
+                    lds[lds_row_index(e + 1, RW, invRW)] = v[b].y;
+                    lds[lds_row_index(e + 2, RW, invRW)] = v[b].z;
+                    lds[lds_row_index(e + 3, RW, invRW)] = v[b].w;
+                }
+            }
         }
         for (int e = (n4 << 2) + threadIdx.x; e < total; e += THREADS) lds[lds_row_index(e, RW, invRW)] = base[e];
     } else {
