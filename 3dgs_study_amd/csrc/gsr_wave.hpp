@@ -10,6 +10,10 @@
 namespace gsr {
 
 // DPP control codes (GFX9 encoding)
+constexpr int DPP_QUAD_XOR1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
+constexpr int DPP_ROW_ROR8 = 0x128;
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;
 constexpr int DPP_ROW_SHL1 = 0x101;
 constexpr int DPP_ROW_SHL2 = 0x102;
 constexpr int DPP_ROW_SHR1 = 0x111;

@@ -92,27 +92,33 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     float R0 = 0.f, R1 = 0.f, R2 = 0.f;
     const uint32_t *list = a.point_list + r.x;
 
-    // After the paired reduce-scatter below the 18 sums sit in the row-last lanes
-    // (15/31/47/63, row rr = lane >> 4) of five registers.  Two DPP row shifts
-    // gather each Gaussian's nine sums into ONE register (lanes 13-15 of the
-    // rows), so each Gaussian costs one atomic wave-instruction: nine lanes into
-    // one 64-B accumulator row = ONE memory-side atomic request (the chip-wide
-    // atomic request rate, not VALU, bounds this kernel).
-    const int rr = lane >> 4, rl = lane & 15;
-    const bool act_a = rl == 15 || rl == 14 || lane == 13;
-    const int slot_a = rl == 15 ? (rr & 1) * 2 + (rr >> 1)          // k0: a0 a2 a1 a3
-                     : rl == 14 ? 4 + (rr & 1) * 2 + (rr >> 1)      // k1: a4 a6 a5 a7
-                                : 8;                                // k2 row 0: a8
-    const bool act_b = rl == 15 || (rl == 14 && rr != 0) || (rl == 13 && !(rr & 1));
-    const int slot_b = rl == 15 ? 2 + (rr & 1) * 2 + (rr >> 1)      // k3: b2 b4 b3 b5
-                     : rl == 14 ? (rr == 1 ? 0 : (rr == 2 ? 8 : 1)) // k2 rows 1-3: b0 b8 b1
-                                : (rr == 0 ? 6 : 7);                // k4 rows 0, 2: b6 b7
+    // The paired reduce-scatter below leaves Gaussian a's nine sums in lanes
+    // {0,32,16,48,8,40,24,56,4} (slots 0..8) and b's in {20,52,12,44,28,60,2,34,36}
+    // of ONE register, so each Gaussian costs one atomic wave-instruction: nine
+    // lanes into one 64-B accumulator row = one memory-side atomic request.
+    // (Derived by simulating the six exchange stages; tests/test_gpu_parity.py
+    // checks every gradient.)
+    int slot_a = -1, slot_b = -1;
+    {
+        constexpr int8_t LA[9] = {0, 32, 16, 48, 8, 40, 24, 56, 4};
+        constexpr int8_t LB[9] = {20, 52, 12, 44, 28, 60, 2, 34, 36};
+#pragma unroll
+        for (int j = 0; j < 9; j++) {
+            slot_a = lane == LA[j] ? j : slot_a;
+            slot_b = lane == LB[j] ? j : slot_b;
+        }
+    }
+    const bool act_a = slot_a >= 0, act_b = slot_b >= 0;
+    // one reduce-scatter step inside a row: lanes with `bit` clear keep c, the
+    // others d; each adds the partner's copy (DPP pattern CTRL pairs the lanes)
+    auto rs_keep = [&](float c, float d, int bit) { return (lane & bit) ? d : c; };
+    auto rs_send = [&](float c, float d, int bit) { return (lane & bit) ? c : d; };
 
     struct Pre {
         float dx, dy, ux, uy, G, alpha;
         bool valid;
     };
-    auto prepare = [&](float4 p0, float4 p1, int entry, bool live) {
+    auto prepare = [&](float4 p0, float4 p1, int k, int lim, bool live) {  // valid needs lo + k < last_contrib
         Pre q;
         q.dx = p0.x - fx;
         q.dy = p0.y - fy;
@@ -121,7 +127,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         const float power = -0.5f * (q.dx * q.ux + q.dy * q.uy);  // == render_fwd.hip, bit for bit
         q.G = __expf(power);
         q.alpha = fminf(0.99f, p1.y * q.G);
-        q.valid = live && entry < last_contrib && !(power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
+        q.valid = live && k < lim && !(power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
         return q;
     };
     struct G9 {
@@ -169,6 +175,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         stage_chunk(st, lane, A, B, C);
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         uint64_t mask = __ballot(rel);
+        const int lim = last_contrib - lo;  // entry lo + k replays for this pixel iff k < lim
         while (mask) {
             const int ka = 63 - __builtin_clzll(mask);
             mask ^= 1ull << ka;
@@ -179,8 +186,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
             const float4 b0 = st.rec[kb][0], b1 = st.rec[kb][1];
             const float2 a2 = *reinterpret_cast<const float2 *>(&st.rec[ka][2]);
             const float2 b2 = *reinterpret_cast<const float2 *>(&st.rec[kb][2]);
-            const Pre qa = prepare(a0, a1, lo + ka, true);  // entry index = upstream `contributor`
-            const Pre qb = prepare(b0, b1, lo + kb, two);
+            const Pre qa = prepare(a0, a1, ka, lim, true);  // entry lo + k = upstream `contributor`
+            const Pre qb = prepare(b0, b1, kb, lim, two);
             if (!__any(qa.valid || qb.valid)) continue;
             const G9 ga = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: ka > kb
             const G9 gb = replay(qb, b1.y, b1.z, b1.w, b2.x);
@@ -194,23 +201,27 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
             const float h6 = swap32_sum(gb.g2, gb.g3);
             const float h7 = swap32_sum(gb.g4, gb.g5);
             const float h8 = swap32_sum(gb.g6, gb.g7);
-            const float k0 = row_sum_to_lane15(swap16_sum(h0, h1));   // lanes 15/31/47/63: a0 a2 a1 a3
-            const float k1 = row_sum_to_lane15(swap16_sum(h2, h3));   //                    a4 a6 a5 a7
-            const float k2 = row_sum_to_lane15(swap16_sum(h4, h5));   //                    a8 b0 b8 b1
-            const float k3 = row_sum_to_lane15(swap16_sum(h6, h7));   //                    b2 b4 b3 b5
-            const float k4 = row_sum_to_lane15(swap16_sum(h8, 0.f));  //                    b6 -  b7 -
-            const float k1s = dpp_f32<DPP_ROW_SHL1>(k1);  // lane 14 of each row <- lane 15
-            const float k2s1 = dpp_f32<DPP_ROW_SHL1>(k2);
-            const float k2s2 = dpp_f32<DPP_ROW_SHL2>(k2);  // lane 13 of each row <- lane 15
-            const float k4s = dpp_f32<DPP_ROW_SHL2>(k4);
-            const float va = rl == 15 ? k0 : (rl == 14 ? k1s : k2s2);
-            const float vb = rl == 15 ? k3 : (rl == 14 ? k2s1 : k4s);
+            // stage 2: v_permlane16_swap, 9 -> 5 registers (rows hold distinct sums)
+            const float k0 = swap16_sum(h0, h1);
+            const float k1 = swap16_sum(h2, h3);
+            const float k2 = swap16_sum(h4, h5);
+            const float k3 = swap16_sum(h6, h7);
+            const float k4 = swap16_sum(h8, 0.f);
+            // stages 3-6 inside each 16-lane row, DPP partners: row_ror:8 (lane ^ 8),
+            // row_half_mirror (lane ^ 7), quad_perm xor 2, quad_perm xor 1
+            const float m0 = rs_keep(k0, k1, 8) + dpp_f32<DPP_ROW_ROR8>(rs_send(k0, k1, 8));
+            const float m1 = rs_keep(k2, k3, 8) + dpp_f32<DPP_ROW_ROR8>(rs_send(k2, k3, 8));
+            const float m2 = rs_keep(k4, 0.f, 8) + dpp_f32<DPP_ROW_ROR8>(rs_send(k4, 0.f, 8));
+            const float n0 = rs_keep(m0, m1, 4) + dpp_f32<DPP_ROW_HALF_MIRROR>(rs_send(m0, m1, 4));
+            const float n1 = rs_keep(m2, 0.f, 4) + dpp_f32<DPP_ROW_HALF_MIRROR>(rs_send(m2, 0.f, 4));
+            const float o0 = rs_keep(n0, n1, 2) + dpp_f32<DPP_QUAD_XOR2>(rs_send(n0, n1, 2));
+            const float v = o0 + dpp_f32<DPP_QUAD_XOR1>(o0);  // odd lanes: unused duplicates
             // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
             // compiler's atomic optimizer (a wave-scan loop) out
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.y));
             const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.y));
-            if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, va);
-            if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, vb);
+            if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, v);
+            if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
         }
     };
     // Double-buffered backwards stream, unrolled by two so the buffers swap roles
