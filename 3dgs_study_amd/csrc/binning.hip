@@ -63,6 +63,8 @@ struct RadixPass {
     const uint32_t *vin;   // values; nullptr = the item index
     uint32_t *kout;        // nullptr = keys not needed after this pass
     uint32_t *vout;
+    const uint2 *gsrc;     // optional: gdst[pos] = gsrc[value] for every written value
+    uint2 *gdst;
     uint32_t n;
     int shift;
     int nbits;             // significant bits of this pass's digit (<= RADIX_BITS)
@@ -193,8 +195,10 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         const uint32_t k = stage_k[i];
         const uint32_t d = (k >> a.shift) & a.dmask;
         const uint32_t pos = gstart[d] + (i - lstart[d]);
+        const uint32_t v = stage_v[i];
         if (a.kout) a.kout[pos] = k;
-        a.vout[pos] = stage_v[i];
+        a.vout[pos] = v;
+        if (a.gdst) a.gdst[pos] = a.gsrc[v];
     }
 }
 
@@ -214,10 +218,10 @@ __device__ __forceinline__ uint32_t rect_area(uint2 q) {
 }
 
 __global__ void __launch_bounds__(EMIT_BLOCK)
-    rank_sums_kernel(const uint32_t *order, const uint2 *rects, int P, uint32_t *sums) {
+    rank_sums_kernel(const uint2 *rects_ranked, int P, uint32_t *sums) {
     __shared__ uint32_t wsum[EMIT_BLOCK / 64];
     const int r = blockIdx.x * EMIT_BLOCK + threadIdx.x;
-    const uint32_t v = r < P ? rect_area(rects[order[r]]) : 0u;
+    const uint32_t v = r < P ? rect_area(rects_ranked[r]) : 0u;
     const uint32_t tot = block_sum<EMIT_BLOCK>(v, wsum);
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
@@ -254,7 +258,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
     __shared__ uint4 rect[EMIT_BLOCK];  // x0, width, y0, id
     const int r = blockIdx.x * EMIT_BLOCK + threadIdx.x;
     const uint32_t id = r < a.P ? a.order[r] : 0u;
-    const uint2 q = r < a.P ? a.rects[id] : make_uint2(0u, 0u);
+    const uint2 q = r < a.P ? a.rects[r] : make_uint2(0u, 0u);  // rects in depth order
     const uint32_t v = rect_area(q);
     uint32_t tot;
     const uint32_t inc = block_inclusive_scan<EMIT_BLOCK>(v, wsum, &tot);
@@ -314,14 +318,18 @@ hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
         a.shift = 8 * p;
         a.nbits = RADIX_BITS;
         a.dmask = RADIX - 1;
+        // the last pass also lays the tile rects out in depth order (one random
+        // gather here instead of one in rank_sums and one in emit)
+        a.gsrc = p == 3 ? at<const uint2>(geom, L.rects) : nullptr;
+        a.gdst = p == 3 ? at<uint2>(geom, L.rects_ranked) : nullptr;
         hipError_t e = radix_pass<DSORT_ITEMS>(a, s);
         if (e != hipSuccess) return e;
     }
     // rank-order exclusive offsets of the instances, per EMIT block
     const int nb = emit_blocks(P);
     uint32_t *sums = at<uint32_t>(geom, L.emit_sums);
-    hipLaunchKernelGGL(rank_sums_kernel, dim3(nb), dim3(EMIT_BLOCK), 0, s, (const uint32_t *)va,
-                       at<const uint2>(geom, L.rects), P, sums);
+    hipLaunchKernelGGL(rank_sums_kernel, dim3(nb), dim3(EMIT_BLOCK), 0, s, at<const uint2>(geom, L.rects_ranked), P,
+                       sums);
     hipLaunchKernelGGL(exclusive_scan_one_block_kernel, dim3(1), dim3(TOPSCAN_THREADS), 0, s, sums, nb);
     return hipGetLastError();
 }
@@ -335,7 +343,7 @@ hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, vo
     a.P = P;
     a.gx = g.gx;
     a.order = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]);
-    a.rects = at<const uint2>(geom, L.rects);
+    a.rects = at<const uint2>(geom, L.rects_ranked);
     a.block_prefix = at<const uint32_t>(geom, L.emit_sums);
     // emit into the buffer pair that the tile passes will end in KEYS/POINT_LIST
     const bool odd = tile_sort_passes(g.tiles) & 1;
@@ -358,6 +366,8 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
     RadixPass a;
     a.n = (uint32_t)I;
     a.NB = radix_blocks(I, TSORT_ITEMS);
+    a.gsrc = nullptr;
+    a.gdst = nullptr;
     a.hist = at<uint32_t>(binning, B.hist);
     a.totals = at<uint32_t>(binning, B.totals);
     for (int p = 0; p < npass; p++) {

@@ -68,6 +68,7 @@ struct GeomLayout {
     size_t off[GSR_GEOM_NFIELDS];
     size_t scan_sums;     // uint32 [pre_blocks(P)] block sums -> exclusive block prefixes
     size_t rects;         // uint2 [P] tile rect {x0 | x1 << 16, y0 | y1 << 16}; 0 when not visible
+    size_t rects_ranked;  // uint2 [P] the same in depth order (written by the last depth pass)
     size_t dsort_keys_a;  // uint32 [P] depth-sort ping-pong (the order lands in GSR_GEOM_DEPTH_ORDER)
     size_t dsort_keys_b;
     size_t dsort_vals_b;
@@ -92,6 +93,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.off[GSR_GEOM_DEPTH_ORDER] = take((size_t)P * 4);
     L.scan_sums = take((size_t)pre_blocks(P) * 4 + 4);
     L.rects = take((size_t)P * 8);
+    L.rects_ranked = take((size_t)P * 8);
     L.dsort_keys_a = take((size_t)P * 4);
     L.dsort_keys_b = take((size_t)P * 4);
     L.dsort_vals_b = take((size_t)P * 4);

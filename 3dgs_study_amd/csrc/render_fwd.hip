@@ -45,10 +45,10 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
 
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
     uint32_t last = 0;
-    bool done = !inside;
+    float live = inside ? 1.0f : 0.0f;  // 0 once the pixel has stopped (or lies outside the image)
     __shared__ ChunkStage stage[BLEND_THREADS / 64];
     ChunkStage &st = stage[w];
-    if (__any(!done) && n > 0) {
+    if (__any(inside) && n > 0) {
         const uint32_t *list = a.point_list + r.x;
         const int nm1 = n - 1;
         // Blend one 64-entry chunk starting at list position pos (lane l <-> entry
@@ -82,24 +82,31 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
                     pb = -0.5f * (dx * ux + dy * uy);
                     alpha_b = fminf(0.99f, b1.y * __expf(pb));
                 }
-                // upstream's front-to-back step, branch-free (selects, not exec-mask
-                // branches): skip power > 0 and alpha < 1/255, stop before T < 1e-4
-                auto step = [&](bool live, float power, float alpha, float cr, float cg, float cb, int k) {
-                    const float test_T = T * (1 - alpha);
-                    const bool ok = live && !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                    const bool sat = ok && test_T < 0.0001f;  // this Gaussian is not blended
-                    const bool blend = ok && !sat;
-                    done = done || sat;
-                    const float wgt = blend ? alpha * T : 0.0f;
+                // upstream's front-to-back step without branches or lane-mask logic
+                // (selects on VGPRs only: the per-Gaussian SALU work of bool masks
+                // and exec juggling, one scalar unit per CU, bounded this loop).
+                // a = the alpha this pixel takes: 0 when upstream would skip the
+                // Gaussian (power > 0, alpha < 1/255, pixel finished) — a zero alpha
+                // leaves T and C unchanged.  T >= 1e-4 holds for every live pixel, so
+                // the stop test can only fire for a > 0, exactly upstream's test.
+                auto step = [&](bool use, float power, float alpha, float cr, float cg, float cb, int k) {
+                    float av = power > 0.0f ? 0.0f : alpha;
+                    av = alpha < 1.0f / 255.0f ? 0.0f : av;
+                    av = use ? av * live : 0.0f;
+                    const float test_T = T * (1 - av);
+                    const bool sat = test_T < 0.0001f;  // this Gaussian is not blended; the pixel stops
+                    av = sat ? 0.0f : av;
+                    live = sat ? 0.0f : live;
+                    const float wgt = av * T;
                     C0 += cr * wgt;
                     C1 += cg * wgt;
                     C2 += cb * wgt;
-                    T = blend ? test_T : T;
-                    last = blend ? (uint32_t)(pos + k + 1) : last;
+                    T = sat ? T : test_T;
+                    last = av > 0.0f ? (uint32_t)(pos + k + 1) : last;
                 };
                 step(true, pa, alpha_a, a1.z, a1.w, acb, ka);
                 step(two, pb, alpha_b, b1.z, b1.w, bcb, kb);
-                if (!__any(!done)) return true;
+                if (!__any(live > 0.0f)) return true;
             }
             return false;
         };
