@@ -24,24 +24,26 @@ constexpr int BLEND_THREADS = 256;  // 4 waves = the 4 quadrants of one tile
 // every pixel of the quadrant would have skipped.  A NaN bound keeps the entry.
 __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb, float cc, float qmax, float x0,
                                          float y0) {
+    // ca, cb, cc, qmax come from the splat record, i.e. times -1/2: the form is
+    // concave, so "min over the box of q <= qmax" reads "max of q' >= qmax'"
     const float dx0 = x0 - mx, dx1 = x0 + 7.0f - mx;
     const float dy0 = y0 - my, dy1 = y0 + 7.0f - my;
     if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return true;  // mean inside: q_min = 0
-    // convex q: with the minimum outside the box, the box minimum lies on an edge
-    // approximate reciprocals only move the edge minimiser by an ulp: q changes at
-    // second order, far inside the preprocess margin
+    // with the extremum outside the box, the box extremum lies on an edge (the
+    // edge optimiser -cb dx / cc is scale-invariant).  Approximate reciprocals
+    // only move it by an ulp: q changes at second order, far inside the margin
     const float icc = __builtin_amdgcn_rcpf(cc), ica = __builtin_amdgcn_rcpf(ca);
-    float q = INFINITY;
+    float q = -INFINITY;
 #pragma unroll
     for (int e = 0; e < 2; e++) {
         const float dx = e ? dx1 : dx0;
         const float dy = fminf(fmaxf(-cb * dx * icc, dy0), dy1);
-        q = fminf(q, ca * dx * dx + 2.0f * cb * dx * dy + cc * dy * dy);
+        q = fmaxf(q, ca * dx * dx + 2.0f * cb * dx * dy + cc * dy * dy);
         const float ey = e ? dy1 : dy0;
         const float ex = fminf(fmaxf(-cb * ey * ica, dx0), dx1);
-        q = fminf(q, ca * ex * ex + 2.0f * cb * ex * ey + cc * ey * ey);
+        q = fmaxf(q, ca * ex * ex + 2.0f * cb * ex * ey + cc * ey * ey);
     }
-    return !(q > qmax);
+    return !(q < qmax);
 }
 
 // s_waitcnt vmcnt(4) expcnt(7) lgkmcnt(15): everything but the 4 youngest

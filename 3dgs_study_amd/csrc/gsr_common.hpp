@@ -24,8 +24,14 @@ constexpr int WAVE = 64;
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
 constexpr int RX_THREADS = 256;
-constexpr int DSORT_ITEMS = 4;
-constexpr int TSORT_ITEMS = 8;
+#ifndef GSR_DSORT_ITEMS
+#define GSR_DSORT_ITEMS 4
+#endif
+#ifndef GSR_TSORT_ITEMS
+#define GSR_TSORT_ITEMS 8
+#endif
+constexpr int DSORT_ITEMS = GSR_DSORT_ITEMS;
+constexpr int TSORT_ITEMS = GSR_TSORT_ITEMS;
 constexpr int EMIT_BLOCK = 256;  // Gaussians per rank-order emit workgroup
 constexpr int PRE_THREADS = 256;          // preprocess block (scan granule)
 

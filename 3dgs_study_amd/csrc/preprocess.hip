@@ -144,9 +144,12 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 a.depths[idx] = p_view.z;
                 a.means2D[idx] = make_float2(px, py);
                 float4 *sp = a.splats + 3 * (size_t)idx;
-                sp[0] = make_float4(px, py, conic_x, conic_y);
-                sp[1] = make_float4(conic_z, opac, rgb[0], rgb[1]);
-                sp[2] = make_float4(rgb[2], __uint_as_float((uint32_t)idx), qmax, 0.0f);
+                // conic and bound stored times -1/2 (exact): the blend kernels then
+                // evaluate upstream's power -0.5 * d^T conic d as d^T conic' d,
+                // bit for bit, one multiply fewer per (pixel, Gaussian)
+                sp[0] = make_float4(px, py, -0.5f * conic_x, -0.5f * conic_y);
+                sp[1] = make_float4(-0.5f * conic_z, opac, rgb[0], rgb[1]);
+                sp[2] = make_float4(rgb[2], __uint_as_float((uint32_t)idx), -0.5f * qmax, 0.0f);
                 a.clamped[idx] = clampbits;
                 radius_out = r;
                 touched = area;

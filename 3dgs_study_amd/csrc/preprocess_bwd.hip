@@ -158,8 +158,11 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
     const float4 acc1 = *reinterpret_cast<const float4 *>(acc + 4);  // conic.w, opacity, color r, color g
     const float accb = acc[8];                                       // color b
     const float dcol[3] = {acc1.z, acc1.w, accb};
-    o.dmeans2D[3 * (size_t)idx + 0] = acc0.x;
-    o.dmeans2D[3 * (size_t)idx + 1] = acc0.y;
+    // render_bwd.hip accumulates sum W (conic' d) and sum W (dx^2, dx dy, dy^2);
+    // the per-Gaussian constant factors are applied here
+    const float g2x = acc0.x * (float)in.W, g2y = acc0.y * (float)in.H;  // dL/dmean2D
+    o.dmeans2D[3 * (size_t)idx + 0] = g2x;
+    o.dmeans2D[3 * (size_t)idx + 1] = g2y;
     o.dmeans2D[3 * (size_t)idx + 2] = 0.f;
     o.dcolors[3 * (size_t)idx + 0] = dcol[0];
     o.dcolors[3 * (size_t)idx + 1] = dcol[1];
@@ -200,7 +203,7 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
     const float ca = cov2D.m[0][0] += 0.3f;
     const float cb = cov2D.m[0][1];
     const float cc = cov2D.m[1][1] += 0.3f;
-    const float gx = acc0.z, gy = acc0.w, gz = acc1.x;  // dL/dconic x, y, w
+    const float gx = -0.5f * acc0.z, gy = -0.5f * acc0.w, gz = -0.5f * acc1.x;  // dL/dconic x, y, w
     const float denom = ca * cc - cb * cb;
     float dL_da = 0, dL_db = 0, dL_dc = 0;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
@@ -253,7 +256,6 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
     const float *pm = Pm.m;
     const float mul1 = (pm[0] * mean.x + pm[4] * mean.y + pm[8] * mean.z + pm[12]) * m_w * m_w;
     const float mul2 = (pm[1] * mean.x + pm[5] * mean.y + pm[9] * mean.z + pm[13]) * m_w * m_w;
-    const float g2x = acc0.x, g2y = acc0.y;
     dmean.x += (pm[0] * m_w - pm[3] * mul1) * g2x + (pm[1] * m_w - pm[3] * mul2) * g2y;
     dmean.y += (pm[4] * m_w - pm[7] * mul1) * g2x + (pm[5] * m_w - pm[7] * mul2) * g2y;
     dmean.z += (pm[8] * m_w - pm[11] * mul1) * g2x + (pm[9] * m_w - pm[11] * mul2) * g2y;

@@ -80,7 +80,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     }
     const float bg_dot = a.bg[0] * dpx0 + a.bg[1] * dpx1 + a.bg[2] * dpx2;
     const float nTbg = -T_final * bg_dot;
-    const float nhx = -0.5f * (float)a.W, nhy = -0.5f * (float)a.H;  // -ddelx_dx, -ddely_dy
     int end = last_contrib;  // wave max: the first (from the back) entry any pixel replays
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) end = max(end, __shfl_xor(end, o));
@@ -122,9 +121,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         Pre q;
         q.dx = p0.x - fx;
         q.dy = p0.y - fy;
-        q.ux = p0.z * q.dx + p0.w * q.dy;  // conic * d
+        q.ux = p0.z * q.dx + p0.w * q.dy;  // conic' * d with conic' = -conic/2 (splat record)
         q.uy = p0.w * q.dx + p1.x * q.dy;
-        const float power = -0.5f * (q.dx * q.ux + q.dy * q.uy);  // == render_fwd.hip, bit for bit
+        const float power = q.dx * q.ux + q.dy * q.uy;  // upstream's power; == render_fwd.hip, bit for bit
         q.G = __expf(power);
         q.alpha = fminf(0.99f, p1.y * q.G);
         q.valid = live && k < lim && !(power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
@@ -150,18 +149,20 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         R2 += av * e2;
         // dL/dalpha (upstream: sum_c (c - accum_rec) dL_dpix_c * T - T_final/(1-alpha) * bg.dL_dpix)
         const float dL_dalpha = q.valid ? dot * T + inv_1ma * nTbg : 0.0f;
-        // dG/d(delta) = -G conic d; with W = G * opacity * dL/dalpha:
-        //   dmean2D = -W (conic d) * (W/2, H/2),  dconic = -W/2 (dx^2, dx dy, dy^2)
-        const float Wg = Gv * op * dL_dalpha;
-        const float hw = -0.5f * Wg;
-        const float hdx = hw * q.dx;
+        // dG/d(delta) = -G conic d; with W = G * opacity * dL/dalpha the per-pixel
+        // terms are dmean2D = -W (conic d) (W/2, H/2) = W (conic' d) (W, H) and
+        // dconic = -W/2 (dx^2, dx dy, dy^2).  The constant factors (W, H) and -1/2
+        // are applied once per Gaussian in preprocess_bwd.hip, so the accumulator
+        // holds sum W (conic' d) and sum W (dx^2, dx dy, dy^2).
         G9 g;
-        g.g0 = q.ux * (Wg * nhx);
-        g.g1 = q.uy * (Wg * nhy);
-        g.g2 = hdx * q.dx;
-        g.g3 = hdx * q.dy;
-        g.g4 = hw * q.dy * q.dy;
         g.g5 = Gv * dL_dalpha;
+        const float Wg = g.g5 * op;
+        const float wdx = Wg * q.dx;
+        g.g0 = Wg * q.ux;
+        g.g1 = Wg * q.uy;
+        g.g2 = wdx * q.dx;
+        g.g3 = wdx * q.dy;
+        g.g4 = Wg * q.dy * q.dy;
         g.g6 = dchannel_dcolor * dpx0;
         g.g7 = dchannel_dcolor * dpx1;
         g.g8 = dchannel_dcolor * dpx2;

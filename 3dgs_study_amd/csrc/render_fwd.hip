@@ -72,14 +72,16 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
                 float pa, pb, alpha_a, alpha_b;
                 {
                     const float dx = a0.x - fx, dy = a0.y - fy;
-                    const float ux = a0.z * dx + a0.w * dy, uy = a0.w * dx + a1.x * dy;  // conic * d
-                    pa = -0.5f * (dx * ux + dy * uy);  // render_bwd.hip recomputes it identically
+                    // conic' = -conic/2 (splat record): pa is upstream's power; render_bwd.hip
+                    // recomputes it bit for bit
+                    const float ux = a0.z * dx + a0.w * dy, uy = a0.w * dx + a1.x * dy;
+                    pa = dx * ux + dy * uy;
                     alpha_a = fminf(0.99f, a1.y * __expf(pa));
                 }
                 {
                     const float dx = b0.x - fx, dy = b0.y - fy;
                     const float ux = b0.z * dx + b0.w * dy, uy = b0.w * dx + b1.x * dy;
-                    pb = -0.5f * (dx * ux + dy * uy);
+                    pb = dx * ux + dy * uy;
                     alpha_b = fminf(0.99f, b1.y * __expf(pb));
                 }
                 // upstream's front-to-back step without branches or lane-mask logic

@@ -122,7 +122,7 @@ int gsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, c
 enum gsr_geom_field {
     GSR_GEOM_DEPTHS = 0,     /* float  [P] */
     GSR_GEOM_MEANS2D,        /* float2 [P]  pixel-space centre */
-    GSR_GEOM_SPLATS,         /* float4 [P][3] {x,y,conic.x,conic.y},{conic.z,opacity,r,g},{b,id bits,qmax,0} */
+    GSR_GEOM_SPLATS,         /* float4 [P][3] {x,y,c.x,c.y},{c.z,opacity,r,g},{b,id bits,qmax,0}, c = -conic/2, qmax = -bound/2 */
     GSR_GEOM_CLAMPED,        /* uint8  [P]  bit c set = channel c clamped in SH->RGB */
     GSR_GEOM_TILES_TOUCHED,  /* uint32 [P] */
     GSR_GEOM_POINT_OFFSETS,  /* uint32 [P]  inclusive scan of tiles_touched */

@@ -32,8 +32,9 @@ def check_forward(h, r, rgb_from_sh=True, ncontrib_frac=0.999):
     np.testing.assert_array_equal(h["means2D"][vis], r["means2D"][vis])
     sp = h["splats"][vis]
     co = r["conic_opacity"][vis]
-    np.testing.assert_allclose(sp[:, 2:4], co[:, 0:2], rtol=1e-6, atol=0)
-    np.testing.assert_allclose(sp[:, 4], co[:, 2], rtol=1e-6, atol=0)
+    # the splat record stores conic * -1/2 (exact)
+    np.testing.assert_allclose(-2.0 * sp[:, 2:4], co[:, 0:2], rtol=1e-6, atol=0)
+    np.testing.assert_allclose(-2.0 * sp[:, 4], co[:, 2], rtol=1e-6, atol=0)
     np.testing.assert_array_equal(sp[:, 5], co[:, 3])
     if rgb_from_sh:
         np.testing.assert_allclose(sp[:, 6:9], r["rgb"][vis], rtol=1e-6, atol=1e-7)

@@ -10,6 +10,6 @@ for v in "$@"; do
   python - "$v" gpurun_out/var_$v.log <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
-print(sys.argv[1], d["value"], {k: v for k, v in d["stages_ms"].items() if k.startswith("render")})
+print(sys.argv[1], d["value"], d["stages_ms"])
 PY
 done

@@ -1,20 +1,27 @@
 #!/bin/bash
-# Build experimental variants of one kernel source with -D flags (in this container):
-#   bash tools/variants.sh render_bwd "A:-DFOO" "B:-DBAR" ...
-# -> 3dgs_study_amd/lib/libgsr_<name>.so ; then on the box:
-#   for v in A B; do GSR_LIBRARY=$PWD/3dgs_study_amd/lib/libgsr_$v.so python bench.py ...; done
+# Build experimental variants of the library with -D flags (in this container):
+#   bash tools/variants.sh SRC "A:-DFOO" "B:-DBAR" ...
+# SRC = one kernel source (render_bwd, ...) or "all" to rebuild every source.
+# -> 3dgs_study_amd/lib/libgsr_<name>.so ; time them on the box with
+#   bash tools/run_variants.sh base A B
 set -e
 SRC=$1; shift
 cd "$(dirname "$0")/../3dgs_study_amd/csrc"
 make -s
-OBJS=""
-for f in preprocess binning render_fwd render_bwd preprocess_bwd abi; do
-  [ "$f" != "$SRC" ] && OBJS="$OBJS ../build/$f.o"
-done
+ALL="preprocess binning render_fwd render_bwd preprocess_bwd abi"
+mkdir -p ../build/var
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -I../../include -munsafe-fp-atomics \
-      -fno-slp-vectorize $flags -c $SRC.hip -o ../build/${SRC}_$name.o
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $OBJS ../build/${SRC}_$name.o -o ../lib/libgsr_$name.so
+  OBJS=""
+  for f in $ALL; do
+    if [ "$SRC" = all ] || [ "$f" = "$SRC" ]; then
+      /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -I../../include -munsafe-fp-atomics \
+          -fno-slp-vectorize $flags -c $f.hip -o ../build/var/${f}_$name.o
+      OBJS="$OBJS ../build/var/${f}_$name.o"
+    else
+      OBJS="$OBJS ../build/$f.o"
+    fi
+  done
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $OBJS -o ../lib/libgsr_$name.so
   echo "built libgsr_$name.so ($flags)"
 done
