@@ -233,6 +233,40 @@ int gsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, c
     return check_hip(launch_mark_visible(P, means3D, viewmatrix, present, s), "mark_visible");
 }
 
+size_t gsr_l1_ssim_scratch_bytes(int32_t C, int32_t H, int32_t W) {
+    if (C <= 0 || H <= 0 || W <= 0) return 0;
+    return l1_ssim_scratch_floats(C, H, W) * sizeof(float);
+}
+
+int gsr_l1_ssim(const float *img, const float *gt, int32_t C, int32_t H, int32_t W, float lambda_dssim,
+                float *grad_img, void *scratch, float *loss_out, void *stream) {
+    if (C <= 0 || H <= 0 || W <= 0) return fail(GSR_ERR_ARGS, "l1_ssim: empty image (%d x %d x %d)", C, H, W);
+    if (!img || !gt || !grad_img || !scratch || !loss_out) return fail(GSR_ERR_ARGS, "l1_ssim: NULL buffer");
+    return check_hip(launch_l1_ssim(img, gt, C, H, W, lambda_dssim, grad_img, (float *)scratch, loss_out,
+                                    (hipStream_t)stream),
+                     "l1_ssim");
+}
+
+int gsr_adam_step(const gsr_adam_segment *segs, int32_t nseg, int32_t step, double beta1, double beta2, double eps,
+                  void *stream) {
+    if (nseg < 0 || nseg > GSR_ADAM_MAX_SEGS) return fail(GSR_ERR_ARGS, "adam: %d segments (max %d)", nseg, GSR_ADAM_MAX_SEGS);
+    if (step < 1) return fail(GSR_ERR_ARGS, "adam: step must be >= 1 (got %d)", step);
+    for (int k = 0; k < nseg; k++)
+        if (segs[k].n > 0 && (!segs[k].param || !segs[k].grad || !segs[k].exp_avg || !segs[k].exp_avg_sq))
+            return fail(GSR_ERR_ARGS, "adam: NULL buffer in segment %d", k);
+    return check_hip(launch_adam(segs, nseg, step, beta1, beta2, eps, (hipStream_t)stream), "adam");
+}
+
+int gsr_densify_stats(int32_t P, const int32_t *radii, const float *viewspace_grad, int32_t grad_stride,
+                      float *max_radii2D, float *xyz_gradient_accum, float *denom, void *stream) {
+    if (P < 0 || grad_stride < 2) return fail(GSR_ERR_ARGS, "densify_stats: bad P %d / stride %d", P, grad_stride);
+    if (P > 0 && (!radii || !viewspace_grad || !max_radii2D || !xyz_gradient_accum || !denom))
+        return fail(GSR_ERR_ARGS, "densify_stats: NULL buffer");
+    return check_hip(launch_densify_stats(P, radii, viewspace_grad, grad_stride, max_radii2D, xyz_gradient_accum,
+                                          denom, (hipStream_t)stream),
+                     "densify_stats");
+}
+
 int gsr_timing_enable(int mask) {
     g_timer.mask = mask;
     g_timer.used = 0;

@@ -34,4 +34,13 @@ struct BwdOutputs {
 hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, const void *geom, const float *accum,
                                  const BwdOutputs &o, hipStream_t s);
 
+// train_ops.hip
+size_t l1_ssim_scratch_floats(int C, int H, int W);
+hipError_t launch_l1_ssim(const float *x, const float *y, int C, int H, int W, float lambda, float *grad,
+                          float *partials, float *out, hipStream_t s);
+hipError_t launch_adam(const gsr_adam_segment *segs, int nseg, int step, double beta1, double beta2, double eps,
+                       hipStream_t s);
+hipError_t launch_densify_stats(int P, const int32_t *radii, const float *vgrad, int vstride, float *max_radii,
+                                float *grad_accum, float *denom, hipStream_t s);
+
 }  // namespace gsr

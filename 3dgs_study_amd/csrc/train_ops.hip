@@ -1,0 +1,344 @@
+// train_ops.hip — the training-step ops right after the rasterizer (SURVEY.md
+// §8f "next" rows 1-2): the fused L1 + D-SSIM loss with its gradient, the Adam
+// update of the six parameter groups, and the densification statistics.
+//
+// Reference: utils/loss_utils.py:17-24 (l1_loss), :59-108 (ssim/_ssim: 11x11
+// Gaussian window, sigma 1.5, zero padding, C1 = 0.01^2, C2 = 0.03^2, mean over
+// C*H*W); train.py:103-105 (loss = (1 - l) L1 + l (1 - SSIM)), :126-141
+// (max_radii2D, add_densification_stats, optimizer.step); scene/gaussian_model.py
+// :176-213 (Adam, eps 1e-15), :565-581 (densification statistics);
+// torch.optim.Adam's update rule (betas 0.9/0.999, bias-corrected).
+#include <cmath>
+
+#include "gsr_kernels.hpp"
+#include "gsr_wave.hpp"
+
+namespace gsr {
+
+// ------------------------------------------------------------ L1 + D-SSIM
+//
+// loss = (1 - l)/N sum |x - y| + l (1 - 1/N sum S), N = C*H*W.  The gradient of
+// the mean SSIM w.r.t. x needs only constants from the loss (dL/dS = -l/N), so
+// ONE pass computes both: per pixel q, with m1 = G*x, m2 = G*y, e11 = G*(x^2),
+// e22 = G*(y^2), e12 = G*(xy) (G the separable 11-tap window) and
+//   S = A1 A2 / (B1 B2),  A1 = 2 m1 m2 + C1,  A2 = 2 (e12 - m1 m2) + C2,
+//                         B1 = m1^2 + m2^2 + C1,  B2 = e11 - m1^2 + e22 - m2^2 + C2,
+//   dS/dm1 = S (2 m2/A1 - 2 m2/A2 - 2 m1/B1 + 2 m1/B2),  dS/de11 = -S/B2,
+//   dS/de12 = 2 S/A2,
+// and dL/dx(p) = (1-l)/N sign(x-y) + G*(dL/dS dS/dm1) + 2 x G*(dL/dS dS/de11)
+//              + y G*(dL/dS dS/de12)   (G symmetric: correlation == convolution).
+// A workgroup owns a 32x16 output tile of one channel and everything it needs
+// in LDS: the inputs over tile +- 10 px, the five blurred maps over tile +- 5 px,
+// the three derivative maps, and their blur back onto the tile.
+constexpr int SS_TX = 32, SS_TY = 16, SS_R = 5;                 // tile, window radius
+constexpr int SS_IX = SS_TX + 4 * SS_R, SS_IY = SS_TY + 4 * SS_R;  // input region 52 x 36
+constexpr int SS_MX = SS_TX + 2 * SS_R, SS_MY = SS_TY + 2 * SS_R;  // map region 42 x 26
+constexpr int SS_THREADS = 256;
+
+struct SsimArgs {
+    const float *x, *y;
+    float *grad;      // [C][H][W]
+    float *partials;  // [blocks][2] sum |x - y|, sum S over the tile's pixels
+    int C, H, W, tiles_x, tiles_y;
+    float lambda, invN;
+    float g[11];      // 1-D window (utils/loss_utils.py gaussian(11, 1.5), normalized)
+};
+
+__global__ void __launch_bounds__(SS_THREADS) l1_ssim_kernel(SsimArgs a) {
+    __shared__ float xs[SS_IY][SS_IX], ys[SS_IY][SS_IX];
+    __shared__ float hb[5][SS_IY][SS_MX];  // horizontal pass of x, y, xx, yy, xy
+    __shared__ float mp[5][SS_MY][SS_MX];  // m1, m2, e11, e22, e12 -> then dS terms a, b, c
+    __shared__ float red[2][SS_THREADS / 64];
+    const int c = blockIdx.z;
+    const int ox = blockIdx.x * SS_TX, oy = blockIdx.y * SS_TY;
+    const size_t plane = (size_t)a.H * a.W;
+    const float *X = a.x + c * plane, *Y = a.y + c * plane;
+    const int t = threadIdx.x;
+    // inputs over the tile +- 2R, zero outside the image (conv2d zero padding)
+    for (int i = t; i < SS_IX * SS_IY; i += SS_THREADS) {
+        const int ry = i / SS_IX, rx = i - ry * SS_IX;
+        const int gy = oy - 2 * SS_R + ry, gx = ox - 2 * SS_R + rx;
+        const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+        xs[ry][rx] = in ? X[(size_t)gy * a.W + gx] : 0.f;
+        ys[ry][rx] = in ? Y[(size_t)gy * a.W + gx] : 0.f;
+    }
+    __syncthreads();
+    // horizontal pass of the five products onto columns [ox - R, ox + TX + R)
+    for (int i = t; i < SS_IY * SS_MX; i += SS_THREADS) {
+        const int ry = i / SS_MX, mx = i - ry * SS_MX;
+        float s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float xv = xs[ry][mx + k], yv = ys[ry][mx + k], w = a.g[k];
+            s0 += w * xv;
+            s1 += w * yv;
+            s2 += w * (xv * xv);
+            s3 += w * (yv * yv);
+            s4 += w * (xv * yv);
+        }
+        hb[0][ry][mx] = s0;
+        hb[1][ry][mx] = s1;
+        hb[2][ry][mx] = s2;
+        hb[3][ry][mx] = s3;
+        hb[4][ry][mx] = s4;
+    }
+    __syncthreads();
+    // vertical pass -> maps over the tile +- R; then the per-pixel SSIM terms
+    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+    const float dLdS = -a.lambda * a.invN;
+    float ssum = 0.f;
+    for (int i = t; i < SS_MY * SS_MX; i += SS_THREADS) {
+        const int my = i / SS_MX, mx = i - my * SS_MX;
+        float m[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float w = a.g[k];
+#pragma unroll
+            for (int q = 0; q < 5; q++) m[q] += w * hb[q][my + k][mx];
+        }
+        const int gy = oy - SS_R + my, gx = ox - SS_R + mx;
+        const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+        const float m1 = m[0], m2 = m[1];
+        const float m1m2 = m1 * m2, m1s = m1 * m1, m2s = m2 * m2;
+        const float s1 = m[2] - m1s, s2 = m[3] - m2s, s12 = m[4] - m1m2;
+        const float A1 = 2 * m1m2 + C1, A2 = 2 * s12 + C2, B1 = m1s + m2s + C1, B2 = s1 + s2 + C2;
+        const float S = (A1 * A2) / (B1 * B2);
+        const bool own = in && my >= SS_R && my < SS_R + SS_TY && mx >= SS_R && mx < SS_R + SS_TX;
+        ssum += own ? S : 0.f;
+        // derivative maps (zero outside the image: those S do not exist)
+        const float k1 = in ? dLdS * S : 0.f;
+        mp[0][my][mx] = k1 * (2 * m2 / A1 - 2 * m2 / A2 - 2 * m1 / B1 + 2 * m1 / B2);
+        mp[1][my][mx] = -k1 / B2;
+        mp[2][my][mx] = 2 * k1 / A2;
+    }
+    __syncthreads();
+    // blur the derivative maps back: horizontal onto the tile's columns (reuse hb)
+    for (int i = t; i < SS_MY * SS_TX; i += SS_THREADS) {
+        const int my = i / SS_TX, tx = i - my * SS_TX;
+        float s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float w = a.g[k];
+            s0 += w * mp[0][my][tx + k];
+            s1 += w * mp[1][my][tx + k];
+            s2 += w * mp[2][my][tx + k];
+        }
+        hb[0][my][tx] = s0;
+        hb[1][my][tx] = s1;
+        hb[2][my][tx] = s2;
+    }
+    __syncthreads();
+    float l1sum = 0.f;
+    const float kl1 = (1.f - a.lambda) * a.invN;
+    float *G = a.grad + c * plane;
+    for (int i = t; i < SS_TX * SS_TY; i += SS_THREADS) {
+        const int ty = i / SS_TX, tx = i - ty * SS_TX;
+        const int gy = oy + ty, gx = ox + tx;
+        if (gy >= a.H || gx >= a.W) continue;
+        float b0 = 0, b1 = 0, b2 = 0;
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            const float w = a.g[k];
+            b0 += w * hb[0][ty + k][tx];
+            b1 += w * hb[1][ty + k][tx];
+            b2 += w * hb[2][ty + k][tx];
+        }
+        const float xv = xs[ty + 2 * SS_R][tx + 2 * SS_R], yv = ys[ty + 2 * SS_R][tx + 2 * SS_R];
+        const float d = xv - yv;
+        l1sum += fabsf(d);
+        const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // torch.sign
+        G[(size_t)gy * a.W + gx] = kl1 * sg + b0 + 2.f * xv * b1 + yv * b2;
+    }
+    // workgroup partial sums (the loss value itself is finished by l1_ssim_finish)
+    const float l1w = wave_sum(l1sum), ssw = wave_sum(ssum);
+    if ((t & 63) == 0) {
+        red[0][t >> 6] = l1w;
+        red[1][t >> 6] = ssw;
+    }
+    __syncthreads();
+    if (t == 0) {
+        float s0 = 0, s1 = 0;
+        for (int k = 0; k < SS_THREADS / 64; k++) {
+            s0 += red[0][k];
+            s1 += red[1][k];
+        }
+        const size_t b = ((size_t)c * a.tiles_y + blockIdx.y) * a.tiles_x + blockIdx.x;
+        a.partials[2 * b] = s0;
+        a.partials[2 * b + 1] = s1;
+    }
+}
+
+// loss = (1 - l) * mean|x - y| + l * (1 - mean S), summed in double for a
+// deterministic, order-independent-enough total
+__global__ void __launch_bounds__(1024) l1_ssim_finish_kernel(const float *partials, int nb, float lambda,
+                                                              float invN, float *out) {
+    __shared__ double s[2][1024 / 64];
+    double l1 = 0, ss = 0;
+    for (int i = threadIdx.x; i < nb; i += 1024) {
+        l1 += partials[2 * i];
+        ss += partials[2 * i + 1];
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        l1 += __shfl_xor(l1, o);
+        ss += __shfl_xor(ss, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s[0][threadIdx.x >> 6] = l1;
+        s[1][threadIdx.x >> 6] = ss;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0, b = 0;
+        for (int k = 0; k < 1024 / 64; k++) {
+            a += s[0][k];
+            b += s[1][k];
+        }
+        out[0] = (float)((1.0 - lambda) * a * invN + lambda * (1.0 - b * invN));
+        out[1] = (float)(a * invN);  // the L1 term alone (train.py logs it)
+        out[2] = (float)(b * invN);  // mean SSIM
+    }
+}
+
+size_t l1_ssim_scratch_floats(int C, int H, int W) {
+    const size_t tx = (W + SS_TX - 1) / SS_TX, ty = (H + SS_TY - 1) / SS_TY;
+    return 2 * tx * ty * C;
+}
+
+hipError_t launch_l1_ssim(const float *x, const float *y, int C, int H, int W, float lambda, float *grad,
+                          float *partials, float *out, hipStream_t s) {
+    SsimArgs a;
+    a.x = x;
+    a.y = y;
+    a.grad = grad;
+    a.partials = partials;
+    a.C = C;
+    a.H = H;
+    a.W = W;
+    a.tiles_x = (W + SS_TX - 1) / SS_TX;
+    a.tiles_y = (H + SS_TY - 1) / SS_TY;
+    a.lambda = lambda;
+    a.invN = (float)(1.0 / ((double)C * H * W));
+    // gaussian(11, 1.5) as utils/loss_utils.py builds it: float32 taps, normalized in float32
+    float sum = 0.f;
+    for (int k = 0; k < 11; k++) {
+        a.g[k] = (float)std::exp(-(double)((k - 5) * (k - 5)) / (2.0 * 1.5 * 1.5));
+        sum += a.g[k];
+    }
+    for (int k = 0; k < 11; k++) a.g[k] /= sum;
+    hipLaunchKernelGGL(l1_ssim_kernel, dim3(a.tiles_x, a.tiles_y, C), dim3(SS_THREADS), 0, s, a);
+    const int nb = a.tiles_x * a.tiles_y * C;
+    hipLaunchKernelGGL(l1_ssim_finish_kernel, dim3(1), dim3(1024), 0, s, (const float *)partials, nb, lambda, a.invN,
+                       out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ Adam
+//
+// torch.optim.Adam (no weight decay, no amsgrad), for up to 8 tensors in one
+// launch.  Workgroups are assigned to segments by a prefix table, each thread
+// updates 4 consecutive floats (16-B accesses).
+constexpr int ADAM_THREADS = 256, ADAM_VEC = 4;
+struct AdamArgs {
+    int nseg;
+    float *p[GSR_ADAM_MAX_SEGS];
+    const float *g[GSR_ADAM_MAX_SEGS];
+    float *m[GSR_ADAM_MAX_SEGS];
+    float *v[GSR_ADAM_MAX_SEGS];
+    int64_t n[GSR_ADAM_MAX_SEGS];
+    float neg_step[GSR_ADAM_MAX_SEGS];  // -lr / (1 - beta1^t)
+    float bc2s[GSR_ADAM_MAX_SEGS];      // sqrt(1 - beta2^t)
+    int block0[GSR_ADAM_MAX_SEGS + 1];  // first workgroup of each segment
+    float w1, beta2, w2, eps;           // w1 = 1 - beta1, w2 = 1 - beta2
+};
+
+// torch's foreach Adam, op for op: exp_avg.lerp_(grad, 1 - beta1) (weight < 0.5
+// form), exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2),
+// denom = sqrt(exp_avg_sq) / sqrt(bias_correction2) + eps,
+// param.addcdiv_(exp_avg, denom, -lr / bias_correction1)
+__device__ __forceinline__ void adam_one(float &p, float g, float &m, float &v, float w1, float b2, float w2, float eps,
+                                         float neg_step, float bc2s) {
+    m = m + w1 * (g - m);
+    v = v * b2;
+    v = v + w2 * (g * g);
+    const float denom = sqrtf(v) / bc2s + eps;
+    p = p + neg_step * (m / denom);
+}
+
+__global__ void __launch_bounds__(ADAM_THREADS) adam_kernel(AdamArgs a) {
+    int s = 0;
+    while (s + 1 < a.nseg && (int)blockIdx.x >= a.block0[s + 1]) s++;
+    const int64_t i0 = ((int64_t)(blockIdx.x - a.block0[s]) * ADAM_THREADS + threadIdx.x) * ADAM_VEC;
+    const int64_t n = a.n[s];
+    if (i0 >= n) return;
+    float *p = a.p[s], *m = a.m[s], *v = a.v[s];
+    const float *g = a.g[s];
+    const float w1 = a.w1, b2 = a.beta2, w2 = a.w2, eps = a.eps, ns = a.neg_step[s], bc = a.bc2s[s];
+    const bool vec = i0 + ADAM_VEC <= n && ((((uintptr_t)(p + i0)) | ((uintptr_t)(g + i0)) | ((uintptr_t)(m + i0)) |
+                                            ((uintptr_t)(v + i0))) & 15u) == 0;
+    if (vec) {
+        float4 P = *reinterpret_cast<float4 *>(p + i0), G = *reinterpret_cast<const float4 *>(g + i0);
+        float4 M = *reinterpret_cast<float4 *>(m + i0), V = *reinterpret_cast<float4 *>(v + i0);
+        adam_one(P.x, G.x, M.x, V.x, w1, b2, w2, eps, ns, bc);
+        adam_one(P.y, G.y, M.y, V.y, w1, b2, w2, eps, ns, bc);
+        adam_one(P.z, G.z, M.z, V.z, w1, b2, w2, eps, ns, bc);
+        adam_one(P.w, G.w, M.w, V.w, w1, b2, w2, eps, ns, bc);
+        *reinterpret_cast<float4 *>(p + i0) = P;
+        *reinterpret_cast<float4 *>(m + i0) = M;
+        *reinterpret_cast<float4 *>(v + i0) = V;
+    } else {
+        for (int64_t i = i0; i < n && i < i0 + ADAM_VEC; i++) adam_one(p[i], g[i], m[i], v[i], w1, b2, w2, eps, ns, bc);
+    }
+}
+
+hipError_t launch_adam(const gsr_adam_segment *segs, int nseg, int step, double beta1, double beta2, double eps,
+                       hipStream_t s) {
+    AdamArgs a;
+    a.nseg = nseg;
+    // Python-side scalars as torch forms them (double math, then float)
+    a.w1 = (float)(1.0 - beta1);
+    a.beta2 = (float)beta2;
+    a.w2 = (float)(1.0 - beta2);
+    a.eps = (float)eps;
+    const double bc1 = 1.0 - std::pow(beta1, step), bc2 = 1.0 - std::pow(beta2, step);
+    int blocks = 0;
+    for (int k = 0; k < nseg; k++) {
+        a.p[k] = segs[k].param;
+        a.g[k] = segs[k].grad;
+        a.m[k] = segs[k].exp_avg;
+        a.v[k] = segs[k].exp_avg_sq;
+        a.n[k] = segs[k].n;
+        a.neg_step[k] = (float)(-(segs[k].lr / bc1));
+        a.bc2s[k] = (float)std::sqrt(bc2);
+        a.block0[k] = blocks;
+        blocks += (int)((segs[k].n + (int64_t)ADAM_THREADS * ADAM_VEC - 1) / ((int64_t)ADAM_THREADS * ADAM_VEC));
+    }
+    a.block0[nseg] = blocks;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(ADAM_THREADS), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ densification statistics
+// max_radii2D[v] = max(max_radii2D[v], radii[v]); xyz_gradient_accum[v] += |dmean2D[v, :2]|;
+// denom[v] += 1, for v with radii > 0 (train.py:126-127, gaussian_model.py:565-581)
+__global__ void densify_stats_kernel(int P, const int32_t *radii, const float *vgrad, int vstride, float *max_radii,
+                                     float *grad_accum, float *denom) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int r = radii[i];
+    if (r <= 0) return;
+    max_radii[i] = fmaxf(max_radii[i], (float)r);
+    const float gx = vgrad[(size_t)i * vstride], gy = vgrad[(size_t)i * vstride + 1];
+    grad_accum[i] += sqrtf(gx * gx + gy * gy);
+    denom[i] += 1.f;
+}
+
+hipError_t launch_densify_stats(int P, const int32_t *radii, const float *vgrad, int vstride, float *max_radii,
+                                float *grad_accum, float *denom, hipStream_t s) {
+    if (P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(densify_stats_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, radii, vgrad, vstride,
+                       max_radii, grad_accum, denom);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

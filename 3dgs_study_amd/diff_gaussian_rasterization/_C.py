@@ -50,7 +50,17 @@ EXPORTED = (
     "gsr_forward_preprocess", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
     "gsr_geom_layout", "gsr_binning_layout", "gsr_img_layout", "gsr_last_error", "gsr_abi_version",
     "gsr_timing_enable", "gsr_timing_read", "gsr_stage_name",
+    "gsr_l1_ssim_scratch_bytes", "gsr_l1_ssim", "gsr_adam_step", "gsr_densify_stats",
 )
+
+
+class GsrAdamSegment(ctypes.Structure):
+    """Mirror of ``gsr_adam_segment`` in include/gsr.h."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_int64), ("lr", ctypes.c_double)]
+
+
+ADAM_MAX_SEGS = 8
 ABI_VERSION = 2
 
 _lib = None
@@ -100,6 +110,15 @@ def load_library():
     lib.gsr_timing_read.restype = ctypes.c_int
     lib.gsr_stage_name.argtypes = [ctypes.c_int]
     lib.gsr_stage_name.restype = ctypes.c_char_p
+    lib.gsr_l1_ssim_scratch_bytes.argtypes = [i32, i32, i32]
+    lib.gsr_l1_ssim_scratch_bytes.restype = sz
+    lib.gsr_l1_ssim.argtypes = [vp, vp, i32, i32, i32, ctypes.c_float, vp, vp, vp, vp]
+    lib.gsr_l1_ssim.restype = ctypes.c_int
+    lib.gsr_adam_step.argtypes = [ctypes.POINTER(GsrAdamSegment), i32, i32, ctypes.c_double, ctypes.c_double,
+                                  ctypes.c_double, vp]
+    lib.gsr_adam_step.restype = ctypes.c_int
+    lib.gsr_densify_stats.argtypes = [i32, vp, vp, i32, vp, vp, vp, vp]
+    lib.gsr_densify_stats.restype = ctypes.c_int
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_abi_version.restype = ctypes.c_int
     if lib.gsr_abi_version() != ABI_VERSION:

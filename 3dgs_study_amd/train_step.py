@@ -152,3 +152,102 @@ def train_step(camera, gaussians, target: torch.Tensor, bg: torch.Tensor, lambda
     loss.backward()
     out["loss"] = loss
     return out
+
+
+# ---------------------------------------------------------------- the full training step (train.py:86-141)
+def expon_lr(lr_init: float, lr_final: float, lr_delay_steps: int = 0, lr_delay_mult: float = 1.0,
+             max_steps: int = 1_000_000):
+    """utils/general_utils.py:30-69 get_expon_lr_func (log-linear decay, optional delay)."""
+
+    def helper(step):
+        if step < 0 or (lr_init == 0.0 and lr_final == 0.0):
+            return 0.0
+        if lr_delay_steps > 0:
+            delay = lr_delay_mult + (1 - lr_delay_mult) * math.sin(0.5 * math.pi * min(max(step / lr_delay_steps, 0), 1))
+        else:
+            delay = 1.0
+        t = min(max(step / max_steps, 0), 1)
+        return delay * math.exp(math.log(lr_init) * (1 - t) + math.log(lr_final) * t)
+
+    return helper
+
+
+# OptimizationParams defaults (arguments/__init__.py:79-93)
+OPT = dict(position_lr_init=0.00016, position_lr_final=0.0000016, position_lr_delay_mult=0.01,
+           position_lr_max_steps=30_000, feature_lr=0.0025, opacity_lr=0.05, scaling_lr=0.005, rotation_lr=0.001,
+           lambda_dssim=0.2, densify_until_iter=15_000)
+
+
+class TrainState:
+    """The optimizer side of GaussianModel for a SynthGaussians: the six Adam groups
+    (scene/gaussian_model.py:176-205, lr 0 default, eps 1e-15), the xyz learning-rate
+    schedule and the densification statistics (:565-581).  ``fused`` swaps torch's
+    Adam and statistics for the HIP kernels of train_ops.py."""
+
+    def __init__(self, g, spatial_lr_scale: float, fused: bool = False, opt: dict = OPT):
+        import train_ops
+
+        self.opt, self.fused = opt, fused
+        groups = [
+            {"params": [g.xyz], "lr": opt["position_lr_init"] * spatial_lr_scale, "name": "xyz"},
+            {"params": [g.features_dc], "lr": opt["feature_lr"], "name": "f_dc"},
+            {"params": [g.features_rest], "lr": opt["feature_lr"] / 20.0, "name": "f_rest"},
+            {"params": [g.opacity], "lr": opt["opacity_lr"], "name": "opacity"},
+            {"params": [g.scaling], "lr": opt["scaling_lr"], "name": "scaling"},
+            {"params": [g.rotation], "lr": opt["rotation_lr"], "name": "rotation"},
+        ]
+        if fused:
+            self.optimizer = train_ops.FusedAdam(groups, lr=0.0, eps=1e-15)
+        else:
+            self.optimizer = torch.optim.Adam(groups, lr=0.0, eps=1e-15)
+        self.xyz_scheduler = expon_lr(opt["position_lr_init"] * spatial_lr_scale,
+                                      opt["position_lr_final"] * spatial_lr_scale,
+                                      lr_delay_mult=opt["position_lr_delay_mult"],
+                                      max_steps=opt["position_lr_max_steps"])
+        P, dev = g.xyz.shape[0], g.xyz.device
+        self.xyz_gradient_accum = torch.zeros((P, 1), device=dev)
+        self.denom = torch.zeros((P, 1), device=dev)
+        self.max_radii2D = torch.zeros((P,), device=dev)
+
+    def update_learning_rate(self, iteration: int):
+        for group in self.optimizer.param_groups:
+            if group["name"] == "xyz":
+                group["lr"] = self.xyz_scheduler(iteration)
+                return group["lr"]
+
+    @torch.no_grad()
+    def densification_stats(self, out: dict):
+        radii, vis, vsp = out["radii"], out["visibility_filter"], out["viewspace_points"]
+        if self.fused:
+            import train_ops
+
+            train_ops.densify_stats(radii, vsp.grad, self.max_radii2D, self.xyz_gradient_accum, self.denom)
+        else:  # train.py:126-127 and scene/gaussian_model.py:565-581
+            self.max_radii2D[vis] = torch.max(self.max_radii2D[vis], radii[vis])
+            self.xyz_gradient_accum[vis] += torch.norm(vsp.grad[vis, :2], dim=-1, keepdim=True)
+            self.denom[vis] += 1
+
+
+def full_train_step(iteration: int, camera, gaussians, state: TrainState, target: torch.Tensor,
+                    bg: torch.Tensor) -> torch.Tensor:
+    """One iteration of train.py:86-141 without logging, checkpoints and the periodic
+    densify/prune/opacity reset: lr schedule, render, L1 + lambda (1 - SSIM), backward,
+    densification statistics, Adam step, zero_grad.  ``state.fused`` selects the HIP
+    loss/Adam/statistics kernels (train_ops.py) over the reference's torch ops."""
+    state.update_learning_rate(iteration)
+    out = render(camera, gaussians, bg)
+    image = out["render"]
+    lam = state.opt["lambda_dssim"]
+    if state.fused:
+        import train_ops
+
+        loss = train_ops.l1_ssim_loss(image, target, lam)
+    else:
+        loss = (1.0 - lam) * l1_loss(image, target) + lam * (1.0 - ssim(image, target))
+    loss.backward()
+    with torch.no_grad():
+        if iteration < state.opt["densify_until_iter"]:
+            state.densification_stats(out)
+        state.optimizer.step()
+        state.optimizer.zero_grad(set_to_none=True)
+    return loss

@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lambda-dssim", type=float, default=0.0,
                     help="0 = L1-only headline unit; 0.2 = the reference's L1+SSIM loss")
+    ap.add_argument("--full-steps", type=int, default=20,
+                    help="timed iterations of the full train.py step (L1+SSIM, Adam), torch vs fused; 0 = skip")
     args = ap.parse_args()
 
     import torch
@@ -225,11 +227,45 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if world == 1 and args.full_steps > 0:
+            line["full_step"] = full_step_rates(cam, P, deg, target, bg, args.full_steps)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(P, W, H, deg)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def full_step_rates(cam, P: int, deg: int, target, bg, steps: int) -> dict:
+    """The reference-faithful training iteration (train.py:86-141 without logging and
+    the periodic densify/prune): lr schedule, render, L1 + 0.2 (1 - SSIM), backward,
+    densification statistics, Adam over the six groups, zero_grad — once with the
+    reference's torch loss/Adam/statistics and once with the fused HIP kernels
+    (SURVEY.md §8f rows 1-2).  Fresh Gaussians per variant; same seed."""
+    import torch
+
+    import synthetic
+    import train_step
+
+    out = {"definition": "render -> (1-0.2) L1 + 0.2 (1-SSIM) -> backward -> densification stats -> "
+                         "Adam (6 groups, eps 1e-15) -> zero_grad; train.py:86-141 minus logging/densify-prune"}
+    for name, fused in (("torch", False), ("fused", True)):
+        g = synthetic.make_gaussians(P, deg, seed=0).to(bg.device, requires_grad=True)
+        st = train_step.TrainState(g, spatial_lr_scale=6.6, fused=fused)
+        it = 1
+        for _ in range(3):
+            train_step.full_train_step(it, cam, g, st, target, bg)
+            it += 1
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            train_step.full_train_step(it, cam, g, st, target, bg)
+            it += 1
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out[name] = {"it_per_s": round(steps / dt, 2), "ms_per_step": round(1e3 * dt / steps, 3)}
+        del g, st
+    return out
 
 
 def _last_num_rendered(cam, g, bg) -> int:

@@ -167,6 +167,40 @@ int gsr_timing_enable(int mask);
 int gsr_timing_read(double *total_ms, int64_t *launches, int cap);
 const char *gsr_stage_name(int stage);
 
+/* ---- Training-step ops after the rasterizer (SURVEY.md §8f "next" rows 1-2) ----
+ *
+ * gsr_l1_ssim: loss = (1 - lambda) L1(img, gt) + lambda (1 - SSIM(img, gt)) for
+ * [C,H,W] float images (utils/loss_utils.py l1_loss + ssim, train.py:103-105),
+ * AND its gradient dloss/dimg in the same pass.  loss_out (device, 3 floats):
+ * loss, L1 term, mean SSIM.  scratch: gsr_l1_ssim_scratch_bytes. */
+size_t gsr_l1_ssim_scratch_bytes(int32_t C, int32_t H, int32_t W);
+int gsr_l1_ssim(const float *img, const float *gt, int32_t C, int32_t H, int32_t W, float lambda_dssim,
+                float *grad_img, void *scratch, float *loss_out, void *stream);
+
+/* gsr_adam_step: torch.optim.Adam's update (no weight decay, no amsgrad) on up
+ * to GSR_ADAM_MAX_SEGS tensors in one launch; step = the 1-based step count
+ * after the increment (scene/gaussian_model.py:176-205: six groups, eps 1e-15).
+ * betas/eps/lr are doubles, as the Python-side scalars torch derives its
+ * per-step constants from. */
+#define GSR_ADAM_MAX_SEGS 8
+typedef struct {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int64_t n;
+    double lr;
+} gsr_adam_segment;
+int gsr_adam_step(const gsr_adam_segment *segs, int32_t nseg, int32_t step, double beta1, double beta2, double eps,
+                  void *stream);
+
+/* gsr_densify_stats: for radii[i] > 0: max_radii2D[i] = max(max_radii2D[i], radii[i]),
+ * xyz_gradient_accum[i] += |viewspace_grad[i, 0:2]|, denom[i] += 1
+ * (train.py:126-127, scene/gaussian_model.py:565-581).  viewspace_grad rows
+ * are grad_stride floats apart (3 for the [P,3] means2D gradient). */
+int gsr_densify_stats(int32_t P, const int32_t *radii, const float *viewspace_grad, int32_t grad_stride,
+                      float *max_radii2D, float *xyz_gradient_accum, float *denom, void *stream);
+
 const char *gsr_last_error(void);
 int gsr_abi_version(void);
 
