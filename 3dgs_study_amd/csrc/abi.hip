@@ -267,6 +267,19 @@ int gsr_densify_stats(int32_t P, const int32_t *radii, const float *viewspace_gr
                      "densify_stats");
 }
 
+size_t gsr_knn_scratch_bytes(int32_t P) { return P > 0 ? knn_scratch_bytes(P) : 0; }
+
+int gsr_knn_mean_dist2(int32_t P, const float *points, float *dist2, void *scratch, void *stream) {
+    if (P < 0) return fail(GSR_ERR_ARGS, "knn: P must be >= 0 (got %d)", P);
+    if (P == 0) return GSR_OK;
+    if (!points || !dist2 || !scratch) return fail(GSR_ERR_ARGS, "knn: NULL buffer");
+    if (!g_pinned) {
+        if (int rc = check_hip(hipHostMalloc((void **)&g_pinned, CTRL_WORDS * 4, hipHostMallocDefault), "hipHostMalloc"))
+            return rc;
+    }
+    return check_hip(launch_knn(P, points, dist2, scratch, g_pinned, (hipStream_t)stream), "knn");
+}
+
 int gsr_timing_enable(int mask) {
     g_timer.mask = mask;
     g_timer.used = 0;

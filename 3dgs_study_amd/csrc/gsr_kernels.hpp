@@ -43,4 +43,8 @@ hipError_t launch_adam(const gsr_adam_segment *segs, int nseg, int step, double 
 hipError_t launch_densify_stats(int P, const int32_t *radii, const float *vgrad, int vstride, float *max_radii,
                                 float *grad_accum, float *denom, hipStream_t s);
 
+// knn.hip
+size_t knn_scratch_bytes(int P);
+hipError_t launch_knn(int P, const float *pts, float *dist2, void *scratch, uint32_t *pinned6, hipStream_t s);
+
 }  // namespace gsr

@@ -51,6 +51,7 @@ EXPORTED = (
     "gsr_geom_layout", "gsr_binning_layout", "gsr_img_layout", "gsr_last_error", "gsr_abi_version",
     "gsr_timing_enable", "gsr_timing_read", "gsr_stage_name",
     "gsr_l1_ssim_scratch_bytes", "gsr_l1_ssim", "gsr_adam_step", "gsr_densify_stats",
+    "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
 )
 
 
@@ -119,6 +120,10 @@ def load_library():
     lib.gsr_adam_step.restype = ctypes.c_int
     lib.gsr_densify_stats.argtypes = [i32, vp, vp, i32, vp, vp, vp, vp]
     lib.gsr_densify_stats.restype = ctypes.c_int
+    lib.gsr_knn_scratch_bytes.argtypes = [i32]
+    lib.gsr_knn_scratch_bytes.restype = sz
+    lib.gsr_knn_mean_dist2.argtypes = [i32, vp, vp, vp, vp]
+    lib.gsr_knn_mean_dist2.restype = ctypes.c_int
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_abi_version.restype = ctypes.c_int
     if lib.gsr_abi_version() != ABI_VERSION:

@@ -9,6 +9,9 @@
   (``exp_avg``, ``exp_avg_sq``, ``step``) kept like torch's.
 * ``densify_stats`` — train.py:126-127 + scene/gaussian_model.py:565-581
   (``max_radii2D``, ``xyz_gradient_accum``, ``denom``) in one HIP launch.
+* ``dist_knn3`` — ``distCUDA2`` of the simple-knn submodule (scene/gaussian_model.py:
+  153-155): mean squared distance to the 3 nearest other
+  points, exact, through a uniform-grid HIP search.
 
 All three call libgsr.so through the C ABI (include/gsr.h) on the current HIP
 stream; there is no CPU path.
@@ -17,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from diff_gaussian_rasterization import _C
@@ -125,3 +129,47 @@ def densify_stats(radii: torch.Tensor, viewspace_grad: torch.Tensor, max_radii2D
     _C._check(lib.gsr_densify_stats(P, radii.contiguous().data_ptr(), vg.data_ptr(), vg.shape[1],
                                     max_radii2D.data_ptr(), xyz_gradient_accum.data_ptr(), denom.data_ptr(),
                                     _C._stream(radii.device)), "gsr_densify_stats")
+
+
+def dist_knn3(points: torch.Tensor) -> torch.Tensor:
+    """distCUDA2(points): [P] mean of the squared distances from each point to its three
+    nearest other points (FLT_MAX stands in for missing neighbours when P < 4)."""
+    lib = _C.load_library()
+    _cuda(points, "dist_knn3")
+    if points.dim() != 2 or points.shape[1] != 3:
+        raise RuntimeError(f"dist_knn3: points must be [P,3], got {tuple(points.shape)}")
+    pts = points.detach().contiguous()
+    P = pts.shape[0]
+    out = torch.empty(P, dtype=torch.float32, device=pts.device)
+    if P == 0:
+        return out
+    scratch = torch.empty(lib.gsr_knn_scratch_bytes(P), dtype=torch.uint8, device=pts.device)
+    _C._check(lib.gsr_knn_mean_dist2(P, pts.data_ptr(), out.data_ptr(), scratch.data_ptr(), _C._stream(pts.device)),
+              "gsr_knn_mean_dist2")
+    return out
+
+
+SH_C0 = 0.28209479177387814
+
+
+def create_from_pcd(points, colors, max_sh_degree: int, device="cuda"):
+    """GaussianModel.create_from_pcd (scene/gaussian_model.py:133-174) -> SynthGaussians:
+    DC = RGB2SH(colors), higher SH zero, log scale = log(sqrt(max(dist_knn3, 1e-7))) x3,
+    identity rotation, opacity = inverse_sigmoid(0.1)."""
+    from synthetic import SynthGaussians
+
+    xyz = torch.as_tensor(np.asarray(points), dtype=torch.float32).to(device)
+    rgb = torch.as_tensor(np.asarray(colors), dtype=torch.float32).to(device)
+    P = xyz.shape[0]
+    M = (max_sh_degree + 1) ** 2
+    features = torch.zeros((P, 3, M), dtype=torch.float32, device=device)
+    features[:, :3, 0] = (rgb - 0.5) / SH_C0
+    dist2 = torch.clamp_min(dist_knn3(xyz), 0.0000001)
+    scales = torch.log(torch.sqrt(dist2))[..., None].repeat(1, 3)
+    rots = torch.zeros((P, 4), device=device)
+    rots[:, 0] = 1
+    op = torch.full((P, 1), 0.1, dtype=torch.float32, device=device)
+    opacities = torch.log(op / (1 - op))
+    return SynthGaussians(xyz, features[:, :, 0:1].transpose(1, 2).contiguous(),
+                          features[:, :, 1:].transpose(1, 2).contiguous(), scales, rots, opacities,
+                          max_sh_degree, 0)

@@ -201,6 +201,14 @@ int gsr_adam_step(const gsr_adam_segment *segs, int32_t nseg, int32_t step, doub
 int gsr_densify_stats(int32_t P, const int32_t *radii, const float *viewspace_grad, int32_t grad_stride,
                       float *max_radii2D, float *xyz_gradient_accum, float *denom, void *stream);
 
+/* gsr_knn_mean_dist2 (distCUDA2 of the absent simple-knn submodule, used at
+ * scene/gaussian_model.py:153-155): dist2[i] = mean of the squared distances
+ * from points[i] to its 3 nearest other points (exact; FLT_MAX for missing
+ * neighbours).  points [P,3] float; synchronises the stream once (the grid
+ * shape depends on the bounding box).  scratch: gsr_knn_scratch_bytes(P). */
+size_t gsr_knn_scratch_bytes(int32_t P);
+int gsr_knn_mean_dist2(int32_t P, const float *points, float *dist2, void *scratch, void *stream);
+
 const char *gsr_last_error(void);
 int gsr_abi_version(void);
 
