@@ -20,7 +20,10 @@ using namespace gsr;
 namespace {
 
 thread_local std::string g_err;
-thread_local uint32_t *g_pinned = nullptr;  // 16 control words read back per forward
+// Per host thread: pinned words the preprocess launch publishes num_rendered into
+// (the call waits for that launch's event before returning, so calls from one
+// thread never share them in flight).
+thread_local uint32_t *g_pinned = nullptr;
 thread_local hipEvent_t g_ctrl_ready = nullptr;
 
 int fail(int code, const char *fmt, ...) {
@@ -139,6 +142,14 @@ int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap) {
 const char *gsr_last_error(void) { return g_err.c_str(); }
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 
+static int ensure_pinned() {
+    if (g_pinned) return GSR_OK;
+    // coherent: the kernel's system-scope stores land in host memory directly
+    if (int rc = check_hip(hipHostMalloc((void **)&g_pinned, CTRL_WORDS * 4, hipHostMallocCoherent), "hipHostMalloc"))
+        return rc;
+    return check_hip(hipEventCreateWithFlags(&g_ctrl_ready, hipEventDisableTiming), "hipEventCreate");
+}
+
 int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered, void *stream) {
     if (int rc = validate(in, true)) return rc;
     if (!num_rendered) return fail(GSR_ERR_ARGS, "num_rendered is NULL");
@@ -147,19 +158,9 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (!geom || !radii) return fail(GSR_ERR_ARGS, "geom/radii buffers are NULL");
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
-    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, s); }), "preprocess", dbg, s)) return rc;
-    if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_scan(in->P, geom, in->W, in->H, s); }), "inclusive scan", dbg, s)) return rc;
-    if (!g_pinned) {
-        if (int rc = check_hip(hipHostMalloc((void **)&g_pinned, CTRL_WORDS * 4, hipHostMallocDefault), "hipHostMalloc"))
-            return rc;
-        if (int rc = check_hip(hipEventCreateWithFlags(&g_ctrl_ready, hipEventDisableTiming), "hipEventCreate"))
-            return rc;
-    }
-    const GeomLayout L = geom_layout(in->P, in->W, in->H);
-    if (int rc = check_hip(hipMemcpyAsync(g_pinned, at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), CTRL_WORDS * 4,
-                                          hipMemcpyDeviceToHost, s),
-                           "num_rendered read-back"))
-        return rc;
+    if (int rc = ensure_pinned()) return rc;
+    g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
+    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s); }), "preprocess", dbg, s)) return rc;
     if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
     // the depth sort does not depend on num_rendered: it runs while the host waits
     if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] { return launch_depth_sort(in->P, in->W, in->H, geom, s); }), "depth sort", dbg, s)) return rc;
@@ -188,13 +189,7 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
         if (int rc = step(timed(GSR_STAGE_TILE_SORT, s, [&] { return launch_tile_sort(in->P, in->W, in->H, geom, binning, num_rendered, s); }),
                           "tile sort", dbg, s))
             return rc;
-    } else {
-        const GeomLayout L = geom_layout(in->P, in->W, in->H);
-        if (int rc = check_hip(hipMemsetAsync(at<uint2>(geom, L.off[GSR_GEOM_RANGES]), 0,
-                                              (size_t)grid_dims(in->W, in->H).tiles * sizeof(uint2), s),
-                               "ranges memset"))
-            return rc;
-    }
+    }  // else every range stays (0, 0) as preprocess left it
     return step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s); }), "render", dbg, s);
 }
 
@@ -273,10 +268,7 @@ int gsr_knn_mean_dist2(int32_t P, const float *points, float *dist2, void *scrat
     if (P < 0) return fail(GSR_ERR_ARGS, "knn: P must be >= 0 (got %d)", P);
     if (P == 0) return GSR_OK;
     if (!points || !dist2 || !scratch) return fail(GSR_ERR_ARGS, "knn: NULL buffer");
-    if (!g_pinned) {
-        if (int rc = check_hip(hipHostMalloc((void **)&g_pinned, CTRL_WORDS * 4, hipHostMallocDefault), "hipHostMalloc"))
-            return rc;
-    }
+    if (int rc = ensure_pinned()) return rc;
     return check_hip(launch_knn(P, points, dist2, scratch, g_pinned, (hipStream_t)stream), "knn");
 }
 

@@ -285,13 +285,37 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
     }
 }
 
-// identifyTileRanges: ranges were zeroed; empty tiles stay (0, 0).
-__global__ void identify_ranges_kernel(const uint32_t *tile_keys, uint32_t n, uint2 *ranges) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t t = tile_keys[i];
-    if (i == 0 || tile_keys[i - 1] != t) ranges[t].x = i;
-    if (i == n - 1 || tile_keys[i + 1] != t) ranges[t].y = i + 1;
+// identifyTileRanges: ranges were zeroed (preprocess.hip); empty tiles stay (0, 0).
+// Four keys per thread (one 16-B load); the thread holding position i (> 0) of a
+// tile change closes the previous tile and opens the next.
+constexpr int RANGE_THREADS = 256;
+__global__ void __launch_bounds__(RANGE_THREADS) identify_ranges_kernel(const uint32_t *tile_keys, uint32_t n,
+                                                                         uint2 *ranges) {
+    const uint32_t i0 = (blockIdx.x * RANGE_THREADS + threadIdx.x) * 4u;
+    if (i0 >= n) return;
+    uint32_t v[4];
+    if (i0 + 4 <= n) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(tile_keys + i0);
+        v[0] = q.x;
+        v[1] = q.y;
+        v[2] = q.z;
+        v[3] = q.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = tile_keys[min(i0 + j, n - 1)];
+    }
+    uint32_t prev = i0 ? tile_keys[i0 - 1] : v[0];
+    if (i0 == 0) ranges[v[0]].x = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t i = i0 + j;
+        if (i < n && v[j] != prev) {
+            ranges[prev].y = i;
+            ranges[v[j]].x = i;
+        }
+        prev = i < n ? v[j] : prev;
+    }
+    if (i0 + 4 >= n) ranges[prev].y = n;
 }
 
 // ------------------------------------------------------------ launchers
@@ -386,10 +410,9 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
         cur ^= 1;
     }
     uint2 *ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
-    hipError_t e = hipMemsetAsync(ranges, 0, (size_t)g.tiles * sizeof(uint2), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(identify_ranges_kernel, dim3((unsigned)((I + 255) / 256)), dim3(256), 0, s,
-                       (const uint32_t *)keys[0], (uint32_t)I, ranges);
+    const int64_t per_block = 4 * RANGE_THREADS;
+    hipLaunchKernelGGL(identify_ranges_kernel, dim3((unsigned)((I + per_block - 1) / per_block)), dim3(RANGE_THREADS),
+                       0, s, (const uint32_t *)keys[0], (uint32_t)I, ranges);
     return hipGetLastError();
 }
 

@@ -15,7 +15,15 @@
 
 namespace gsr {
 
-constexpr int BLEND_THREADS = 256;  // 4 waves = the 4 quadrants of one tile
+// Waves per workgroup: 4 = the 4 quadrants of one tile; 1 = one quadrant per
+// workgroup (a finished quadrant frees its slot at once instead of waiting for
+// the tile's slowest quadrant).
+#ifndef GSR_BLEND_WAVES
+#define GSR_BLEND_WAVES 1
+#endif
+constexpr int BLEND_WAVES = GSR_BLEND_WAVES;
+constexpr int BLEND_THREADS = 64 * BLEND_WAVES;
+static_assert(BLEND_WAVES == 4 || BLEND_WAVES == 1, "GSR_BLEND_WAVES must be 4 or 1");
 
 // Exact cull: min over the quadrant's pixel centres [x0, x0+7] x [y0, y0+7] of
 // q(d) = ca dx^2 + 2 cb dx dy + cc dy^2 (d = pixel - mean) against qmax.  The
@@ -76,14 +84,33 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int k) { return (uint32_
 // to one XCD's L2, and the strips are dealt round-robin over the XCDs so that
 // every XCD gets an even share of the heavy centre of the image.
 constexpr int XCD_STRIP = 4;
+template <int STRIP = XCD_STRIP>
 __device__ __forceinline__ int xcd_tile(int b, int tiles) {
     const int x = b & 7, j = b >> 3;
-    const int t = ((j / XCD_STRIP) * 8 + x) * XCD_STRIP + (j % XCD_STRIP);
+    const int t = ((j / STRIP) * 8 + x) * STRIP + (j % STRIP);
     return t < tiles ? t : -1;
 }
+template <int STRIP = XCD_STRIP>
 __host__ __device__ inline int xcd_grid(int tiles) {
-    const int strips = (tiles + XCD_STRIP - 1) / XCD_STRIP;
-    return ((strips + 7) / 8) * 8 * XCD_STRIP;
+    const int strips = (tiles + STRIP - 1) / STRIP;
+    return ((strips + 7) / 8) * 8 * STRIP;
+}
+
+// (tile, quadrant) of this wave; tile < 0 = past the end of the grid
+struct QuadSlot {
+    int tile, w;
+};
+__device__ __forceinline__ QuadSlot quad_slot(int tiles) {
+    if constexpr (BLEND_WAVES == 4) {
+        // wave index in an SGPR: the LDS record addresses are then scalar + immediate
+        return {xcd_tile(blockIdx.x, tiles), __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)};
+    } else {
+        const int u = xcd_tile<4 * XCD_STRIP>(blockIdx.x, 4 * tiles);
+        return {u < 0 ? -1 : u >> 2, u & 3};
+    }
+}
+__host__ inline int blend_grid(int tiles) {
+    return BLEND_WAVES == 4 ? xcd_grid(tiles) : xcd_grid<4 * XCD_STRIP>(4 * tiles);
 }
 
 }  // namespace gsr

@@ -62,7 +62,8 @@ __host__ __device__ inline int tile_sort_passes(int T) {
 }
 __host__ __device__ inline int pre_blocks(int P) { return (P + PRE_THREADS - 1) / PRE_THREADS; }
 
-// ---- control words (uint32 [16]) inside the geom buffer ----
+// ---- control words (uint32 [16]) inside the geom buffer (a device copy of what
+// preprocess publishes to the host: num_rendered, the prefiltered error) ----
 enum CtrlWord {
     CTRL_NUM_RENDERED_LO = 0,
     CTRL_NUM_RENDERED_HI = 1,
@@ -72,7 +73,7 @@ enum CtrlWord {
 
 struct GeomLayout {
     size_t off[GSR_GEOM_NFIELDS];
-    size_t scan_sums;     // uint32 [pre_blocks(P)] block sums -> exclusive block prefixes
+    size_t block_sums;    // uint32 [pre_blocks(P)] instances per preprocess workgroup
     size_t rects;         // uint2 [P] tile rect {x0 | x1 << 16, y0 | y1 << 16}; 0 when not visible
     size_t rects_ranked;  // uint2 [P] the same in depth order (written by the last depth pass)
     size_t dsort_keys_a;  // uint32 [P] depth-sort ping-pong (the order lands in GSR_GEOM_DEPTH_ORDER)
@@ -93,11 +94,10 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.off[GSR_GEOM_SPLATS] = take((size_t)P * 48);
     L.off[GSR_GEOM_CLAMPED] = take((size_t)P);
     L.off[GSR_GEOM_TILES_TOUCHED] = take((size_t)P * 4);
-    L.off[GSR_GEOM_POINT_OFFSETS] = take((size_t)P * 4);
     L.off[GSR_GEOM_RANGES] = take((size_t)g.tiles * 8);
     L.off[GSR_GEOM_CTRL] = take(CTRL_WORDS * 4);
     L.off[GSR_GEOM_DEPTH_ORDER] = take((size_t)P * 4);
-    L.scan_sums = take((size_t)pre_blocks(P) * 4 + 4);
+    L.block_sums = take((size_t)pre_blocks(P) * 4);
     L.rects = take((size_t)P * 8);
     L.rects_ranked = take((size_t)P * 8);
     L.dsort_keys_a = take((size_t)P * 4);
@@ -139,12 +139,10 @@ struct ImgLayout {
 };
 __host__ __device__ inline ImgLayout img_layout(int W, int H) {
     ImgLayout L;
-    GridDims g = grid_dims(W, H);
     size_t o = 0;
     auto take = [&](size_t b) { size_t r = o; o = align_up(o + b, 256); return r; };
     L.off[GSR_IMG_FINAL_T] = take((size_t)W * H * 4);
     L.off[GSR_IMG_N_CONTRIB] = take((size_t)W * H * 4);
-    L.off[GSR_IMG_TILE_MAX_CONTRIB] = take((size_t)g.tiles * 4);
     L.bytes = o;
     return L;
 }

@@ -8,8 +8,7 @@
 namespace gsr {
 
 // preprocess.hip
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, hipStream_t s);
-hipError_t launch_scan(int P, void *geom, int W, int H, hipStream_t s);
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, uint32_t *host_ctrl, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 

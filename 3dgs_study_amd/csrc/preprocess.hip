@@ -27,8 +27,9 @@ struct PreArgs {
     uint8_t *clamped;
     uint32_t *tiles_touched;
     uint2 *rects;  // packed tile rect per Gaussian (binning.hip)
-    uint32_t *scan_sums;
-    uint32_t *ctrl;
+    uint2 *ranges;           // [T] zeroed here (empty tiles keep (0, 0); binning.hip fills the rest)
+    int tiles;
+    uint32_t *block_sums;    // [pre_blocks(P)] instances per workgroup | prefiltered error << 31
     int32_t *radii;
 };
 
@@ -72,6 +73,8 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         __syncthreads();
     }
     uint32_t touched = 0;
+    bool perr = false;
+    for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
     if (idx < in.P) {
         int radius_out = 0;
         uint2 rect_out = make_uint2(0u, 0u);
@@ -85,7 +88,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         bool ok = true;
         if (p_view.z <= 0.2f) {
             ok = false;
-            if (in.prefiltered) atomicOr(&a.ctrl[CTRL_PREFILTER_ERR], 1u);
+            perr = in.prefiltered != 0;
         }
         float c3[6];
         if (ok) {
@@ -160,39 +163,50 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         a.tiles_touched[idx] = touched;
         a.rects[idx] = rect_out;
     }
+    // num_rendered is only a total (emit works in depth order, binning.hip): each
+    // workgroup stores its sum, bit 31 flags a prefiltered violation
     const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
-    if (threadIdx.x == 0) a.scan_sums[blockIdx.x] = tot;
+    const int berr = __syncthreads_or(perr);
+    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = tot | (berr ? 0x80000000u : 0u);
 }
 
-// Exclusive scan of the per-block sums in place (one workgroup, any length);
-// the grand total is num_rendered.
-constexpr int TOP_THREADS = 1024;
-__global__ void __launch_bounds__(TOP_THREADS) scan_top_kernel(uint32_t *sums, int n, uint32_t *ctrl) {
-    __shared__ uint32_t wsum[TOP_THREADS / 64];
-    uint64_t carry = 0;
-    for (int base = 0; base < n; base += TOP_THREADS) {
-        const int i = base + threadIdx.x;
-        const uint32_t v = i < n ? sums[i] : 0u;
-        uint32_t tot;
-        const uint32_t inc = block_inclusive_scan<TOP_THREADS>(v, wsum, &tot);
-        if (i < n) sums[i] = (uint32_t)carry + inc - v;
-        carry += tot;
+// One workgroup totals the block sums and publishes num_rendered and the error
+// flag into the geom control words and, with system-scope stores, straight into
+// the caller's pinned host words (no copy; the host waits for this kernel's event).
+constexpr int TOTAL_THREADS = 1024;
+__global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint32_t *sums, int n, uint32_t *ctrl,
+                                                                      uint32_t *host_ctrl) {
+    __shared__ unsigned long long part[TOTAL_THREADS / 64];
+    __shared__ uint32_t perr[TOTAL_THREADS / 64];
+    unsigned long long t = 0;
+    uint32_t e = 0;
+    for (int i = threadIdx.x; i < n; i += TOTAL_THREADS) {
+        const uint32_t v = sums[i];
+        t += v & 0x7fffffffu;
+        e |= v >> 31;
     }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        t += __shfl_xor(t, o);
+        e |= __shfl_xor(e, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[threadIdx.x >> 6] = t;
+        perr[threadIdx.x >> 6] = e;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        ctrl[CTRL_NUM_RENDERED_LO] = (uint32_t)carry;
-        ctrl[CTRL_NUM_RENDERED_HI] = (uint32_t)(carry >> 32);
+        for (int k = 1; k < TOTAL_THREADS / 64; k++) {
+            t += part[k];
+            e |= perr[k];
+        }
+        const uint32_t w[3] = {(uint32_t)t, (uint32_t)(t >> 32), e};
+        for (int k = 0; k < 3; k++) {
+            ctrl[k] = w[k];
+            __hip_atomic_store(&host_ctrl[k], w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __threadfence_system();
     }
-}
-
-// point_offsets = inclusive scan of tiles_touched (block prefix + in-block scan).
-__global__ void __launch_bounds__(PRE_THREADS)
-    scan_down_kernel(const uint32_t *tiles_touched, const uint32_t *block_prefix, uint32_t *offsets, int P) {
-    __shared__ uint32_t wsum[PRE_THREADS / 64];
-    const int idx = blockIdx.x * PRE_THREADS + threadIdx.x;
-    const uint32_t v = idx < P ? tiles_touched[idx] : 0u;
-    uint32_t tot;
-    const uint32_t inc = block_inclusive_scan<PRE_THREADS>(v, wsum, &tot);
-    if (idx < P) offsets[idx] = block_prefix[blockIdx.x] + inc;
 }
 
 // auxiliary.h in_frustum via checkFrustum (markVisible).
@@ -205,7 +219,7 @@ __global__ void mark_visible_kernel(int P, const float *means3D, const float *vi
     present[idx] = !(pv.z <= 0.2f);
 }
 
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, hipStream_t s) {
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, uint32_t *host_ctrl, hipStream_t s) {
     const GeomLayout L = geom_layout(in.P, in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
     PreArgs a;
@@ -220,26 +234,15 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, h
     a.clamped = at<uint8_t>(geom, L.off[GSR_GEOM_CLAMPED]);
     a.tiles_touched = at<uint32_t>(geom, L.off[GSR_GEOM_TILES_TOUCHED]);
     a.rects = at<uint2>(geom, L.rects);
-    a.scan_sums = at<uint32_t>(geom, L.scan_sums);
-    a.ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+    a.ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
+    a.tiles = g.tiles;
+    a.block_sums = at<uint32_t>(geom, L.block_sums);
     a.radii = radii;
-    hipError_t e = hipMemsetAsync(a.ctrl, 0, CTRL_WORDS * 4, s);
-    if (e != hipSuccess) return e;
     const int nb = pre_blocks(in.P);
     const size_t lds = (in.sh && !in.colors_precomp) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     hipLaunchKernelGGL(preprocess_fwd_kernel, dim3(nb), dim3(PRE_THREADS), lds, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_scan(int P, void *geom, int W, int H, hipStream_t s) {
-    const GeomLayout L = geom_layout(P, W, H);
-    uint32_t *sums = at<uint32_t>(geom, L.scan_sums);
-    uint32_t *ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
-    const int nb = pre_blocks(P);
-    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(TOP_THREADS), 0, s, sums, nb, ctrl);
-    hipLaunchKernelGGL(scan_down_kernel, dim3(nb), dim3(PRE_THREADS), 0, s,
-                       at<const uint32_t>(geom, L.off[GSR_GEOM_TILES_TOUCHED]), (const uint32_t *)sums,
-                       at<uint32_t>(geom, L.off[GSR_GEOM_POINT_OFFSETS]), P);
+    hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint32_t *)a.block_sums, nb,
+                       at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl);
     return hipGetLastError();
 }
 

@@ -158,12 +158,6 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
     const float4 acc1 = *reinterpret_cast<const float4 *>(acc + 4);  // conic.w, opacity, color r, color g
     const float accb = acc[8];                                       // color b
     const float dcol[3] = {acc1.z, acc1.w, accb};
-    // render_bwd.hip accumulates sum W (conic' d) and sum W (dx^2, dx dy, dy^2);
-    // the per-Gaussian constant factors are applied here
-    const float g2x = acc0.x * (float)in.W, g2y = acc0.y * (float)in.H;  // dL/dmean2D
-    o.dmeans2D[3 * (size_t)idx + 0] = g2x;
-    o.dmeans2D[3 * (size_t)idx + 1] = g2y;
-    o.dmeans2D[3 * (size_t)idx + 2] = 0.f;
     o.dcolors[3 * (size_t)idx + 0] = dcol[0];
     o.dcolors[3 * (size_t)idx + 1] = dcol[1];
     o.dcolors[3 * (size_t)idx + 2] = dcol[2];
@@ -205,6 +199,16 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
     const float cc = cov2D.m[1][1] += 0.3f;
     const float gx = -0.5f * acc0.z, gy = -0.5f * acc0.w, gz = -0.5f * acc1.x;  // dL/dconic x, y, w
     const float denom = ca * cc - cb * cb;
+    // render_bwd.hip accumulates sum W (dx, dy) and sum W (dx^2, dx dy, dy^2); the
+    // per-Gaussian factors -conic/2 (the forward's conic, preprocess.hip) and
+    // (W, H) of dL/dmean2D are applied here
+    const float det_inv = 1.f / denom;
+    const float kx = cc * det_inv, ky = -cb * det_inv, kz = ca * det_inv;
+    const float g2x = -0.5f * (kx * acc0.x + ky * acc0.y) * (float)in.W;
+    const float g2y = -0.5f * (ky * acc0.x + kz * acc0.y) * (float)in.H;
+    o.dmeans2D[3 * (size_t)idx + 0] = g2x;
+    o.dmeans2D[3 * (size_t)idx + 1] = g2y;
+    o.dmeans2D[3 * (size_t)idx + 2] = 0.f;
     float dL_da = 0, dL_db = 0, dL_dc = 0;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
     float dc3[6] = {0, 0, 0, 0, 0, 0};

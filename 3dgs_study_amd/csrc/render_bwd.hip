@@ -12,15 +12,27 @@
 // lane-parallel exact cull as the forward, and walks the surviving Gaussians
 // from the back, two Gaussians per iteration.  Upstream issues ~9 float atomics
 // per contributing (pixel, Gaussian) pair; here the 2 x 9 partials are summed
-// over the wave's 64 pixels by one reduce-scatter (v_permlane32_swap,
-// v_permlane16_swap, DPP row shifts: ~25 VALU per Gaussian) and ONE 9-lane
-// atomic wave-instruction per Gaussian adds them to its 64-byte accumulator
-// row — a single memory-side atomic request, the resource that bounds this
-// kernel (MI355X_MICROARCH.md §Global float atomics: ~20 G requests/s).
+// over the wave's 64 pixels by one reduce-scatter — five ds_swizzle stages
+// inside each 32-lane half (the exchanges run in the LDS pipe; DPP adds and
+// v_permlane swaps cost 3.5x / 7x a plain VALU op on gfx950, tests/hip/
+// xlane_probe.hip) and one v_permlane32 self-swap — and ONE 9-lane atomic
+// wave-instruction per Gaussian adds them to its 64-byte accumulator row: a
+// single memory-side atomic request (splitting it, e.g. one per 32-lane half,
+// doubled the kernel's time).
 #include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
 
 namespace gsr {
+
+#ifdef GSR_BWD_STATS
+// Work counters for tuning (tools/bwd_stats.py): waves, chunks, pairs walked,
+// pairs with a contributing pixel, quadrant hits, end entries, valid lanes.
+__device__ unsigned long long g_bwd_stats[8];
+#define BWD_STAT(k, v) \
+    do { if (lane == 0) atomicAdd(&g_bwd_stats[k], (unsigned long long)(v)); } while (0)
+#else
+#define BWD_STAT(k, v) do { } while (0)
+#endif
 
 struct RenderBwdArgs {
     int W, H, gx, tiles;
@@ -43,25 +55,22 @@ __device__ __forceinline__ float swap32_sum(float a, float b) {  // -> [a_lo + a
     const uint32_t x = r[0], y = r[1];
     return __builtin_bit_cast(float, x) + __builtin_bit_cast(float, y);
 }
-__device__ __forceinline__ float swap16_sum(float a, float b) {  // rows: [a0+a1 | b0+b1 | a2+a3 | b2+b3]
-    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
-                                                    false, false);
-    const uint32_t x = r[0], y = r[1];
-    return __builtin_bit_cast(float, x) + __builtin_bit_cast(float, y);
-}
-__device__ __forceinline__ float row_sum_to_lane15(float v) {  // sum of each 16-lane row lands in its lane 15
-    v += dpp_f32<DPP_ROW_SHR1>(v);
-    v += dpp_f32<DPP_ROW_SHR2>(v);
-    v += dpp_f32<DPP_ROW_SHR4>(v);  // only lane 15 is consumed: no bank masks needed,
-    v += dpp_f32<DPP_ROW_SHR8>(v);  // so each step is one v_add_f32_dpp
-    return v;
+// One ds_swizzle reduce-scatter step inside each 32-lane half: lanes with bit K
+// clear keep c, the others d, and each adds its partner's (lane ^ K) copy of the
+// other one.  The exchange runs in the LDS pipe; the VALU pays two selects and
+// an add (a DPP add costs ~3.5 plain adds on gfx950, a v_permlane swap ~7).
+template <int K>
+__device__ __forceinline__ float swz_stage(float c, float d, int lane) {
+    const bool hi = (lane & K) != 0;
+    const float keep = hi ? d : c, send = hi ? c : d;
+    return keep + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send), 0x1F | (K << 10)));
 }
 
 __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs a) {
-    const int tile = xcd_tile(blockIdx.x, a.tiles);
+    const QuadSlot qs = quad_slot(a.tiles);
+    const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
     if (tile < 0) return;
     const int tx = tile % a.gx, ty = tile / a.gx;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
@@ -84,9 +93,11 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) end = max(end, __shfl_xor(end, o));
     if (end <= 0) return;
+    BWD_STAT(0, 1);
+    BWD_STAT(5, end);
 
-    __shared__ ChunkStage stage[BLEND_THREADS / 64];
-    ChunkStage &st = stage[w];
+    __shared__ ChunkStage stage[BLEND_WAVES];
+    ChunkStage &st = stage[BLEND_WAVES == 1 ? 0 : w];
     float T = T_final;
     float R0 = 0.f, R1 = 0.f, R2 = 0.f;
     const uint32_t *list = a.point_list + r.x;
@@ -99,8 +110,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     // checks every gradient.)
     int slot_a = -1, slot_b = -1;
     {
-        constexpr int8_t LA[9] = {0, 32, 16, 48, 8, 40, 24, 56, 4};
-        constexpr int8_t LB[9] = {20, 52, 12, 44, 28, 60, 2, 34, 36};
+        constexpr int8_t LA[9] = {0, 16, 8, 24, 4, 20, 12, 28, 2};
+        constexpr int8_t LB[9] = {50, 42, 58, 38, 54, 46, 62, 33, 49};
 #pragma unroll
         for (int j = 0; j < 9; j++) {
             slot_a = lane == LA[j] ? j : slot_a;
@@ -108,22 +119,18 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         }
     }
     const bool act_a = slot_a >= 0, act_b = slot_b >= 0;
-    // one reduce-scatter step inside a row: lanes with `bit` clear keep c, the
-    // others d; each adds the partner's copy (DPP pattern CTRL pairs the lanes)
-    auto rs_keep = [&](float c, float d, int bit) { return (lane & bit) ? d : c; };
-    auto rs_send = [&](float c, float d, int bit) { return (lane & bit) ? c : d; };
 
     struct Pre {
-        float dx, dy, ux, uy, G, alpha;
+        float dx, dy, G, alpha;
         bool valid;
     };
     auto prepare = [&](float4 p0, float4 p1, int k, int lim, bool live) {  // valid needs lo + k < last_contrib
         Pre q;
         q.dx = p0.x - fx;
         q.dy = p0.y - fy;
-        q.ux = p0.z * q.dx + p0.w * q.dy;  // conic' * d with conic' = -conic/2 (splat record)
-        q.uy = p0.w * q.dx + p1.x * q.dy;
-        const float power = q.dx * q.ux + q.dy * q.uy;  // upstream's power; == render_fwd.hip, bit for bit
+        const float ux = p0.z * q.dx + p0.w * q.dy;  // conic' * d with conic' = -conic/2 (splat record)
+        const float uy = p0.w * q.dx + p1.x * q.dy;
+        const float power = q.dx * ux + q.dy * uy;  // upstream's power; == render_fwd.hip, bit for bit
         q.G = __expf(power);
         q.alpha = fminf(0.99f, p1.y * q.G);
         q.valid = live && k < lim && !(power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
@@ -138,7 +145,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     // last_alpha * last_color + (1 - last_alpha) * accum_rec.
     auto replay = [&](const Pre &q, float op, float cr, float cg, float cb) {
         const float av = q.valid ? q.alpha : 0.0f;
-        const float Gv = q.valid ? q.G : 0.0f;
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
         T = T * inv_1ma;
         const float dchannel_dcolor = av * T;
@@ -150,19 +156,19 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         // dL/dalpha (upstream: sum_c (c - accum_rec) dL_dpix_c * T - T_final/(1-alpha) * bg.dL_dpix)
         const float dL_dalpha = q.valid ? dot * T + inv_1ma * nTbg : 0.0f;
         // dG/d(delta) = -G conic d; with W = G * opacity * dL/dalpha the per-pixel
-        // terms are dmean2D = -W (conic d) (W/2, H/2) = W (conic' d) (W, H) and
-        // dconic = -W/2 (dx^2, dx dy, dy^2).  The constant factors (W, H) and -1/2
-        // are applied once per Gaussian in preprocess_bwd.hip, so the accumulator
-        // holds sum W (conic' d) and sum W (dx^2, dx dy, dy^2).
+        // terms are dmean2D = -W (conic d) (W/2, H/2) and dconic = -W/2 (dx^2,
+        // dx dy, dy^2).  conic, (W, H) and -1/2 are per-Gaussian constants applied
+        // once in preprocess_bwd.hip, so the accumulator holds sum W (dx, dy) and
+        // sum W (dx^2, dx dy, dy^2).  G is finite (power <= 0 for the positive-
+        // definite conic), so an invalid pixel's zero dL/dalpha zeroes them all.
         G9 g;
-        g.g5 = Gv * dL_dalpha;
+        g.g5 = q.G * dL_dalpha;
         const float Wg = g.g5 * op;
-        const float wdx = Wg * q.dx;
-        g.g0 = Wg * q.ux;
-        g.g1 = Wg * q.uy;
-        g.g2 = wdx * q.dx;
-        g.g3 = wdx * q.dy;
-        g.g4 = Wg * q.dy * q.dy;
+        g.g0 = Wg * q.dx;
+        g.g1 = Wg * q.dy;
+        g.g2 = g.g0 * q.dx;
+        g.g3 = g.g0 * q.dy;
+        g.g4 = g.g1 * q.dy;
         g.g6 = dchannel_dcolor * dpx0;
         g.g7 = dchannel_dcolor * dpx1;
         g.g8 = dchannel_dcolor * dpx2;
@@ -176,6 +182,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         stage_chunk(st, lane, A, B, C);
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         uint64_t mask = __ballot(rel);
+        BWD_STAT(1, 1);
+        BWD_STAT(4, __builtin_popcountll(mask));
         const int lim = last_contrib - lo;  // entry lo + k replays for this pixel iff k < lim
         while (mask) {
             const int ka = 63 - __builtin_clzll(mask);
@@ -189,34 +197,42 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
             const float2 b2 = *reinterpret_cast<const float2 *>(&st.rec[kb][2]);
             const Pre qa = prepare(a0, a1, ka, lim, true);  // entry lo + k = upstream `contributor`
             const Pre qb = prepare(b0, b1, kb, lim, two);
-            if (!__any(qa.valid || qb.valid)) continue;
+            BWD_STAT(2, 1);
+            // (no early-out for pairs without a contributing pixel: 98.6% of the
+            // walked pairs have one at config C, the test cost more than it saved)
+#ifdef GSR_BWD_STATS
+            {
+                const uint64_t va = __builtin_amdgcn_ballot_w64(qa.valid), vb = __builtin_amdgcn_ballot_w64(qb.valid);
+                BWD_STAT(3, (va | vb) != 0);
+                BWD_STAT(6, __builtin_popcountll(va) + __builtin_popcountll(vb));
+            }
+#endif
             const G9 ga = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: ka > kb
             const G9 gb = replay(qb, b1.y, b1.z, b1.w, b2.x);
-            // reduce-scatter of the 18 sums over 64 lanes (convergent: all lanes active)
-            const float h0 = swap32_sum(ga.g0, ga.g1);  // lanes 0-31: first, 32-63: second
-            const float h1 = swap32_sum(ga.g2, ga.g3);
-            const float h2 = swap32_sum(ga.g4, ga.g5);
-            const float h3 = swap32_sum(ga.g6, ga.g7);
-            const float h4 = swap32_sum(ga.g8, gb.g8);
-            const float h5 = swap32_sum(gb.g0, gb.g1);
-            const float h6 = swap32_sum(gb.g2, gb.g3);
-            const float h7 = swap32_sum(gb.g4, gb.g5);
-            const float h8 = swap32_sum(gb.g6, gb.g7);
-            // stage 2: v_permlane16_swap, 9 -> 5 registers (rows hold distinct sums)
-            const float k0 = swap16_sum(h0, h1);
-            const float k1 = swap16_sum(h2, h3);
-            const float k2 = swap16_sum(h4, h5);
-            const float k3 = swap16_sum(h6, h7);
-            const float k4 = swap16_sum(h8, 0.f);
-            // stages 3-6 inside each 16-lane row, DPP partners: row_ror:8 (lane ^ 8),
-            // row_half_mirror (lane ^ 7), quad_perm xor 2, quad_perm xor 1
-            const float m0 = rs_keep(k0, k1, 8) + dpp_f32<DPP_ROW_ROR8>(rs_send(k0, k1, 8));
-            const float m1 = rs_keep(k2, k3, 8) + dpp_f32<DPP_ROW_ROR8>(rs_send(k2, k3, 8));
-            const float m2 = rs_keep(k4, 0.f, 8) + dpp_f32<DPP_ROW_ROR8>(rs_send(k4, 0.f, 8));
-            const float n0 = rs_keep(m0, m1, 4) + dpp_f32<DPP_ROW_HALF_MIRROR>(rs_send(m0, m1, 4));
-            const float n1 = rs_keep(m2, 0.f, 4) + dpp_f32<DPP_ROW_HALF_MIRROR>(rs_send(m2, 0.f, 4));
-            const float o0 = rs_keep(n0, n1, 2) + dpp_f32<DPP_QUAD_XOR2>(rs_send(n0, n1, 2));
-            const float v = o0 + dpp_f32<DPP_QUAD_XOR1>(o0);  // odd lanes: unused duplicates
+            // reduce-scatter of the 18 sums inside each 32-lane half with ds_swizzle
+            // (xor 16, 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per output
+            // register) and one final v_permlane32 self-swap adding the two halves
+            const float s0 = swz_stage<16>(ga.g0, ga.g1, lane);
+            const float s1 = swz_stage<16>(ga.g2, ga.g3, lane);
+            const float s2 = swz_stage<16>(ga.g4, ga.g5, lane);
+            const float s3 = swz_stage<16>(ga.g6, ga.g7, lane);
+            const float s4 = swz_stage<16>(ga.g8, gb.g0, lane);
+            const float s5 = swz_stage<16>(gb.g1, gb.g2, lane);
+            const float s6 = swz_stage<16>(gb.g3, gb.g4, lane);
+            const float s7 = swz_stage<16>(gb.g5, gb.g6, lane);
+            const float s8 = swz_stage<16>(gb.g7, gb.g8, lane);
+            const float t0 = swz_stage<8>(s0, s1, lane);
+            const float t1 = swz_stage<8>(s2, s3, lane);
+            const float t2 = swz_stage<8>(s4, s5, lane);
+            const float t3 = swz_stage<8>(s6, s7, lane);
+            const float t4 = swz_stage<8>(s8, 0.f, lane);
+            const float u0 = swz_stage<4>(t0, t1, lane);
+            const float u1 = swz_stage<4>(t2, t3, lane);
+            const float u2 = swz_stage<4>(t4, 0.f, lane);
+            const float w0 = swz_stage<2>(u0, u1, lane);
+            const float w1 = swz_stage<2>(u2, 0.f, lane);
+            const float o0 = swz_stage<1>(w0, w1, lane);
+            const float v = swap32_sum(o0, o0);  // both halves: the full sum
             // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
             // compiler's atomic optimizer (a wave-scan loop) out
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.y));
@@ -270,8 +286,17 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
     a.dL_dpix = dL_dpix;
     a.accum = accum;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(xcd_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
+    hipLaunchKernelGGL(render_bwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
 
 }  // namespace gsr
+
+#ifdef GSR_BWD_STATS
+extern "C" int gsr_debug_bwd_stats(unsigned long long *out) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_bwd_stats), sizeof(gsr::g_bwd_stats));
+    const unsigned long long z[8] = {};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_bwd_stats), z, sizeof z);
+}
+#endif

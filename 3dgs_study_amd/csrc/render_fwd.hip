@@ -28,14 +28,13 @@ struct RenderFwdArgs {
     float *out_color;
     float *final_T;
     uint32_t *n_contrib;
-    uint32_t *tile_maxc;
 };
 
 __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs a) {
-    const int tile = xcd_tile(blockIdx.x, a.tiles);
+    const QuadSlot qs = quad_slot(a.tiles);
+    const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
     if (tile < 0) return;
     const int tx = tile % a.gx, ty = tile / a.gx;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
@@ -46,8 +45,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
     uint32_t last = 0;
     float live = inside ? 1.0f : 0.0f;  // 0 once the pixel has stopped (or lies outside the image)
-    __shared__ ChunkStage stage[BLEND_THREADS / 64];
-    ChunkStage &st = stage[w];
+    __shared__ ChunkStage stage[BLEND_WAVES];
+    ChunkStage &st = stage[BLEND_WAVES == 1 ? 0 : w];
     if (__any(inside) && n > 0) {
         const uint32_t *list = a.point_list + r.x;
         const int nm1 = n - 1;
@@ -147,11 +146,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
         a.out_color[HW + pix] = C1 + T * a.bg[1];
         a.out_color[2 * HW + pix] = C2 + T * a.bg[2];
     }
-    // per-quadrant max n_contrib -> tile max (the backward starts its walk there)
-    uint32_t m = last;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    if (lane == 0) atomicMax(&a.tile_maxc[tile], m);
 }
 
 hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,
@@ -171,10 +165,7 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
     a.out_color = out_color;
     a.final_T = at<float>(img, Im.off[GSR_IMG_FINAL_T]);
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
-    a.tile_maxc = at<uint32_t>(img, Im.off[GSR_IMG_TILE_MAX_CONTRIB]);
-    hipError_t e = hipMemsetAsync(a.tile_maxc, 0, (size_t)g.tiles * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(render_fwd_kernel, dim3(xcd_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
+    hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

@@ -62,7 +62,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lib = None
 
@@ -294,7 +294,6 @@ def layouts(P, W, H, num_rendered):
     nb = lib.gsr_binning_layout(num_rendered, W, H, b, 16)
     im = (ctypes.c_size_t * 16)()
     ni = lib.gsr_img_layout(W, H, im, 16)
-    geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "point_offsets", "ranges", "ctrl",
-                  "depth_order")
+    geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "ranges", "ctrl", "depth_order")
     return (dict(zip(geom_names, list(g)[:n])), dict(zip(("keys", "point_list"), list(b)[:nb])),
-            dict(zip(("final_T", "n_contrib", "tile_max_contrib"), list(im)[:ni])))
+            dict(zip(("final_T", "n_contrib"), list(im)[:ni])))

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 2
+#define GSR_ABI_VERSION 3
 
 enum gsr_status {
     GSR_OK = 0,
@@ -125,7 +125,6 @@ enum gsr_geom_field {
     GSR_GEOM_SPLATS,         /* float4 [P][3] {x,y,c.x,c.y},{c.z,opacity,r,g},{b,id bits,qmax,0}, c = -conic/2, qmax = -bound/2 */
     GSR_GEOM_CLAMPED,        /* uint8  [P]  bit c set = channel c clamped in SH->RGB */
     GSR_GEOM_TILES_TOUCHED,  /* uint32 [P] */
-    GSR_GEOM_POINT_OFFSETS,  /* uint32 [P]  inclusive scan of tiles_touched */
     GSR_GEOM_RANGES,         /* uint2  [T]  [start,end) of each tile in point_list */
     GSR_GEOM_CTRL,           /* uint32 [16] num_rendered, status flags */
     GSR_GEOM_DEPTH_ORDER,    /* uint32 [P]  Gaussian ids in (depth_bits, id) order */
@@ -139,7 +138,6 @@ enum gsr_binning_field {
 enum gsr_img_field {
     GSR_IMG_FINAL_T = 0,     /* float  [H*W] */
     GSR_IMG_N_CONTRIB,       /* uint32 [H*W] */
-    GSR_IMG_TILE_MAX_CONTRIB,/* uint32 [T]  max n_contrib over the tile's pixels */
     GSR_IMG_NFIELDS
 };
 int gsr_geom_layout(int32_t P, int32_t W, int32_t H, size_t *offsets, int cap);

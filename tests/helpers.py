@@ -81,7 +81,7 @@ def read_intermediates(geom, binning, img, P, W, H, I):
     d["splats"] = _view(geom, go["splats"], 12 * P, torch.float32, np.float32).reshape(P, 12)
     d["clamped"] = _view(geom, go["clamped"], P, torch.uint8, np.uint8)
     d["tiles_touched"] = _view(geom, go["tiles_touched"], P, torch.int32, np.uint32)
-    d["point_offsets"] = _view(geom, go["point_offsets"], P, torch.int32, np.uint32)
+    d["ctrl"] = _view(geom, go["ctrl"], 16, torch.int32, np.uint32)
     d["ranges"] = _view(geom, go["ranges"], 2 * T, torch.int32, np.uint32).reshape(T, 2)
     d["depth_order"] = _view(geom, go["depth_order"], P, torch.int32, np.uint32)
     if I > 0:
@@ -92,7 +92,6 @@ def read_intermediates(geom, binning, img, P, W, H, I):
         d["point_list"] = np.zeros(0, np.uint32)
     d["final_T"] = _view(img, io["final_T"], W * H, torch.float32, np.float32).reshape(H, W)
     d["n_contrib"] = _view(img, io["n_contrib"], W * H, torch.int32, np.uint32).reshape(H, W)
-    d["tile_max_contrib"] = _view(img, io["tile_max_contrib"], T, torch.int32, np.uint32)
     return d
 
 

@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 2
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 3
     # 10 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 40 + 11 * 8
     assert _C.GsrInputs.bg.offset == 40

@@ -6,9 +6,14 @@ TAG=${1:-prof}
 shift
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof" -o run -- \
-    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline "$@" > "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof.log" 2>&1
+# raw traces stay in /tmp (they exceed what gpurun copies back); only the summary returns
+RAW=/tmp/${TAG}_prof
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$RAW" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --full-steps 0 "$@" \
+    > "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof.log" 2>&1
 rc=$?
 cd "$GRAFT_REPO_ROOT"
-python3 tools/prof_summary.py gpurun_out/${TAG}_prof gpurun_out/${TAG}_kernel_stats.csv --top 28
+python3 tools/prof_summary.py "$RAW" gpurun_out/${TAG}_kernel_stats.csv --top 40 --step-trace gpurun_out/${TAG}_step_trace.csv
+f=$(find "$RAW" -name "*kernel_stats.csv" | head -1)
+[ -n "$f" ] && cp "$f" gpurun_out/${TAG}_rocprof_kernel_stats.csv
 exit $rc

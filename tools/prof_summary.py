@@ -34,5 +34,19 @@ with open(out, "w", newline="") as f:
     w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "StdDev"])
     for r in stats:
         w.writerow([r[0], r[1], int(r[2]), round(r[3], 1), round(r[4], 2), int(r[5]), int(r[6]), round(r[7], 1)])
+# one step's dispatch sequence: the kernels between the last two preprocess launches
+if "--step-trace" in sys.argv:
+    seq = con.execute("select name, start, end from kernels order by start").fetchall()
+    marks = [i for i, r in enumerate(seq) if "preprocess_fwd_kernel" in r[0]]
+    if len(marks) >= 3:
+        a, b = marks[-3], marks[-2]
+        t0 = seq[a][1]
+        with open(sys.argv[sys.argv.index("--step-trace") + 1], "w") as f:
+            f.write("start_us,dur_us,gap_us,name\n")
+            prev = t0
+            for name, st, en in seq[a:b]:
+                f.write(f"{(st - t0) / 1e3:.1f},{(en - st) / 1e3:.1f},{(st - prev) / 1e3:.1f},{name[:120]}\n")
+                prev = en
+            f.write(f"{(seq[b][1] - t0) / 1e3:.1f},0,0,<next step>\n")
 for r in stats[:top]:
     print(f"{r[2] / 1e6:8.2f} ms {r[1]:5d} {r[3] / 1e3:8.1f} us  {r[0][:90]}")

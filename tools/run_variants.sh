@@ -1,15 +1,21 @@
 #!/bin/bash
-# On the box: time each variant library with a short bench run.
-#   bash tools/run_variants.sh A B ...
+# On the box: time each variant library with short bench runs, round-robin over
+# ROUNDS rounds (default 2) so clock drift hits every variant alike.
+#   ROUNDS=3 bash tools/run_variants.sh base A B ...
 set -o pipefail
 mkdir -p gpurun_out
-for v in "$@"; do
-  lib=$PWD/3dgs_study_amd/lib/libgsr_$v.so
-  [ "$v" = base ] && lib=$PWD/3dgs_study_amd/lib/libgsr.so
-  GSR_LIBRARY=$lib timeout -k 10 200 python bench.py --steps 30 --warmup 10 --no-cpu-baseline > gpurun_out/var_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/var_$v.log; exit 1; }
-  python - "$v" gpurun_out/var_$v.log <<'PY'
+ROUNDS=${ROUNDS:-2}
+for r in $(seq 1 $ROUNDS); do
+  for v in "$@"; do
+    lib=$PWD/3dgs_study_amd/lib/libgsr_$v.so
+    [ "$v" = base ] && lib=$PWD/3dgs_study_amd/lib/libgsr.so
+    GSR_LIBRARY=$lib timeout -k 10 200 python bench.py --steps 60 --warmup 10 --no-cpu-baseline --full-steps 0 \
+        > gpurun_out/var_${v}_$r.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/var_${v}_$r.log; exit 1; }
+    python - "$v" gpurun_out/var_${v}_$r.log <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
-print(sys.argv[1], d["value"], d["stages_ms"])
+s = d["stages_ms"]
+print(f"{sys.argv[1]:>10} {d['value']:8.2f}  " + " ".join(f"{k[:8]}={v * 1e3:.0f}" for k, v in s.items() if v))
 PY
+  done
 done
