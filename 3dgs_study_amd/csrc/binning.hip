@@ -63,8 +63,8 @@ struct RadixPass {
     const uint32_t *vin;   // values; nullptr = the item index
     uint32_t *kout;        // nullptr = keys not needed after this pass
     uint32_t *vout;
-    const uint2 *gsrc;     // optional: gdst[pos] = gsrc[value] for every written value
-    uint2 *gdst;
+    const uint4 *gsrc;     // optional: gdst[pos] = gsrc[value] for every written value
+    uint4 *gdst;
     uint32_t n;
     int shift;
     int nbits;             // significant bits of this pass's digit (<= RADIX_BITS)
@@ -213,15 +213,40 @@ static hipError_t radix_pass(const RadixPass &a, hipStream_t s) {
 
 // ------------------------------------------------------------ rank-order scan
 
-__device__ __forceinline__ uint32_t rect_area(uint2 q) {
+__device__ __forceinline__ uint32_t rect_area(uint4 q) {
     return ((q.x >> 16) - (q.x & 0xffffu)) * ((q.y >> 16) - (q.y & 0xffffu));
+}
+// instances of a Gaussian: the set bits of its tile mask (preprocess.hip), or the
+// whole rect when it spans more than 64 tiles
+__device__ __forceinline__ uint32_t rect_count(uint4 q) {
+    const uint32_t area = rect_area(q);
+    return area <= 64 ? (uint32_t)(__builtin_popcount(q.z) + __builtin_popcount(q.w)) : area;
+}
+// index of the k-th set bit (k < popcount) of the 64-bit mask {lo, hi}
+__device__ __forceinline__ uint32_t kth_set_bit(uint32_t lo, uint32_t hi, uint32_t k) {
+    uint32_t c = __builtin_popcount(lo), x = lo, base = 0;
+    if (k >= c) {
+        k -= c;
+        x = hi;
+        base = 32;
+    }
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        c = __builtin_popcount(x & ((1u << w) - 1u));
+        if (k >= c) {
+            k -= c;
+            x >>= w;
+            base += w;
+        }
+    }
+    return base;
 }
 
 __global__ void __launch_bounds__(EMIT_BLOCK)
-    rank_sums_kernel(const uint2 *rects_ranked, int P, uint32_t *sums) {
+    rank_sums_kernel(const uint4 *rects_ranked, int P, uint32_t *sums) {
     __shared__ uint32_t wsum[EMIT_BLOCK / 64];
     const int r = blockIdx.x * EMIT_BLOCK + threadIdx.x;
-    const uint32_t v = r < P ? rect_area(rects_ranked[r]) : 0u;
+    const uint32_t v = r < P ? rect_count(rects_ranked[r]) : 0u;
     const uint32_t tot = block_sum<EMIT_BLOCK>(v, wsum);
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
@@ -247,7 +272,7 @@ __global__ void __launch_bounds__(TOPSCAN_THREADS) exclusive_scan_one_block_kern
 struct EmitArgs {
     int P, gx;
     const uint32_t *order;
-    const uint2 *rects;
+    const uint4 *rects;
     const uint32_t *block_prefix;
     uint32_t *tile_keys;
     uint32_t *ids;
@@ -256,15 +281,19 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
     __shared__ uint32_t wsum[EMIT_BLOCK / 64];
     __shared__ uint32_t loff[EMIT_BLOCK + 1];
     __shared__ uint4 rect[EMIT_BLOCK];  // x0, width, y0, id
+    __shared__ uint2 mask[EMIT_BLOCK];  // tile mask; {~0, ~0} = every tile of the rect
     const int r = blockIdx.x * EMIT_BLOCK + threadIdx.x;
     const uint32_t id = r < a.P ? a.order[r] : 0u;
-    const uint2 q = r < a.P ? a.rects[r] : make_uint2(0u, 0u);  // rects in depth order
-    const uint32_t v = rect_area(q);
+    const uint4 q = r < a.P ? a.rects[r] : make_uint4(0u, 0u, 0u, 0u);  // rects in depth order
+    const uint32_t v = rect_count(q);
     uint32_t tot;
     const uint32_t inc = block_inclusive_scan<EMIT_BLOCK>(v, wsum, &tot);
     loff[threadIdx.x] = inc - v;
     if (threadIdx.x == EMIT_BLOCK - 1) loff[EMIT_BLOCK] = tot;
-    if (v) rect[threadIdx.x] = make_uint4(q.x & 0xffffu, (q.x >> 16) - (q.x & 0xffffu), q.y & 0xffffu, id);
+    if (v) {
+        rect[threadIdx.x] = make_uint4(q.x & 0xffffu, (q.x >> 16) - (q.x & 0xffffu), q.y & 0xffffu, id);
+        mask[threadIdx.x] = rect_area(q) <= 64 ? make_uint2(q.z, q.w) : make_uint2(~0u, ~0u);
+    }
     __syncthreads();
     const uint32_t base = a.block_prefix[blockIdx.x];
     for (uint32_t j = threadIdx.x; j < tot; j += EMIT_BLOCK) {
@@ -275,11 +304,14 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
             if (loff[mid] <= j) lo = mid; else hi = mid;
         }
         const uint4 rc = rect[lo];
-        const uint32_t q = j - loff[lo];
-        uint32_t y = (uint32_t)((float)q * __builtin_amdgcn_rcpf((float)rc.y));
-        if (y * rc.y > q) y--;
-        if ((y + 1) * rc.y <= q) y++;
-        const uint32_t x = q - y * rc.y;
+        const uint2 mk = mask[lo];
+        const uint32_t k = j - loff[lo];
+        // position in the rect (row-major): the k-th kept tile
+        const uint32_t pos = (mk.x & mk.y) == ~0u ? k : kth_set_bit(mk.x, mk.y, k);
+        uint32_t y = (uint32_t)((float)pos * __builtin_amdgcn_rcpf((float)rc.y));
+        if (y * rc.y > pos) y--;
+        if ((y + 1) * rc.y <= pos) y++;
+        const uint32_t x = pos - y * rc.y;
         a.tile_keys[base + j] = (rc.z + y) * (uint32_t)a.gx + rc.x + x;
         a.ids[base + j] = rc.w;
     }
@@ -344,15 +376,15 @@ hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
         a.dmask = RADIX - 1;
         // the last pass also lays the tile rects out in depth order (one random
         // gather here instead of one in rank_sums and one in emit)
-        a.gsrc = p == 3 ? at<const uint2>(geom, L.rects) : nullptr;
-        a.gdst = p == 3 ? at<uint2>(geom, L.rects_ranked) : nullptr;
+        a.gsrc = p == 3 ? at<const uint4>(geom, L.rects) : nullptr;
+        a.gdst = p == 3 ? at<uint4>(geom, L.rects_ranked) : nullptr;
         hipError_t e = radix_pass<DSORT_ITEMS>(a, s);
         if (e != hipSuccess) return e;
     }
     // rank-order exclusive offsets of the instances, per EMIT block
     const int nb = emit_blocks(P);
     uint32_t *sums = at<uint32_t>(geom, L.emit_sums);
-    hipLaunchKernelGGL(rank_sums_kernel, dim3(nb), dim3(EMIT_BLOCK), 0, s, at<const uint2>(geom, L.rects_ranked), P,
+    hipLaunchKernelGGL(rank_sums_kernel, dim3(nb), dim3(EMIT_BLOCK), 0, s, at<const uint4>(geom, L.rects_ranked), P,
                        sums);
     hipLaunchKernelGGL(exclusive_scan_one_block_kernel, dim3(1), dim3(TOPSCAN_THREADS), 0, s, sums, nb);
     return hipGetLastError();
@@ -367,7 +399,7 @@ hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, vo
     a.P = P;
     a.gx = g.gx;
     a.order = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]);
-    a.rects = at<const uint2>(geom, L.rects_ranked);
+    a.rects = at<const uint4>(geom, L.rects_ranked);
     a.block_prefix = at<const uint32_t>(geom, L.emit_sums);
     // emit into the buffer pair that the tile passes will end in KEYS/POINT_LIST
     const bool odd = tile_sort_passes(g.tiles) & 1;

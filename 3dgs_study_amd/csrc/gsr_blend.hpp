@@ -30,12 +30,15 @@ static_assert(BLEND_WAVES == 4 || BLEND_WAVES == 1, "GSR_BLEND_WAVES must be 4 o
 // forward/backward reject a pixel when o*exp(-q/2) < 1/255, i.e. q > 2 ln(255 o);
 // qmax is that bound widened in preprocess, so a skipped Gaussian is one that
 // every pixel of the quadrant would have skipped.  A NaN bound keeps the entry.
-__device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb, float cc, float qmax, float x0,
-                                         float y0) {
+// box_hit is the same test over [x0, x0+ext] x [y0, y0+ext] (preprocess.hip uses
+// it per 16x16 tile, ext = 15, to drop the bounding-rect tiles a Gaussian cannot
+// reach).
+__device__ __forceinline__ bool box_hit(float mx, float my, float ca, float cb, float cc, float qmax, float x0,
+                                        float y0, float ext) {
     // ca, cb, cc, qmax come from the splat record, i.e. times -1/2: the form is
     // concave, so "min over the box of q <= qmax" reads "max of q' >= qmax'"
-    const float dx0 = x0 - mx, dx1 = x0 + 7.0f - mx;
-    const float dy0 = y0 - my, dy1 = y0 + 7.0f - my;
+    const float dx0 = x0 - mx, dx1 = x0 + ext - mx;
+    const float dy0 = y0 - my, dy1 = y0 + ext - my;
     if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return true;  // mean inside: q_min = 0
     // with the extremum outside the box, the box extremum lies on an edge (the
     // edge optimiser -cb dx / cc is scale-invariant).  Approximate reciprocals
@@ -52,6 +55,10 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
         q = fmaxf(q, ca * ex * ex + 2.0f * cb * ex * ey + cc * ey * ey);
     }
     return !(q < qmax);
+}
+__device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb, float cc, float qmax, float x0,
+                                         float y0) {
+    return box_hit(mx, my, ca, cb, cc, qmax, x0, y0, 7.0f);
 }
 
 // s_waitcnt vmcnt(4) expcnt(7) lgkmcnt(15): everything but the 4 youngest

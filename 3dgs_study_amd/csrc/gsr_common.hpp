@@ -74,8 +74,8 @@ enum CtrlWord {
 struct GeomLayout {
     size_t off[GSR_GEOM_NFIELDS];
     size_t block_sums;    // uint32 [pre_blocks(P)] instances per preprocess workgroup
-    size_t rects;         // uint2 [P] tile rect {x0 | x1 << 16, y0 | y1 << 16}; 0 when not visible
-    size_t rects_ranked;  // uint2 [P] the same in depth order (written by the last depth pass)
+    size_t rects;         // uint4 [P] tile rect {x0 | x1 << 16, y0 | y1 << 16} + 64-bit tile mask; 0 when not visible
+    size_t rects_ranked;  // uint4 [P] the same in depth order (written by the last depth pass)
     size_t dsort_keys_a;  // uint32 [P] depth-sort ping-pong (the order lands in GSR_GEOM_DEPTH_ORDER)
     size_t dsort_keys_b;
     size_t dsort_vals_b;
@@ -98,8 +98,8 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.off[GSR_GEOM_CTRL] = take(CTRL_WORDS * 4);
     L.off[GSR_GEOM_DEPTH_ORDER] = take((size_t)P * 4);
     L.block_sums = take((size_t)pre_blocks(P) * 4);
-    L.rects = take((size_t)P * 8);
-    L.rects_ranked = take((size_t)P * 8);
+    L.rects = take((size_t)P * 16);
+    L.rects_ranked = take((size_t)P * 16);
     L.dsort_keys_a = take((size_t)P * 4);
     L.dsort_keys_b = take((size_t)P * 4);
     L.dsort_vals_b = take((size_t)P * 4);
