@@ -72,7 +72,25 @@ struct RadixPass {
     uint32_t *hist;        // [RADIX][NB] block counts -> block offsets within each digit
     uint32_t *totals;      // [RADIX]
     int NB;
+    // depth sort only (nullptr / 0 otherwise): the geom control words and this
+    // pass's role when the key range allows three passes instead of four
+    const uint32_t *ctrl;
+    int role;              // RX_PLAIN, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH
+    uint32_t *vout_final;  // RX_DEPTH_THIRD in three-pass mode: the order lands here
 };
+enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
+
+// First depth pass: key = depth bits - base, clamped to 24 bits in three-pass
+// mode (only invisible Gaussians, +inf keys, reach the clamp).
+__device__ __forceinline__ uint32_t load_key(const RadixPass &a, uint32_t idx) {
+    const uint32_t k = a.kin[idx];
+    if (a.role != RX_DEPTH_FIRST) return k;
+    const uint32_t d = k - a.ctrl[CTRL_KEY_BASE];
+    return a.ctrl[CTRL_DSORT_PASSES] == 3 ? min(d, 0xffffffu) : d;
+}
+__device__ __forceinline__ bool pass_skipped(const RadixPass &a) {
+    return a.role == RX_DEPTH_FOURTH && a.ctrl[CTRL_DSORT_PASSES] == 3;
+}
 
 // ITEMS per thread: fewer for short inputs (more workgroups, shorter serial
 // rank chains), more for long ones (fewer blocks in the digit scan).
@@ -80,6 +98,7 @@ template <int ITEMS>
 __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) {
     constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
     __shared__ uint32_t h[RX_WAVES][RADIX];
+    if (pass_skipped(a)) return;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
@@ -89,7 +108,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
         const uint32_t idx = base + 64u * r;
-        kk[r] = idx < a.n ? a.kin[idx] : 0u;
+        kk[r] = idx < a.n ? load_key(a, idx) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < ITEMS; r++)
@@ -104,6 +123,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
 // One workgroup per digit: exclusive scan of that digit's block counts.
 __global__ void __launch_bounds__(256) radix_digit_scan_kernel(RadixPass a) {
     __shared__ uint32_t wsum[4];
+    if (pass_skipped(a)) return;
     uint32_t *row = a.hist + (size_t)blockIdx.x * a.NB;
     uint32_t carry = 0;
     for (int base = 0; base < a.NB; base += 256) {
@@ -125,6 +145,12 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     __shared__ uint32_t gstart[RADIX];   // global start of this block's run of each digit
     __shared__ uint32_t wsum[RX_WAVES];
     __shared__ uint32_t stage_k[TILE_N], stage_v[TILE_N];
+    if (pass_skipped(a)) return;
+    // three-pass depth sort: the third pass is the last one
+    const bool final3 = a.role == RX_DEPTH_THIRD && a.ctrl[CTRL_DSORT_PASSES] == 3;
+    uint32_t *const kout = final3 ? nullptr : a.kout;
+    uint32_t *const vout = final3 ? a.vout_final : a.vout;
+    const bool gather = a.gdst && (a.role != RX_DEPTH_THIRD || final3);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t b0 = blockIdx.x * (uint32_t)TILE_N;
     const uint32_t base = b0 + w * (uint32_t)WAVE_N + lane;
@@ -133,7 +159,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     for (int r = 0; r < ITEMS; r++) {
         const uint32_t idx = base + 64u * r;
         const bool ok = idx < a.n;
-        kk[r] = ok ? a.kin[idx] : 0u;
+        kk[r] = ok ? load_key(a, idx) : 0u;
         vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
     }
     {  // where this block's items of digit d go: all smaller digits + earlier blocks
@@ -196,9 +222,9 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         const uint32_t d = (k >> a.shift) & a.dmask;
         const uint32_t pos = gstart[d] + (i - lstart[d]);
         const uint32_t v = stage_v[i];
-        if (a.kout) a.kout[pos] = k;
-        a.vout[pos] = v;
-        if (a.gdst) a.gdst[pos] = a.gsrc[v];
+        if (kout) kout[pos] = k;
+        vout[pos] = v;
+        if (gather) a.gdst[pos] = a.gsrc[v];
     }
 }
 
@@ -361,23 +387,31 @@ hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
     const uint32_t *depth_bits = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTHS]);
     uint32_t *ka = at<uint32_t>(geom, L.dsort_keys_a), *kb = at<uint32_t>(geom, L.dsort_keys_b);
     uint32_t *va = at<uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), *vb = at<uint32_t>(geom, L.dsort_vals_b);
-    // (depth, index) -> b -> a -> b -> a(order); the last pass drops the keys
+    uint32_t *vc = at<uint32_t>(geom, L.dsort_vals_c);
+    // (depth - base, index) -> b -> a -> b -> a(order); values - -> b -> c -> b -> order.
+    // With every visible key within 2^24 of the base (publish_total_kernel) the
+    // third pass writes the order itself and the fourth returns at once: the
+    // choice is made on the device, so the launches need not wait for the host.
     const uint32_t *kin[4] = {depth_bits, kb, ka, kb};
-    const uint32_t *vin[4] = {nullptr, vb, va, vb};
+    const uint32_t *vin[4] = {nullptr, vb, vc, vb};
     uint32_t *kout[4] = {kb, ka, kb, nullptr};
-    uint32_t *vout[4] = {vb, va, vb, va};
+    uint32_t *vout[4] = {vb, vc, vb, va};
+    const int role[4] = {RX_DEPTH_FIRST, RX_PLAIN, RX_DEPTH_THIRD, RX_DEPTH_FOURTH};
+    a.ctrl = at<const uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+    a.vout_final = va;
     for (int p = 0; p < 4; p++) {
         a.kin = kin[p];
         a.vin = vin[p];
         a.kout = kout[p];
         a.vout = vout[p];
+        a.role = role[p];
         a.shift = 8 * p;
         a.nbits = RADIX_BITS;
         a.dmask = RADIX - 1;
         // the last pass also lays the tile rects out in depth order (one random
         // gather here instead of one in rank_sums and one in emit)
-        a.gsrc = p == 3 ? at<const uint4>(geom, L.rects) : nullptr;
-        a.gdst = p == 3 ? at<uint4>(geom, L.rects_ranked) : nullptr;
+        a.gsrc = p >= 2 ? at<const uint4>(geom, L.rects) : nullptr;
+        a.gdst = p >= 2 ? at<uint4>(geom, L.rects_ranked) : nullptr;
         hipError_t e = radix_pass<DSORT_ITEMS>(a, s);
         if (e != hipSuccess) return e;
     }
@@ -424,6 +458,9 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
     a.NB = radix_blocks(I, TSORT_ITEMS);
     a.gsrc = nullptr;
     a.gdst = nullptr;
+    a.ctrl = nullptr;
+    a.role = RX_PLAIN;
+    a.vout_final = nullptr;
     a.hist = at<uint32_t>(binning, B.hist);
     a.totals = at<uint32_t>(binning, B.totals);
     for (int p = 0; p < npass; p++) {

@@ -68,17 +68,20 @@ enum CtrlWord {
     CTRL_NUM_RENDERED_LO = 0,
     CTRL_NUM_RENDERED_HI = 1,
     CTRL_PREFILTER_ERR = 2,
+    CTRL_KEY_BASE = 3,      // smallest depth key (bits) of a visible Gaussian
+    CTRL_DSORT_PASSES = 4,  // 3 when every visible key lies within 2^24 of the base, else 4
     CTRL_WORDS = 16
 };
 
 struct GeomLayout {
     size_t off[GSR_GEOM_NFIELDS];
-    size_t block_sums;    // uint32 [pre_blocks(P)] instances per preprocess workgroup
+    size_t block_sums;    // uint4 [pre_blocks(P)] per preprocess workgroup: instances | error << 31, key min, max
     size_t rects;         // uint4 [P] tile rect {x0 | x1 << 16, y0 | y1 << 16} + 64-bit tile mask; 0 when not visible
     size_t rects_ranked;  // uint4 [P] the same in depth order (written by the last depth pass)
     size_t dsort_keys_a;  // uint32 [P] depth-sort ping-pong (the order lands in GSR_GEOM_DEPTH_ORDER)
     size_t dsort_keys_b;
     size_t dsort_vals_b;
+    size_t dsort_vals_c;
     size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, DSORT_ITEMS)]
     size_t dsort_totals;  // uint32 [RADIX]
     size_t emit_sums;     // uint32 [emit_blocks(P)] rank-order instance offsets per emit block
@@ -97,12 +100,13 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.off[GSR_GEOM_RANGES] = take((size_t)g.tiles * 8);
     L.off[GSR_GEOM_CTRL] = take(CTRL_WORDS * 4);
     L.off[GSR_GEOM_DEPTH_ORDER] = take((size_t)P * 4);
-    L.block_sums = take((size_t)pre_blocks(P) * 4);
+    L.block_sums = take((size_t)pre_blocks(P) * 16);
     L.rects = take((size_t)P * 16);
     L.rects_ranked = take((size_t)P * 16);
     L.dsort_keys_a = take((size_t)P * 4);
     L.dsort_keys_b = take((size_t)P * 4);
     L.dsort_vals_b = take((size_t)P * 4);
+    L.dsort_vals_c = take((size_t)P * 4);
     L.dsort_hist = take((size_t)RADIX * radix_blocks(P, DSORT_ITEMS) * 4);
     L.dsort_totals = take((size_t)RADIX * 4);
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);

@@ -30,7 +30,7 @@ struct PreArgs {
     uint4 *rects;  // tile rect {x0 | x1 << 16, y0 | y1 << 16} + 64-bit tile mask per Gaussian (binning.hip)
     uint2 *ranges;           // [T] zeroed here (empty tiles keep (0, 0); binning.hip fills the rest)
     int tiles;
-    uint32_t *block_sums;    // [pre_blocks(P)] instances per workgroup | prefiltered error << 31
+    uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, key min, key max, 0}
     int32_t *radii;
 };
 
@@ -73,8 +73,8 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         rows_to_lds<PRE_THREADS>(in.sh, g0, min(PRE_THREADS, in.P - g0), RW, sh_lds);
         __syncthreads();
     }
-    uint32_t touched = 0;
-    bool perr = false;
+    uint32_t touched = 0, key = 0;
+    bool perr = false, key_vis = false;
     for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
     if (idx < in.P) {
         int radius_out = 0;
@@ -198,47 +198,84 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 rect_out = make_uint4(rc.x0 | (rc.x1 << 16), rc.y0 | (rc.y1 << 16), (uint32_t)m, (uint32_t)(m >> 32));
             }
         }
+        // depth keys of invisible Gaussians: +inf bits, sorted behind every visible one
+        if (radius_out) {
+            key = __float_as_uint(p_view.z);
+            key_vis = true;
+        } else {
+            a.depths[idx] = __uint_as_float(0x7f800000u);
+        }
         a.radii[idx] = radius_out;
         a.tiles_touched[idx] = touched;
         a.rects[idx] = rect_out;
     }
     // num_rendered is only a total (emit works in depth order, binning.hip): each
-    // workgroup stores its sum, bit 31 flags a prefiltered violation
+    // workgroup stores its sum (bit 31 flags a prefiltered violation) and the
+    // range of its visible depth keys (the depth sort drops constant top bits)
     const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
     const int berr = __syncthreads_or(perr);
-    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = tot | (berr ? 0x80000000u : 0u);
+    uint32_t kmin = key_vis ? key : 0xffffffffu, kmax = key_vis ? key : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+    }
+    __shared__ uint32_t wmin[PRE_THREADS / 64], wmax[PRE_THREADS / 64];
+    if ((threadIdx.x & 63) == 0) {
+        wmin[threadIdx.x >> 6] = kmin;
+        wmax[threadIdx.x >> 6] = kmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < PRE_THREADS / 64; k++) {
+            kmin = min(kmin, wmin[k]);
+            kmax = max(kmax, wmax[k]);
+        }
+        a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), kmin, kmax, 0u);
+    }
 }
 
 // One workgroup totals the block sums and publishes num_rendered and the error
 // flag into the geom control words and, with system-scope stores, straight into
 // the caller's pinned host words (no copy; the host waits for this kernel's event).
 constexpr int TOTAL_THREADS = 1024;
-__global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint32_t *sums, int n, uint32_t *ctrl,
+__global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint4 *sums, int n, uint32_t *ctrl,
                                                                       uint32_t *host_ctrl) {
     __shared__ unsigned long long part[TOTAL_THREADS / 64];
-    __shared__ uint32_t perr[TOTAL_THREADS / 64];
+    __shared__ uint32_t perr[TOTAL_THREADS / 64], pmin[TOTAL_THREADS / 64], pmax[TOTAL_THREADS / 64];
     unsigned long long t = 0;
-    uint32_t e = 0;
+    uint32_t e = 0, kmin = 0xffffffffu, kmax = 0u;
     for (int i = threadIdx.x; i < n; i += TOTAL_THREADS) {
-        const uint32_t v = sums[i];
-        t += v & 0x7fffffffu;
-        e |= v >> 31;
+        const uint4 v = sums[i];
+        t += v.x & 0x7fffffffu;
+        e |= v.x >> 31;
+        kmin = min(kmin, v.y);
+        kmax = max(kmax, v.z);
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
         t += __shfl_xor(t, o);
         e |= __shfl_xor(e, o);
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
     }
     if ((threadIdx.x & 63) == 0) {
         part[threadIdx.x >> 6] = t;
         perr[threadIdx.x >> 6] = e;
+        pmin[threadIdx.x >> 6] = kmin;
+        pmax[threadIdx.x >> 6] = kmax;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int k = 1; k < TOTAL_THREADS / 64; k++) {
             t += part[k];
             e |= perr[k];
+            kmin = min(kmin, pmin[k]);
+            kmax = max(kmax, pmax[k]);
         }
+        const bool any = kmin <= kmax;
+        ctrl[CTRL_KEY_BASE] = any ? kmin : 0u;
+        ctrl[CTRL_DSORT_PASSES] = any && kmax - kmin > 0xffffffu ? 4u : 3u;
         const uint32_t w[3] = {(uint32_t)t, (uint32_t)(t >> 32), e};
         for (int k = 0; k < 3; k++) {
             ctrl[k] = w[k];
@@ -275,12 +312,12 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
     a.rects = at<uint4>(geom, L.rects);
     a.ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
     a.tiles = g.tiles;
-    a.block_sums = at<uint32_t>(geom, L.block_sums);
+    a.block_sums = at<uint4>(geom, L.block_sums);
     a.radii = radii;
     const int nb = pre_blocks(in.P);
     const size_t lds = (in.sh && !in.colors_precomp) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     hipLaunchKernelGGL(preprocess_fwd_kernel, dim3(nb), dim3(PRE_THREADS), lds, s, a);
-    hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint32_t *)a.block_sums, nb,
+    hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint4 *)a.block_sums, nb,
                        at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl);
     return hipGetLastError();
 }

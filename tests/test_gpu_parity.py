@@ -316,3 +316,16 @@ def test_config_c_full_size_parity(dev, oracle):
     for t in np.flatnonzero(rg[:, 1] - rg[:, 0] > 1)[:200]:
         s, e = rg[t]
         assert np.all(np.diff(d[s:e]) >= 0)
+
+
+@pytest.mark.parametrize("radius,passes", [(2.0, 3), (5.5, 4)])
+def test_depth_sort_pass_count(dev, oracle, radius, passes):
+    """Visible depth keys within 2^24 of the smallest: the depth sort's fourth radix
+    pass is skipped on the device; a wide depth range (0.5..11.5) takes all four."""
+    cam, g = case(20_000, 160, 120, 1, seed=7, radius=radius)
+    dL = random_dL(120, 160)
+    h = run_hip(cam, g, dev, dL=dL)
+    assert int(h["ctrl"][4]) == passes
+    r = run_oracle(oracle, cam, g)
+    check_forward(h, r)
+    check_backward(h, oracle.backward(r, dL))
