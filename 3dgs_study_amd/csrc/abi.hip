@@ -24,6 +24,8 @@ thread_local std::string g_err;
 // (the call waits for that launch's event before returning, so calls from one
 // thread never share them in flight).
 thread_local uint32_t *g_pinned = nullptr;
+// pinned words: num_rendered lo / hi, prefiltered error, depth-sort pass count
+constexpr int HOST_DSORT_PASSES = 3;
 thread_local hipEvent_t g_ctrl_ready = nullptr;
 
 int fail(int code, const char *fmt, ...) {
@@ -56,9 +58,12 @@ StageTimer g_timer;  // the ABI is driven from one host thread per process
 const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess", "scan",       "depth_sort", "duplicate",
                                             "tile_sort",  "render_fwd", "render_bwd", "preprocess_bwd"};
 
+// st | TIMED_MORE: more work of a stage already counted once in this step (its
+// time is added, its launch count is not)
+constexpr int TIMED_MORE = 0x100;
 template <typename F>
 hipError_t timed(int st, hipStream_t s, F &&launch) {
-    if (!(g_timer.mask & (1 << st))) return launch();
+    if (!(g_timer.mask & (1 << (st & 0xff)))) return launch();
     if (g_timer.used == g_timer.pool.size()) {
         hipEvent_t a, b;
         hipError_t e = hipEventCreate(&a);
@@ -170,7 +175,10 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     const int64_t I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
     if (I > 0xFFFFFFFFll) return fail(GSR_ERR_CAPACITY, "num_rendered %lld exceeds 32-bit list indexing", (long long)I);
     *num_rendered = I;
-    return GSR_OK;
+    // the depth sort's fourth pass (wide depth ranges only) and the emission offsets
+    const bool fourth = g_pinned[HOST_DSORT_PASSES] == 4;
+    return step(timed(GSR_STAGE_DUPLICATE | TIMED_MORE, s, [&] { return launch_depth_sort_tail(in->P, in->W, in->H, geom, fourth, s); }),
+                "depth sort", dbg, s);
 }
 
 int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
@@ -288,8 +296,8 @@ int gsr_timing_read(double *total_ms, int64_t *launches, int cap) {
         if (int rc = check_hip(hipEventSynchronize(ev.second), "timing event")) return -rc;
         float ms = 0.f;
         if (int rc = check_hip(hipEventElapsedTime(&ms, ev.first, ev.second), "timing event")) return -rc;
-        g_timer.total_ms[g_timer.stage[i]] += ms;
-        g_timer.launches[g_timer.stage[i]] += 1;
+        g_timer.total_ms[g_timer.stage[i] & 0xff] += ms;
+        g_timer.launches[g_timer.stage[i] & 0xff] += (g_timer.stage[i] & TIMED_MORE) ? 0 : 1;
     }
     g_timer.used = 0;
     int n = 0;

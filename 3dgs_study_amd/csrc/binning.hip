@@ -377,7 +377,13 @@ __global__ void __launch_bounds__(RANGE_THREADS) identify_ranges_kernel(const ui
 }
 
 // ------------------------------------------------------------ launchers
-hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
+// The depth sort is launched in two parts around the host's one sync.  Passes 1-3
+// go first (they overlap the host wait); the third pass writes the final order
+// itself when every visible key lies within 2^24 of the base (decided on the
+// device from publish_total_kernel's control words).  Once the host has read the
+// pass count, launch_depth_sort_tail adds the fourth pass only when it is needed,
+// then the rank-order block offsets of the emission.
+static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     const GeomLayout L = geom_layout(P, W, H);
     RadixPass a;
     a.n = (uint32_t)P;
@@ -388,10 +394,7 @@ hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
     uint32_t *ka = at<uint32_t>(geom, L.dsort_keys_a), *kb = at<uint32_t>(geom, L.dsort_keys_b);
     uint32_t *va = at<uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), *vb = at<uint32_t>(geom, L.dsort_vals_b);
     uint32_t *vc = at<uint32_t>(geom, L.dsort_vals_c);
-    // (depth - base, index) -> b -> a -> b -> a(order); values - -> b -> c -> b -> order.
-    // With every visible key within 2^24 of the base (publish_total_kernel) the
-    // third pass writes the order itself and the fourth returns at once: the
-    // choice is made on the device, so the launches need not wait for the host.
+    // (depth - base, index) -> b -> a -> b -> a(order); values - -> b -> c -> b -> order
     const uint32_t *kin[4] = {depth_bits, kb, ka, kb};
     const uint32_t *vin[4] = {nullptr, vb, vc, vb};
     uint32_t *kout[4] = {kb, ka, kb, nullptr};
@@ -399,29 +402,48 @@ hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
     const int role[4] = {RX_DEPTH_FIRST, RX_PLAIN, RX_DEPTH_THIRD, RX_DEPTH_FOURTH};
     a.ctrl = at<const uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
     a.vout_final = va;
-    for (int p = 0; p < 4; p++) {
-        a.kin = kin[p];
-        a.vin = vin[p];
-        a.kout = kout[p];
-        a.vout = vout[p];
-        a.role = role[p];
-        a.shift = 8 * p;
-        a.nbits = RADIX_BITS;
-        a.dmask = RADIX - 1;
-        // the last pass also lays the tile rects out in depth order (one random
-        // gather here instead of one in rank_sums and one in emit)
-        a.gsrc = p >= 2 ? at<const uint4>(geom, L.rects) : nullptr;
-        a.gdst = p >= 2 ? at<uint4>(geom, L.rects_ranked) : nullptr;
-        hipError_t e = radix_pass<DSORT_ITEMS>(a, s);
-        if (e != hipSuccess) return e;
-    }
+    a.kin = kin[p];
+    a.vin = vin[p];
+    a.kout = kout[p];
+    a.vout = vout[p];
+    a.role = role[p];
+    a.shift = 8 * p;
+    a.nbits = RADIX_BITS;
+    a.dmask = RADIX - 1;
+    // the last pass also lays the tile rects out in depth order (one random
+    // gather here instead of one in rank_sums and one in emit)
+    a.gsrc = p >= 2 ? at<const uint4>(geom, L.rects) : nullptr;
+    a.gdst = p >= 2 ? at<uint4>(geom, L.rects_ranked) : nullptr;
+    return a;
+}
+
+static hipError_t launch_rank_offsets(int P, int W, int H, void *geom, hipStream_t s) {
     // rank-order exclusive offsets of the instances, per EMIT block
+    const GeomLayout L = geom_layout(P, W, H);
     const int nb = emit_blocks(P);
     uint32_t *sums = at<uint32_t>(geom, L.emit_sums);
     hipLaunchKernelGGL(rank_sums_kernel, dim3(nb), dim3(EMIT_BLOCK), 0, s, at<const uint4>(geom, L.rects_ranked), P,
                        sums);
     hipLaunchKernelGGL(exclusive_scan_one_block_kernel, dim3(1), dim3(TOPSCAN_THREADS), 0, s, sums, nb);
     return hipGetLastError();
+}
+
+// Passes 1-3 and the emission offsets are queued before the host waits (they
+// keep the device busy while the host wakes up and launches the rest); in the
+// rare four-pass case the tail redoes the offsets after the fourth pass.
+hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
+    for (int p = 0; p < 3; p++) {
+        hipError_t e = radix_pass<DSORT_ITEMS>(depth_pass(P, W, H, geom, p), s);
+        if (e != hipSuccess) return e;
+    }
+    return launch_rank_offsets(P, W, H, geom, s);
+}
+
+hipError_t launch_depth_sort_tail(int P, int W, int H, void *geom, bool fourth_pass, hipStream_t s) {
+    if (!fourth_pass) return hipSuccess;
+    hipError_t e = radix_pass<DSORT_ITEMS>(depth_pass(P, W, H, geom, 3), s);
+    if (e != hipSuccess) return e;
+    return launch_rank_offsets(P, W, H, geom, s);
 }
 
 hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,

@@ -80,6 +80,23 @@ __device__ __forceinline__ void stage_chunk(ChunkStage &st, int lane, const floa
     st.rec[lane][2] = C;
 }
 
+// Compacted chunk image: only the entries that survived the cull, in chunk
+// order (slot = number of survivors in lower lanes), each record's last word
+// holding the entry's lane (its list position minus the chunk start).  The
+// Gaussian loops then walk slots 0..n-1 with an affine index — no find-first-set
+// chains on the scalar unit between one pair's LDS reads and the next's.
+__device__ __forceinline__ int stage_survivors(ChunkStage &st, int lane, bool rel, uint64_t mask, const float4 &A,
+                                               const float4 &B, const float4 &C) {
+    if (rel) {
+        const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        st.rec[slot][0] = A;
+        st.rec[slot][1] = B;
+        st.rec[slot][2] = make_float4(C.x, C.y, C.z, __int_as_float(lane));
+    }
+    return __builtin_popcountll(mask);
+}
+
 __device__ __forceinline__ float bcast(float v, int k) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
 }

@@ -276,9 +276,9 @@ __global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint
         const bool any = kmin <= kmax;
         ctrl[CTRL_KEY_BASE] = any ? kmin : 0u;
         ctrl[CTRL_DSORT_PASSES] = any && kmax - kmin > 0xffffffu ? 4u : 3u;
-        const uint32_t w[3] = {(uint32_t)t, (uint32_t)(t >> 32), e};
-        for (int k = 0; k < 3; k++) {
-            ctrl[k] = w[k];
+        const uint32_t w[4] = {(uint32_t)t, (uint32_t)(t >> 32), e, ctrl[CTRL_DSORT_PASSES]};
+        for (int k = 0; k < 4; k++) {
+            if (k < 3) ctrl[k] = w[k];
             __hip_atomic_store(&host_ctrl[k], w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __threadfence_system();

@@ -131,7 +131,11 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         const float ux = p0.z * q.dx + p0.w * q.dy;  // conic' * d with conic' = -conic/2 (splat record)
         const float uy = p0.w * q.dx + p1.x * q.dy;
         const float power = q.dx * ux + q.dy * uy;  // upstream's power; == render_fwd.hip, bit for bit
+#ifdef GSR_EXP_NO_EXP  // timing experiment only
+        q.G = 1.0f + power * (1.0f + 0.5f * power);
+#else
         q.G = __expf(power);
+#endif
         q.alpha = fminf(0.99f, p1.y * q.G);
         q.valid = live && k < lim && !(power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
         return q;
@@ -175,28 +179,81 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         return g;
     };
 
+    // Reduce-scatter of a pair's 18 sums and their two atomic wave instructions.
+    auto reduce_emit = [&](const G9 &ga, const G9 &gb, uint32_t gida, uint32_t gidb, bool two) {
+        // reduce-scatter of the 18 sums inside each 32-lane half with ds_swizzle
+        // (xor 16, 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per output
+        // register) and one final v_permlane32 self-swap adding the two halves
+#ifdef GSR_EXP_NO_REDUCE  // timing experiment only
+        const float v = ga.g0 + ga.g1 + ga.g2 + ga.g3 + ga.g4 + ga.g5 + ga.g6 + ga.g7 + ga.g8 + gb.g0 + gb.g1 +
+                        gb.g2 + gb.g3 + gb.g4 + gb.g5 + gb.g6 + gb.g7 + gb.g8;
+#else
+        const float s0 = swz_stage<16>(ga.g0, ga.g1, lane);
+        const float s1 = swz_stage<16>(ga.g2, ga.g3, lane);
+        const float s2 = swz_stage<16>(ga.g4, ga.g5, lane);
+        const float s3 = swz_stage<16>(ga.g6, ga.g7, lane);
+        const float s4 = swz_stage<16>(ga.g8, gb.g0, lane);
+        const float s5 = swz_stage<16>(gb.g1, gb.g2, lane);
+        const float s6 = swz_stage<16>(gb.g3, gb.g4, lane);
+        const float s7 = swz_stage<16>(gb.g5, gb.g6, lane);
+        const float s8 = swz_stage<16>(gb.g7, gb.g8, lane);
+        const float t0 = swz_stage<8>(s0, s1, lane);
+        const float t1 = swz_stage<8>(s2, s3, lane);
+        const float t2 = swz_stage<8>(s4, s5, lane);
+        const float t3 = swz_stage<8>(s6, s7, lane);
+        const float t4 = swz_stage<8>(s8, 0.f, lane);
+        const float u0 = swz_stage<4>(t0, t1, lane);
+        const float u1 = swz_stage<4>(t2, t3, lane);
+        const float u2 = swz_stage<4>(t4, 0.f, lane);
+#ifdef GSR_BWD_DPP_TAIL  // experiment: the last two (short) stages on DPP quad permutes
+        const float w0 = ((lane & 2) ? u1 : u0) + dpp_f32<DPP_QUAD_XOR2>((lane & 2) ? u0 : u1);
+        const float w1 = ((lane & 2) ? 0.f : u2) + dpp_f32<DPP_QUAD_XOR2>((lane & 2) ? u2 : 0.f);
+        const float o0 = ((lane & 1) ? w1 : w0) + dpp_f32<DPP_QUAD_XOR1>((lane & 1) ? w0 : w1);
+#else
+        const float w0 = swz_stage<2>(u0, u1, lane);
+        const float w1 = swz_stage<2>(u2, 0.f, lane);
+        const float o0 = swz_stage<1>(w0, w1, lane);
+#endif
+#ifdef GSR_BWD_BPERM_FINAL  // experiment: the cross-half add through ds_bpermute
+        const float v = o0 + __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2,
+                                                                                    __builtin_bit_cast(int, o0)));
+#else
+        const float v = swap32_sum(o0, o0);  // both halves: the full sum
+#endif
+#endif
+        // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
+        // compiler's atomic optimizer (a wave-scan loop) out
+#ifdef GSR_EXP_NO_ATOMIC  // timing experiment only
+        if (v == 1234.5f) a.accum[lane] = v;
+#else
+        if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, v);
+        if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
+#endif
+    };
+#ifdef GSR_BWD_PIPE
+    G9 pga = {}, pgb = {};  // the pending pair (zeros into Gaussian 0's row at first: harmless)
+    uint32_t pgida = 0, pgidb = 0;
+    bool ptwo = false;
+#endif
+
     // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l),
     // two Gaussians per iteration: independent LDS reads and exps (ILP), one
     // fused reduce-scatter of their 18 sums (no half-empty permlane32 stage).
     auto replay_chunk = [&](int lo, float4 A, float4 B, float4 C) {
-        stage_chunk(st, lane, A, B, C);
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
-        uint64_t mask = __ballot(rel);
+        const uint64_t mask = __ballot(rel);
+        const int ns = stage_survivors(st, lane, rel, mask, A, B, C);
         BWD_STAT(1, 1);
-        BWD_STAT(4, __builtin_popcountll(mask));
-        const int lim = last_contrib - lo;  // entry lo + k replays for this pixel iff k < lim
-        while (mask) {
-            const int ka = 63 - __builtin_clzll(mask);
-            mask ^= 1ull << ka;
-            const bool two = mask != 0;  // wave-uniform
-            const int kb = two ? 63 - __builtin_clzll(mask) : ka;
-            if (two) mask ^= 1ull << kb;
-            const float4 a0 = st.rec[ka][0], a1 = st.rec[ka][1];
-            const float4 b0 = st.rec[kb][0], b1 = st.rec[kb][1];
-            const float2 a2 = *reinterpret_cast<const float2 *>(&st.rec[ka][2]);
-            const float2 b2 = *reinterpret_cast<const float2 *>(&st.rec[kb][2]);
-            const Pre qa = prepare(a0, a1, ka, lim, true);  // entry lo + k = upstream `contributor`
-            const Pre qb = prepare(b0, b1, kb, lim, two);
+        BWD_STAT(4, ns);
+        const int lim = last_contrib - lo;  // entry lo + l replays for this pixel iff l < lim
+        for (int k = ns - 1; k >= 0; k -= 2) {
+            const bool two = k >= 1;  // wave-uniform
+            const int ka = k, kb = two ? k - 1 : k;
+            const float4 a0 = st.rec[ka][0], a1 = st.rec[ka][1], a2 = st.rec[ka][2];
+            const float4 b0 = st.rec[kb][0], b1 = st.rec[kb][1], b2 = st.rec[kb][2];
+            const int la = __float_as_int(a2.w), lb = __float_as_int(b2.w);
+            const Pre qa = prepare(a0, a1, la, lim, true);  // entry lo + l = upstream `contributor`
+            const Pre qb = prepare(b0, b1, lb, lim, two);
             BWD_STAT(2, 1);
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
@@ -209,36 +266,20 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
 #endif
             const G9 ga = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: ka > kb
             const G9 gb = replay(qb, b1.y, b1.z, b1.w, b2.x);
-            // reduce-scatter of the 18 sums inside each 32-lane half with ds_swizzle
-            // (xor 16, 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per output
-            // register) and one final v_permlane32 self-swap adding the two halves
-            const float s0 = swz_stage<16>(ga.g0, ga.g1, lane);
-            const float s1 = swz_stage<16>(ga.g2, ga.g3, lane);
-            const float s2 = swz_stage<16>(ga.g4, ga.g5, lane);
-            const float s3 = swz_stage<16>(ga.g6, ga.g7, lane);
-            const float s4 = swz_stage<16>(ga.g8, gb.g0, lane);
-            const float s5 = swz_stage<16>(gb.g1, gb.g2, lane);
-            const float s6 = swz_stage<16>(gb.g3, gb.g4, lane);
-            const float s7 = swz_stage<16>(gb.g5, gb.g6, lane);
-            const float s8 = swz_stage<16>(gb.g7, gb.g8, lane);
-            const float t0 = swz_stage<8>(s0, s1, lane);
-            const float t1 = swz_stage<8>(s2, s3, lane);
-            const float t2 = swz_stage<8>(s4, s5, lane);
-            const float t3 = swz_stage<8>(s6, s7, lane);
-            const float t4 = swz_stage<8>(s8, 0.f, lane);
-            const float u0 = swz_stage<4>(t0, t1, lane);
-            const float u1 = swz_stage<4>(t2, t3, lane);
-            const float u2 = swz_stage<4>(t4, 0.f, lane);
-            const float w0 = swz_stage<2>(u0, u1, lane);
-            const float w1 = swz_stage<2>(u2, 0.f, lane);
-            const float o0 = swz_stage<1>(w0, w1, lane);
-            const float v = swap32_sum(o0, o0);  // both halves: the full sum
-            // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
-            // compiler's atomic optimizer (a wave-scan loop) out
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.y));
             const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.y));
-            if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, v);
-            if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
+#ifdef GSR_BWD_PIPE
+            // software pipeline: this pair's sums are reduced in the next iteration,
+            // so the swizzle chain's LDS latency overlaps the next pair's replay
+            reduce_emit(pga, pgb, pgida, pgidb, ptwo);
+            pga = ga;
+            pgb = gb;
+            pgida = gida;
+            pgidb = gidb;
+            ptwo = two;
+#else
+            reduce_emit(ga, gb, gida, gidb, two);
+#endif
         }
     };
     // Double-buffered backwards stream, unrolled by two so the buffers swap roles
@@ -266,6 +307,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         replay_chunk(lo, A1, B1, C1);
         if ((lo -= 64) + 64 <= 0) break;
     }
+#ifdef GSR_BWD_PIPE
+    reduce_emit(pga, pgb, pgida, pgidb, ptwo);
+#endif
 }
 
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,

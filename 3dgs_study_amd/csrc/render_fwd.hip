@@ -53,21 +53,18 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
         // Blend one 64-entry chunk starting at list position pos (lane l <-> entry
         // pos + l); returns true once every pixel of the quadrant is saturated.
         auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
-            stage_chunk(st, lane, A, B, C);
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
-            uint64_t mask = __ballot(rel);
+            const int ns = stage_survivors(st, lane, rel, __ballot(rel), A, B, C);
             // Two Gaussians per iteration: their LDS reads, powers and exps are
             // independent, so each wave has twice the instruction-level parallelism
             // to cover LDS and transcendental latency; only the T recurrence is serial.
-            while (mask) {
-                const int ka = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                const bool two = mask != 0;  // wave-uniform
-                const int kb = two ? __builtin_ctzll(mask) : ka;
-                mask &= mask - 1;
+            for (int k = 0; k < ns; k += 2) {
+                const bool two = k + 1 < ns;  // wave-uniform
+                const int ka = k, kb = two ? k + 1 : k;
                 const float4 a0 = st.rec[ka][0], a1 = st.rec[ka][1];
                 const float4 b0 = st.rec[kb][0], b1 = st.rec[kb][1];
                 const float acb = st.rec[ka][2].x, bcb = st.rec[kb][2].x;
+                const int la = __float_as_int(st.rec[ka][2].w), lb = __float_as_int(st.rec[kb][2].w);
                 float pa, pb, alpha_a, alpha_b;
                 {
                     const float dx = a0.x - fx, dy = a0.y - fy;
@@ -105,8 +102,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
                     T = sat ? T : test_T;
                     last = av > 0.0f ? (uint32_t)(pos + k + 1) : last;
                 };
-                step(true, pa, alpha_a, a1.z, a1.w, acb, ka);
-                step(two, pb, alpha_b, b1.z, b1.w, bcb, kb);
+                step(true, pa, alpha_a, a1.z, a1.w, acb, la);
+                step(two, pb, alpha_b, b1.z, b1.w, bcb, lb);
                 if (!__any(live > 0.0f)) return true;
             }
             return false;
