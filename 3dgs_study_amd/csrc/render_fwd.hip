@@ -30,6 +30,11 @@ struct RenderFwdArgs {
     uint32_t *n_contrib;
 };
 
+#ifndef GSR_FWD_GROUP
+#define GSR_FWD_GROUP 2
+#endif
+constexpr int FWD_GROUP = GSR_FWD_GROUP;  // Gaussians per blend iteration
+
 __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs a) {
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
@@ -55,30 +60,26 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
         auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
             const int ns = stage_survivors(st, lane, rel, __ballot(rel), A, B, C);
-            // Two Gaussians per iteration: their LDS reads, powers and exps are
-            // independent, so each wave has twice the instruction-level parallelism
+            // FWD_GROUP Gaussians per iteration: their LDS reads, powers and exps are
+            // independent, so each wave has that much instruction-level parallelism
             // to cover LDS and transcendental latency; only the T recurrence is serial.
-            for (int k = 0; k < ns; k += 2) {
-                const bool two = k + 1 < ns;  // wave-uniform
-                const int ka = k, kb = two ? k + 1 : k;
-                const float4 a0 = st.rec[ka][0], a1 = st.rec[ka][1];
-                const float4 b0 = st.rec[kb][0], b1 = st.rec[kb][1];
-                const float acb = st.rec[ka][2].x, bcb = st.rec[kb][2].x;
-                const int la = __float_as_int(st.rec[ka][2].w), lb = __float_as_int(st.rec[kb][2].w);
-                float pa, pb, alpha_a, alpha_b;
-                {
-                    const float dx = a0.x - fx, dy = a0.y - fy;
-                    // conic' = -conic/2 (splat record): pa is upstream's power; render_bwd.hip
+            for (int k = 0; k < ns; k += FWD_GROUP) {
+                float pw[FWD_GROUP], al[FWD_GROUP], cr[FWD_GROUP], cg[FWD_GROUP], cb[FWD_GROUP];
+                int li[FWD_GROUP];
+#pragma unroll
+                for (int g = 0; g < FWD_GROUP; g++) {
+                    const int kg = min(k + g, ns - 1);
+                    const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1];
+                    cb[g] = st.rec[kg][2].x;
+                    li[g] = __float_as_int(st.rec[kg][2].w);
+                    const float dx = r0.x - fx, dy = r0.y - fy;
+                    // conic' = -conic/2 (splat record): pw is upstream's power; render_bwd.hip
                     // recomputes it bit for bit
-                    const float ux = a0.z * dx + a0.w * dy, uy = a0.w * dx + a1.x * dy;
-                    pa = dx * ux + dy * uy;
-                    alpha_a = fminf(0.99f, a1.y * __expf(pa));
-                }
-                {
-                    const float dx = b0.x - fx, dy = b0.y - fy;
-                    const float ux = b0.z * dx + b0.w * dy, uy = b0.w * dx + b1.x * dy;
-                    pb = dx * ux + dy * uy;
-                    alpha_b = fminf(0.99f, b1.y * __expf(pb));
+                    const float ux = r0.z * dx + r0.w * dy, uy = r0.w * dx + r1.x * dy;
+                    pw[g] = dx * ux + dy * uy;
+                    al[g] = fminf(0.99f, r1.y * __expf(pw[g]));
+                    cr[g] = r1.z;
+                    cg[g] = r1.w;
                 }
                 // upstream's front-to-back step without branches or lane-mask logic
                 // (selects on VGPRs only: the per-Gaussian SALU work of bool masks
@@ -87,23 +88,23 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
                 // Gaussian (power > 0, alpha < 1/255, pixel finished) — a zero alpha
                 // leaves T and C unchanged.  T >= 1e-4 holds for every live pixel, so
                 // the stop test can only fire for a > 0, exactly upstream's test.
-                auto step = [&](bool use, float power, float alpha, float cr, float cg, float cb, int k) {
-                    float av = power > 0.0f ? 0.0f : alpha;
-                    av = alpha < 1.0f / 255.0f ? 0.0f : av;
+#pragma unroll
+                for (int g = 0; g < FWD_GROUP; g++) {
+                    const bool use = g == 0 || k + g < ns;  // wave-uniform
+                    float av = pw[g] > 0.0f ? 0.0f : al[g];
+                    av = al[g] < 1.0f / 255.0f ? 0.0f : av;
                     av = use ? av * live : 0.0f;
                     const float test_T = T * (1 - av);
                     const bool sat = test_T < 0.0001f;  // this Gaussian is not blended; the pixel stops
                     av = sat ? 0.0f : av;
                     live = sat ? 0.0f : live;
                     const float wgt = av * T;
-                    C0 += cr * wgt;
-                    C1 += cg * wgt;
-                    C2 += cb * wgt;
+                    C0 += cr[g] * wgt;
+                    C1 += cg[g] * wgt;
+                    C2 += cb[g] * wgt;
                     T = sat ? T : test_T;
-                    last = av > 0.0f ? (uint32_t)(pos + k + 1) : last;
-                };
-                step(true, pa, alpha_a, a1.z, a1.w, acb, la);
-                step(two, pb, alpha_b, b1.z, b1.w, bcb, lb);
+                    last = av > 0.0f ? (uint32_t)(pos + li[g] + 1) : last;
+                }
                 if (!__any(live > 0.0f)) return true;
             }
             return false;
