@@ -14,18 +14,28 @@
 
 namespace gsr {
 
-// row r, column c of a [rows][RW] block -> padded LDS index
+// row r, column c of a [rows][RW] block -> padded LDS index.  RWC > 0: the row
+// width is a compile-time constant and the division is a multiply-shift (the
+// SH row of degree 3 is 48 floats); RWC = 0: run-time width, float reciprocal
+// with exact integer fix-ups.
+template <int RWC>
 __device__ __forceinline__ int lds_row_index(int e, int RW, float invRW) {
-    int r = (int)((float)e * invRW);
-    r += ((r + 1) * RW <= e) ? 1 : 0;
-    r -= (r * RW > e) ? 1 : 0;
-    return r * (RW + 1) + (e - r * RW);
+    if constexpr (RWC > 0) {
+        const int r = (int)((uint32_t)e / (uint32_t)RWC);
+        return r * (RWC + 1) + (e - r * RWC);
+    } else {
+        int r = (int)((float)e * invRW);
+        r += ((r + 1) * RW <= e) ? 1 : 0;
+        r -= (r * RW > e) ? 1 : 0;
+        return r * (RW + 1) + (e - r * RW);
+    }
 }
 
 // Copy rows [g0, g0 + n) of a row-major float [*, RW] array into LDS rows of
 // stride RW + 1.  All threads of the workgroup must call it.
-template <int THREADS>
-__device__ inline void rows_to_lds(const float *__restrict__ src, int g0, int n, int RW, float *lds) {
+template <int THREADS, int RWC = 0>
+__device__ inline void rows_to_lds(const float *__restrict__ src, int g0, int n, int RW_, float *lds) {
+    const int RW = RWC > 0 ? RWC : RW_;
     const int total = n * RW;
     const float invRW = 1.0f / (float)RW;
     const float *base = src + (size_t)g0 * RW;
@@ -47,22 +57,23 @@ __device__ inline void rows_to_lds(const float *__restrict__ src, int g0, int n,
                 const int i = i0 + b * THREADS;
                 if (i < n4) {
                     const int e = i << 2;
-                    lds[lds_row_index(e, RW, invRW)] = v[b].x;
-                    lds[lds_row_index(e + 1, RW, invRW)] = v[b].y;
-                    lds[lds_row_index(e + 2, RW, invRW)] = v[b].z;
-                    lds[lds_row_index(e + 3, RW, invRW)] = v[b].w;
+                    lds[lds_row_index<RWC>(e, RW, invRW)] = v[b].x;
+                    lds[lds_row_index<RWC>(e + 1, RW, invRW)] = v[b].y;
+                    lds[lds_row_index<RWC>(e + 2, RW, invRW)] = v[b].z;
+                    lds[lds_row_index<RWC>(e + 3, RW, invRW)] = v[b].w;
                 }
             }
         }
-        for (int e = (n4 << 2) + threadIdx.x; e < total; e += THREADS) lds[lds_row_index(e, RW, invRW)] = base[e];
+        for (int e = (n4 << 2) + threadIdx.x; e < total; e += THREADS) lds[lds_row_index<RWC>(e, RW, invRW)] = base[e];
     } else {
-        for (int e = threadIdx.x; e < total; e += THREADS) lds[lds_row_index(e, RW, invRW)] = base[e];
+        for (int e = threadIdx.x; e < total; e += THREADS) lds[lds_row_index<RWC>(e, RW, invRW)] = base[e];
     }
 }
 
 // The reverse: LDS rows (stride RW + 1) -> global rows [g0, g0 + n).
-template <int THREADS>
-__device__ inline void lds_to_rows(const float *lds, int g0, int n, int RW, float *__restrict__ dst) {
+template <int THREADS, int RWC = 0>
+__device__ inline void lds_to_rows(const float *lds, int g0, int n, int RW_, float *__restrict__ dst) {
+    const int RW = RWC > 0 ? RWC : RW_;
     const int total = n * RW;
     const float invRW = 1.0f / (float)RW;
     float *base = dst + (size_t)g0 * RW;
@@ -72,15 +83,15 @@ __device__ inline void lds_to_rows(const float *lds, int g0, int n, int RW, floa
         for (int i = threadIdx.x; i < n4; i += THREADS) {
             const int e = i << 2;
             float4 v;
-            v.x = lds[lds_row_index(e, RW, invRW)];
-            v.y = lds[lds_row_index(e + 1, RW, invRW)];
-            v.z = lds[lds_row_index(e + 2, RW, invRW)];
-            v.w = lds[lds_row_index(e + 3, RW, invRW)];
+            v.x = lds[lds_row_index<RWC>(e, RW, invRW)];
+            v.y = lds[lds_row_index<RWC>(e + 1, RW, invRW)];
+            v.z = lds[lds_row_index<RWC>(e + 2, RW, invRW)];
+            v.w = lds[lds_row_index<RWC>(e + 3, RW, invRW)];
             b4[i] = v;
         }
-        for (int e = (n4 << 2) + threadIdx.x; e < total; e += THREADS) base[e] = lds[lds_row_index(e, RW, invRW)];
+        for (int e = (n4 << 2) + threadIdx.x; e < total; e += THREADS) base[e] = lds[lds_row_index<RWC>(e, RW, invRW)];
     } else {
-        for (int e = threadIdx.x; e < total; e += THREADS) base[e] = lds[lds_row_index(e, RW, invRW)];
+        for (int e = threadIdx.x; e < total; e += THREADS) base[e] = lds[lds_row_index<RWC>(e, RW, invRW)];
     }
 }
 

@@ -61,16 +61,17 @@ __device__ inline float sh_channel(const float *sh, int c, int deg, float x, flo
     return result + 0.5f;
 }
 
+template <int RWC>
 __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) {
     __shared__ uint32_t wsum[PRE_THREADS / 64];
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
     const gsr_inputs &in = a.in;
     const int g0 = blockIdx.x * PRE_THREADS;
     const int idx = g0 + threadIdx.x;
-    const int RW = 3 * in.M;
+    const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
     const bool use_sh = in.sh != nullptr && in.colors_precomp == nullptr;
     if (use_sh) {
-        rows_to_lds<PRE_THREADS>(in.sh, g0, min(PRE_THREADS, in.P - g0), RW, sh_lds);
+        rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, min(PRE_THREADS, in.P - g0), RW, sh_lds);
         __syncthreads();
     }
     uint32_t touched = 0, key = 0;
@@ -316,7 +317,13 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
     a.radii = radii;
     const int nb = pre_blocks(in.P);
     const size_t lds = (in.sh && !in.colors_precomp) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
-    hipLaunchKernelGGL(preprocess_fwd_kernel, dim3(nb), dim3(PRE_THREADS), lds, s, a);
+    // SH row width as a compile-time constant for the common degrees (cheap LDS
+    // row indexing); any other width takes the run-time path
+    switch (3 * in.M) {
+        case 48: hipLaunchKernelGGL(preprocess_fwd_kernel<48>, dim3(nb), dim3(PRE_THREADS), lds, s, a); break;
+        case 3: hipLaunchKernelGGL(preprocess_fwd_kernel<3>, dim3(nb), dim3(PRE_THREADS), lds, s, a); break;
+        default: hipLaunchKernelGGL(preprocess_fwd_kernel<0>, dim3(nb), dim3(PRE_THREADS), lds, s, a); break;
+    }
     hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint4 *)a.block_sums, nb,
                        at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl);
     return hipGetLastError();

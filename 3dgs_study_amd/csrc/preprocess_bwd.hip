@@ -112,15 +112,16 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
 // One workgroup = PB_THREADS consecutive Gaussians.  SH rows are staged in LDS
 // (coalesced 16-B loads), each thread overwrites its row with dL/dSH, and the
 // rows are streamed back out coalesced.
+template <int RWC>
 __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PB_THREADS][3M + 1]
     const gsr_inputs &in = a.in;
     const int g0 = blockIdx.x * PB_THREADS;
     const int n = min(PB_THREADS, in.P - g0);
-    const int RW = 3 * in.M;
+    const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
     const bool stage = in.sh != nullptr && a.o.dsh != nullptr && in.M > 0;
     if (stage) {
-        rows_to_lds<PB_THREADS>(in.sh, g0, n, RW, sh_lds);
+        rows_to_lds<PB_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
         __syncthreads();
     }
     if ((int)threadIdx.x < n) {
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     }
     if (stage) {
         __syncthreads();
-        lds_to_rows<PB_THREADS>(sh_lds, g0, n, RW, a.o.dsh);
+        lds_to_rows<PB_THREADS, RWC>(sh_lds, g0, n, RW, a.o.dsh);
     }
 }
 
@@ -330,7 +331,12 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     a.o = o;
     const bool stage = in.sh && o.dsh && in.M > 0;
     const size_t lds = stage ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
-    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + PB_THREADS - 1) / PB_THREADS), dim3(PB_THREADS), lds, s, a);
+    const dim3 grid((in.P + PB_THREADS - 1) / PB_THREADS);
+    switch (3 * in.M) {  // see launch_preprocess
+        case 48: hipLaunchKernelGGL(preprocess_bwd_kernel<48>, grid, dim3(PB_THREADS), lds, s, a); break;
+        case 3: hipLaunchKernelGGL(preprocess_bwd_kernel<3>, grid, dim3(PB_THREADS), lds, s, a); break;
+        default: hipLaunchKernelGGL(preprocess_bwd_kernel<0>, grid, dim3(PB_THREADS), lds, s, a); break;
+    }
     return hipGetLastError();
 }
 
