@@ -34,8 +34,48 @@ __device__ unsigned long long g_bwd_stats[8];
 #define BWD_STAT(k, v) do { } while (0)
 #endif
 
+// Wave order: most forward work first (GSR_BWD_ORDER=1), so that the longest
+// replays start at once instead of forming the kernel's tail; 0 = the forward's
+// XCD strip order.
+#ifndef GSR_BWD_ORDER
+#define GSR_BWD_ORDER 1
+#endif
+
+// Counting sort of the 4T quadrants by the number of Gaussians their forward wave
+// blended, descending (one workgroup: LDS histogram, scan, scatter).  Ties land in
+// any order; only the schedule depends on it, not a result.
+constexpr int ORDER_THREADS = 1024;
+constexpr int ORDER_BUCKETS = ORDER_THREADS;
+__device__ __forceinline__ int order_bucket(uint32_t work) {
+    return ORDER_BUCKETS - 1 - (int)min(work, (uint32_t)ORDER_BUCKETS - 1);
+}
+__global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_t *qwork, int nq, uint32_t *order) {
+    __shared__ uint32_t hist[ORDER_BUCKETS];
+    __shared__ uint32_t wave_sum[ORDER_THREADS / 64];
+    const int t = threadIdx.x, lane = t & 63;
+    hist[t] = 0;
+    __syncthreads();
+    for (int q = t; q < nq; q += ORDER_THREADS) atomicAdd(&hist[order_bucket(qwork[q])], 1u);
+    __syncthreads();
+    const uint32_t v = hist[t];
+    uint32_t x = v;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        x += lane >= o ? y : 0u;
+    }
+    if (lane == 63) wave_sum[t >> 6] = x;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < (t >> 6); i++) base += wave_sum[i];
+    hist[t] = base + x - v;  // exclusive start of bucket t
+    __syncthreads();
+    for (int q = t; q < nq; q += ORDER_THREADS) order[atomicAdd(&hist[order_bucket(qwork[q])], 1u)] = (uint32_t)q;
+}
+
 struct RenderBwdArgs {
     int W, H, gx, tiles;
+    const uint32_t *order;  // [4T] quadrant per workgroup (GSR_BWD_ORDER)
     const uint2 *ranges;
     const uint32_t *point_list;
     const float4 *splats;
@@ -67,9 +107,15 @@ __device__ __forceinline__ float swz_stage(float c, float d, int lane) {
 }
 
 __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs a) {
+#if GSR_BWD_ORDER
+    static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
+    const uint32_t quad = a.order[blockIdx.x];
+    const int tile = (int)(quad >> 2), w = (int)(quad & 3), lane = threadIdx.x & 63;
+#else
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
     if (tile < 0) return;
+#endif
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
@@ -330,7 +376,16 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
     a.dL_dpix = dL_dpix;
     a.accum = accum;
+#if GSR_BWD_ORDER
+    uint32_t *order = at<uint32_t>(const_cast<void *>(img), Im.qorder);
+    a.order = order;
+    hipLaunchKernelGGL(quad_order_kernel, dim3(1), dim3(ORDER_THREADS), 0, s, at<uint32_t>(img, Im.qwork), 4 * g.tiles,
+                       order);
+    hipLaunchKernelGGL(render_bwd_kernel, dim3(4 * g.tiles), dim3(BLEND_THREADS), 0, s, a);
+#else
+    a.order = nullptr;
     hipLaunchKernelGGL(render_bwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
+#endif
     return hipGetLastError();
 }
 

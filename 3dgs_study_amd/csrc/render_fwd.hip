@@ -28,6 +28,7 @@ struct RenderFwdArgs {
     float *out_color;
     float *final_T;
     uint32_t *n_contrib;
+    uint32_t *qwork;  // [4T] Gaussians this quadrant blended: the backward's wave-order key
 };
 
 #ifndef GSR_FWD_GROUP
@@ -49,6 +50,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
 
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
     uint32_t last = 0;
+    uint32_t work = 0;  // wave-uniform: surviving Gaussians walked (~ the backward's replay work)
     float live = inside ? 1.0f : 0.0f;  // 0 once the pixel has stopped (or lies outside the image)
     __shared__ ChunkStage stage[BLEND_WAVES];
     ChunkStage &st = stage[BLEND_WAVES == 1 ? 0 : w];
@@ -60,6 +62,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
         auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
             const int ns = stage_survivors(st, lane, rel, __ballot(rel), A, B, C);
+            work += ns;
             // FWD_GROUP Gaussians per iteration: their LDS reads, powers and exps are
             // independent, so each wave has that much instruction-level parallelism
             // to cover LDS and transcendental latency; only the T recurrence is serial.
@@ -135,6 +138,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
             if ((pos += 64) >= n) break;
         }
     }
+    if (lane == 0) a.qwork[4 * tile + w] = work;
     if (inside) {
         const size_t pix = (size_t)a.W * py + px;
         const size_t HW = (size_t)a.W * a.H;
@@ -163,6 +167,7 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
     a.out_color = out_color;
     a.final_T = at<float>(img, Im.off[GSR_IMG_FINAL_T]);
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
+    a.qwork = at<uint32_t>(img, Im.qwork);
     hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }

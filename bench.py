@@ -38,7 +38,9 @@ WORKLOADS = {
     "C": "1M Gaussians, 1920x1080, SH deg 3, render->L1->backward, one view per GPU per step",
     "B": "100k Gaussians, 800x800, SH deg 3, render->L1->backward, one view per GPU per step",
     "A": "10k Gaussians, 256x256, SH deg 0, render->L1->backward, one view per GPU per step",
+    "E": "5M Gaussians, 3840x2160, SH deg 3, render() forward only (no grad), one view per GPU per step",
 }
+RENDER_METRIC = "render frames/sec (fwd-only) + Mpix/sec, 4K (3840x2160), 5M Gaussians, SH3"
 
 
 def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, M: int) -> float:
@@ -112,6 +114,8 @@ def main():
                     help="0 = L1-only headline unit; 0.2 = the reference's L1+SSIM loss")
     ap.add_argument("--full-steps", type=int, default=20,
                     help="timed iterations of the full train.py step (L1+SSIM, Adam), torch vs fused; 0 = skip")
+    ap.add_argument("--render-steps", type=int, default=20,
+                    help="timed forward-only renders of config E (5M, 4K) reported beside the C line; 0 = skip")
     args = ap.parse_args()
 
     import torch
@@ -132,6 +136,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    if not synthetic.CONFIGS[args.config]["backward"]:
+        render_main(args, dev, world, rank)
+        return
     cfg = synthetic.CONFIGS[args.config]
     P, W, H, deg = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
     M = (deg + 1) ** 2
@@ -229,8 +236,96 @@ def main():
         }
         if world == 1 and args.full_steps > 0:
             line["full_step"] = full_step_rates(cam, P, deg, target, bg, args.full_steps)
+        if world == 1 and args.render_steps > 0:
+            del out
+            line["config_E_render"] = render_rates("E", dev, args.render_steps, 3)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(P, W, H, deg)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0) -> dict:
+    """Forward-only throughput of reference render() (render.py:37-49 renders under
+    torch.no_grad()) at a forward-only config (E: 5M Gaussians, 4K, SH3): frames/s,
+    Mpix/s, the per-stage split, and render_fwd's algorithmic bytes ÷ its live time."""
+    import torch
+
+    import synthetic
+    import train_step
+    from diff_gaussian_rasterization import _C
+
+    cfg = synthetic.CONFIGS[cfg_name]
+    P, W, H, deg = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
+    M = (deg + 1) ** 2
+    cam = synthetic.make_camera(W, H, view=view).to(dev)
+    g = synthetic.make_gaussians(P, deg, seed=0).to(dev)
+    bg = torch.zeros(3, device=dev)
+    with torch.no_grad():
+        for i in range(warmup):
+            if i == warmup - 1:
+                _C.timing_enable(True)
+            train_step.render(cam, g, bg)
+        torch.cuda.synchronize()
+        stages = _C.timing_read()
+        _C.timing_enable(["render_fwd"])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            train_step.render(cam, g, bg)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        live = _C.timing_read()["render_fwd"]
+        _C.timing_enable(False)
+    I = _last_num_rendered(cam, g, bg)
+    fwd_ms = live[0] / live[1] if live[1] else 0.0
+    ab = algorithmic_bytes("render_fwd", P, I, W, H, M)
+    achieved = ab / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+    fps = steps / dt
+    res = {
+        "metric": RENDER_METRIC, "value": round(fps, 3), "unit": "frames/s", "ms_per_frame": round(1e3 * dt / steps, 4),
+        "mpix_per_s": round(fps * W * H / 1e6, 2), "steps": steps, "warmup": warmup,
+        "config": {"workload": f"{cfg_name}: {WORKLOADS[cfg_name]}", "gaussians": P, "width": W, "height": H,
+                   "sh_degree": deg, "num_rendered": I},
+        "stages_ms": {k: round(ms / n, 4) for k, (ms, n) in stages.items() if n},
+        "roofline": {"bound": "hbm", "kernel": "render_fwd", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("render_fwd_E"),
+                     "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(fwd_ms, 4)},
+    }
+    fwd_bytes = sum(algorithmic_bytes(k, P, I, W, H, M) for k in
+                    ("preprocess", "depth_sort", "duplicate", "tile_sort", "render_fwd"))
+    res["forward_algorithmic_bytes"] = fwd_bytes
+    res["forward_hbm_frac"] = round(fwd_bytes * fps / 1e9 / HBM_PEAK_GBS, 4)
+    del g
+    torch.cuda.empty_cache()
+    return res
+
+
+def render_main(args, dev, world: int, rank: int) -> None:
+    """--config E: the forward-only stress config as its own JSON line (views shard
+    over ranks, no collective: each rank renders view rank % 8)."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.barrier()
+    r = render_rates(args.config, dev, args.steps, args.warmup, view=rank % 8)
+    elapsed = args.steps / r["value"]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        W, H = r["config"]["width"], r["config"]["height"]
+        value = world * args.steps / elapsed
+        line = {"metric": RENDER_METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic (seeded Gaussians in a radius-2 ball, camera at distance 6, SURVEY.md §8d)",
+                "config": dict(r["config"], views_per_step=world, parallelism=f"view-parallel x{world}"),
+                "mpix_per_s": round(value * W * H / 1e6, 2), "stages_ms": r["stages_ms"], "roofline": r["roofline"],
+                "forward_hbm_frac": r["forward_hbm_frac"], "cpu_baseline": None}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
