@@ -71,7 +71,7 @@ __device__ __forceinline__ void wait_vmcnt_4() { __builtin_amdgcn_s_waitcnt(0x0F
 // per-Gaussian loop reads the record back with uniform-address ds_reads
 // (broadcast) — LDS-pipe work instead of nine or ten VALU v_readlanes.
 struct ChunkStage {
-    float4 rec[64][3];
+    float4 rec[65][3];  // render_bwd.hip keeps its survivors in 1..64 (0 = a zero record)
 };
 __device__ __forceinline__ void stage_chunk(ChunkStage &st, int lane, const float4 &A, const float4 &B,
                                             const float4 &C) {
@@ -81,15 +81,15 @@ __device__ __forceinline__ void stage_chunk(ChunkStage &st, int lane, const floa
 }
 
 // Compacted chunk image: only the entries that survived the cull, in chunk
-// order (slot = number of survivors in lower lanes), each record's last word
+// order (slot = first + number of survivors in lower lanes), each record's last word
 // holding the entry's lane (its list position minus the chunk start).  The
 // Gaussian loops then walk slots 0..n-1 with an affine index — no find-first-set
 // chains on the scalar unit between one pair's LDS reads and the next's.
 __device__ __forceinline__ int stage_survivors(ChunkStage &st, int lane, bool rel, uint64_t mask, const float4 &A,
-                                               const float4 &B, const float4 &C) {
+                                               const float4 &B, const float4 &C, int first = 0) {
     if (rel) {
-        const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        const int slot = first + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
         st.rec[slot][0] = A;
         st.rec[slot][1] = B;
         st.rec[slot][2] = make_float4(C.x, C.y, C.z, __int_as_float(lane));

@@ -106,6 +106,13 @@ __device__ __forceinline__ float swz_stage(float c, float d, int lane) {
     return keep + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send), 0x1F | (K << 10)));
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const volatile f32x4 lds_f32x4;
+__device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
+    const f32x4 v = *p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs a) {
 #if GSR_BWD_ORDER
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
@@ -144,20 +151,23 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
 
     __shared__ ChunkStage stage[BLEND_WAVES];
     ChunkStage &st = stage[BLEND_WAVES == 1 ? 0 : w];
+    // record 0: the dummy b of an odd survivor count — zeros replay as a skipped
+    // Gaussian (alpha 0, finite colour), and its atomic is never issued
+    if (lane < 3) st.rec[0][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     float T = T_final;
     float R0 = 0.f, R1 = 0.f, R2 = 0.f;
     const uint32_t *list = a.point_list + r.x;
 
-    // The paired reduce-scatter below leaves Gaussian a's nine sums in lanes
-    // {0,32,16,48,8,40,24,56,4} (slots 0..8) and b's in {20,52,12,44,28,60,2,34,36}
-    // of ONE register, so each Gaussian costs one atomic wave-instruction: nine
-    // lanes into one 64-B accumulator row = one memory-side atomic request.
-    // (Derived by simulating the six exchange stages; tests/test_gpu_parity.py
-    // checks every gradient.)
+    // The role-swapped reduce-scatter below leaves Gaussian a's nine sums in lanes
+    // {0,8,4,12,2,10,6,14,1} (slots 0..8) and b's in {16,24,20,28,18,26,22,30,17}
+    // of ONE register (and again 32 lanes up), so each Gaussian costs one atomic
+    // wave-instruction: nine lanes into one 64-B accumulator row = one memory-side
+    // atomic request.  (Derived by simulating the exchange stages; tests/
+    // test_gpu_parity.py checks every gradient.)
     int slot_a = -1, slot_b = -1;
     {
-        constexpr int8_t LA[9] = {0, 16, 8, 24, 4, 20, 12, 28, 2};
-        constexpr int8_t LB[9] = {50, 42, 58, 38, 54, 46, 62, 33, 49};
+        constexpr int8_t LA[9] = {0, 8, 4, 12, 2, 10, 6, 14, 1};
+        constexpr int8_t LB[9] = {16, 24, 20, 28, 18, 26, 22, 30, 17};
 #pragma unroll
         for (int j = 0; j < 9; j++) {
             slot_a = lane == LA[j] ? j : slot_a;
@@ -165,6 +175,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         }
     }
     const bool act_a = slot_a >= 0, act_b = slot_b >= 0;
+    // lanes 16-31 (and 48-63) keep Gaussian b's sums in the first exchange stage
+    const bool h16 = (lane & 16) != 0;
 
     struct Pre {
         float dx, dy, G, alpha;
@@ -186,8 +198,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         q.valid = live && k < lim && !(power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
         return q;
     };
-    struct G9 {
-        float g0, g1, g2, g3, g4, g5, g6, g7, g8;
+    // The per-pixel quantities the nine sums of one Gaussian are made of.
+    struct Part {
+        float W, dx, dy, g5, t;
     };
     // Branch-free replay step: a skipped pixel sees alpha = 0 (T and the running
     // colour R unchanged) and zero gradients.  R is upstream's accum_rec advanced
@@ -197,7 +210,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         const float av = q.valid ? q.alpha : 0.0f;
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
         T = T * inv_1ma;
-        const float dchannel_dcolor = av * T;
         const float e0 = cr - R0, e1 = cg - R1, e2 = cb - R2;
         const float dot = e0 * dpx0 + e1 * dpx1 + e2 * dpx2;
         R0 += av * e0;
@@ -211,61 +223,58 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         // once in preprocess_bwd.hip, so the accumulator holds sum W (dx, dy) and
         // sum W (dx^2, dx dy, dy^2).  G is finite (power <= 0 for the positive-
         // definite conic), so an invalid pixel's zero dL/dalpha zeroes them all.
-        G9 g;
-        g.g5 = q.G * dL_dalpha;
-        const float Wg = g.g5 * op;
-        g.g0 = Wg * q.dx;
-        g.g1 = Wg * q.dy;
-        g.g2 = g.g0 * q.dx;
-        g.g3 = g.g0 * q.dy;
-        g.g4 = g.g1 * q.dy;
-        g.g6 = dchannel_dcolor * dpx0;
-        g.g7 = dchannel_dcolor * dpx1;
-        g.g8 = dchannel_dcolor * dpx2;
-        return g;
+        Part p;
+        p.g5 = q.G * dL_dalpha;
+        p.W = p.g5 * op;
+        p.dx = q.dx;
+        p.dy = q.dy;
+        p.t = av * T;  // dchannel/dcolor
+        return p;
     };
 
     // Reduce-scatter of a pair's 18 sums and their two atomic wave instructions.
-    auto reduce_emit = [&](const G9 &ga, const G9 &gb, uint32_t gida, uint32_t gidb, bool two) {
-        // reduce-scatter of the 18 sums inside each 32-lane half with ds_swizzle
-        // (xor 16, 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per output
-        // register) and one final v_permlane32 self-swap adding the two halves
+    // First stage (xor 16) with swapped roles: lanes 16-31 keep b's values and
+    // send a's, so the nine outputs need only the ten selects of the five base
+    // quantities instead of eighteen selects of the products.  Then four more
+    // ds_swizzle stages (xor 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per
+    // output register) and one final v_permlane32 self-swap adding the two halves.
+    auto reduce_emit = [&](const Part &pa, const Part &pb, uint32_t gida, uint32_t gidb, bool two) {
+        const float kW = h16 ? pb.W : pa.W, sW = h16 ? pa.W : pb.W;
+        const float kx = h16 ? pb.dx : pa.dx, sx = h16 ? pa.dx : pb.dx;
+        const float ky = h16 ? pb.dy : pa.dy, sy = h16 ? pa.dy : pb.dy;
+        const float k5 = h16 ? pb.g5 : pa.g5, s5 = h16 ? pa.g5 : pb.g5;
+        const float kt = h16 ? pb.t : pa.t, st_ = h16 ? pa.t : pb.t;
+        const float k0 = kW * kx, s0 = sW * sx;
+        const float k1 = kW * ky, s1 = sW * sy;
+        auto x16 = [&](float keep, float send) {
+            return keep + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send),
+                                                                                0x1F | (16 << 10)));
+        };
 #ifdef GSR_EXP_NO_REDUCE  // timing experiment only
-        const float v = ga.g0 + ga.g1 + ga.g2 + ga.g3 + ga.g4 + ga.g5 + ga.g6 + ga.g7 + ga.g8 + gb.g0 + gb.g1 +
-                        gb.g2 + gb.g3 + gb.g4 + gb.g5 + gb.g6 + gb.g7 + gb.g8;
+        const float v = k0 + s0 + k1 + s1 + k0 * kx + s0 * sx + k0 * ky + s0 * sy + k1 * ky + s1 * sy + k5 + s5 +
+                        kt * dpx0 + st_ * dpx1 + kt * dpx2;
 #else
-        const float s0 = swz_stage<16>(ga.g0, ga.g1, lane);
-        const float s1 = swz_stage<16>(ga.g2, ga.g3, lane);
-        const float s2 = swz_stage<16>(ga.g4, ga.g5, lane);
-        const float s3 = swz_stage<16>(ga.g6, ga.g7, lane);
-        const float s4 = swz_stage<16>(ga.g8, gb.g0, lane);
-        const float s5 = swz_stage<16>(gb.g1, gb.g2, lane);
-        const float s6 = swz_stage<16>(gb.g3, gb.g4, lane);
-        const float s7 = swz_stage<16>(gb.g5, gb.g6, lane);
-        const float s8 = swz_stage<16>(gb.g7, gb.g8, lane);
-        const float t0 = swz_stage<8>(s0, s1, lane);
-        const float t1 = swz_stage<8>(s2, s3, lane);
-        const float t2 = swz_stage<8>(s4, s5, lane);
-        const float t3 = swz_stage<8>(s6, s7, lane);
-        const float t4 = swz_stage<8>(s8, 0.f, lane);
+        const float o0 = x16(k0, s0);
+        const float o1 = x16(k1, s1);
+        const float o2 = x16(k0 * kx, s0 * sx);
+        const float o3 = x16(k0 * ky, s0 * sy);
+        const float o4 = x16(k1 * ky, s1 * sy);
+        const float o5 = x16(k5, s5);
+        const float o6 = x16(kt * dpx0, st_ * dpx0);
+        const float o7 = x16(kt * dpx1, st_ * dpx1);
+        const float o8 = x16(kt * dpx2, st_ * dpx2);
+        const float t0 = swz_stage<8>(o0, o1, lane);
+        const float t1 = swz_stage<8>(o2, o3, lane);
+        const float t2 = swz_stage<8>(o4, o5, lane);
+        const float t3 = swz_stage<8>(o6, o7, lane);
+        const float t4 = swz_stage<8>(o8, 0.f, lane);
         const float u0 = swz_stage<4>(t0, t1, lane);
         const float u1 = swz_stage<4>(t2, t3, lane);
         const float u2 = swz_stage<4>(t4, 0.f, lane);
-#ifdef GSR_BWD_DPP_TAIL  // experiment: the last two (short) stages on DPP quad permutes
-        const float w0 = ((lane & 2) ? u1 : u0) + dpp_f32<DPP_QUAD_XOR2>((lane & 2) ? u0 : u1);
-        const float w1 = ((lane & 2) ? 0.f : u2) + dpp_f32<DPP_QUAD_XOR2>((lane & 2) ? u2 : 0.f);
-        const float o0 = ((lane & 1) ? w1 : w0) + dpp_f32<DPP_QUAD_XOR1>((lane & 1) ? w0 : w1);
-#else
         const float w0 = swz_stage<2>(u0, u1, lane);
         const float w1 = swz_stage<2>(u2, 0.f, lane);
-        const float o0 = swz_stage<1>(w0, w1, lane);
-#endif
-#ifdef GSR_BWD_BPERM_FINAL  // experiment: the cross-half add through ds_bpermute
-        const float v = o0 + __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2,
-                                                                                    __builtin_bit_cast(int, o0)));
-#else
-        const float v = swap32_sum(o0, o0);  // both halves: the full sum
-#endif
+        const float x0 = swz_stage<1>(w0, w1, lane);
+        const float v = swap32_sum(x0, x0);  // both halves: the full sum
 #endif
         // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
         // compiler's atomic optimizer (a wave-scan loop) out
@@ -276,27 +285,31 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
 #endif
     };
-#ifdef GSR_BWD_PIPE
-    G9 pga = {}, pgb = {};  // the pending pair (zeros into Gaussian 0's row at first: harmless)
-    uint32_t pgida = 0, pgidb = 0;
-    bool ptwo = false;
-#endif
 
     // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l),
     // two Gaussians per iteration: independent LDS reads and exps (ILP), one
-    // fused reduce-scatter of their 18 sums (no half-empty permlane32 stage).
+    // fused reduce-scatter of their 18 sums.  The survivors sit in records 1..ns
+    // (record 0 is the odd pair's dummy b), so pair (a, b) = records (s + 1, s) and
+    // both are read from ONE VGPR address with immediate offsets.
     auto replay_chunk = [&](int lo, float4 A, float4 B, float4 C) {
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         const uint64_t mask = __ballot(rel);
-        const int ns = stage_survivors(st, lane, rel, mask, A, B, C);
+        const int ns = stage_survivors(st, lane, rel, mask, A, B, C, 1);
         BWD_STAT(1, 1);
         BWD_STAT(4, ns);
         const int lim = last_contrib - lo;  // entry lo + l replays for this pixel iff l < lim
+        // byte offset of record b = k - 1 + 1 in a VGPR (asm barrier: keep it there)
+        uint32_t boff = (uint32_t)(ns - 1) * (uint32_t)sizeof(st.rec[0]);
+        asm volatile("" : "+v"(boff));
+        const char *sbase = reinterpret_cast<const char *>(&st.rec[0][0]);
         for (int k = ns - 1; k >= 0; k -= 2) {
             const bool two = k >= 1;  // wave-uniform
-            const int ka = k, kb = two ? k - 1 : k;
-            const float4 a0 = st.rec[ka][0], a1 = st.rec[ka][1], a2 = st.rec[ka][2];
-            const float4 b0 = st.rec[kb][0], b1 = st.rec[kb][1], b2 = st.rec[kb][2];
+            // whole 16-B reads (volatile: the load vectorizer would otherwise split
+            // the records into 8-B pieces around the unused fields)
+            lds_f32x4 *rb = (lds_f32x4 *)(sbase + boff);
+            const float4 b0 = ld4(rb + 0), b1 = ld4(rb + 1), b2 = ld4(rb + 2);
+            const float4 a0 = ld4(rb + 3), a1 = ld4(rb + 4), a2 = ld4(rb + 5);
+            boff -= 2 * (uint32_t)sizeof(st.rec[0]);
             const int la = __float_as_int(a2.w), lb = __float_as_int(b2.w);
             const Pre qa = prepare(a0, a1, la, lim, true);  // entry lo + l = upstream `contributor`
             const Pre qb = prepare(b0, b1, lb, lim, two);
@@ -310,22 +323,11 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
                 BWD_STAT(6, __builtin_popcountll(va) + __builtin_popcountll(vb));
             }
 #endif
-            const G9 ga = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: ka > kb
-            const G9 gb = replay(qb, b1.y, b1.z, b1.w, b2.x);
+            const Part pa = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: a before b
+            const Part pb = replay(qb, b1.y, b1.z, b1.w, b2.x);
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.y));
             const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.y));
-#ifdef GSR_BWD_PIPE
-            // software pipeline: this pair's sums are reduced in the next iteration,
-            // so the swizzle chain's LDS latency overlaps the next pair's replay
-            reduce_emit(pga, pgb, pgida, pgidb, ptwo);
-            pga = ga;
-            pgb = gb;
-            pgida = gida;
-            pgidb = gidb;
-            ptwo = two;
-#else
-            reduce_emit(ga, gb, gida, gidb, two);
-#endif
+            reduce_emit(pa, pb, gida, gidb, two);
         }
     };
     // Double-buffered backwards stream, unrolled by two so the buffers swap roles
@@ -353,9 +355,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         replay_chunk(lo, A1, B1, C1);
         if ((lo -= 64) + 64 <= 0) break;
     }
-#ifdef GSR_BWD_PIPE
-    reduce_emit(pga, pgb, pgida, pgidb, ptwo);
-#endif
 }
 
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
