@@ -92,6 +92,18 @@ __device__ __forceinline__ bool pass_skipped(const RadixPass &a) {
     return a.role == RX_DEPTH_FOURTH && a.ctrl[CTRL_DSORT_PASSES] == 3;
 }
 
+// Workgroup -> radix block.  The per-block digit counts live column-major
+// (hist[digit][block], so the digit scan reads rows); neighbouring blocks share
+// their 32-B sectors.  Workgroups are dealt round-robin over the 8 XCDs, so give
+// each XCD a contiguous run of blocks: a sector's partial writes (upsweep) and
+// reads (downsweep) then meet in one L2 instead of crossing to HBM once per
+// block.  A bijection on [0, NB); placement is a speed hint only.
+__device__ __forceinline__ uint32_t radix_block(int NB) {
+    const uint32_t x = blockIdx.x & 7u, j = blockIdx.x >> 3;
+    const uint32_t q = (uint32_t)NB >> 3, r = (uint32_t)NB & 7u;
+    return x * q + min(x, r) + j;
+}
+
 // ITEMS per thread: fewer for short inputs (more workgroups, shorter serial
 // rank chains), more for long ones (fewer blocks in the digit scan).
 template <int ITEMS>
@@ -103,7 +115,8 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t base = blockIdx.x * (uint32_t)TILE_N + w * (uint32_t)WAVE_N + lane;
+    const uint32_t blk = radix_block(a.NB);
+    const uint32_t base = blk * (uint32_t)TILE_N + w * (uint32_t)WAVE_N + lane;
     uint32_t kk[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
@@ -117,7 +130,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) c += h[k][threadIdx.x];
-    a.hist[(size_t)threadIdx.x * a.NB + blockIdx.x] = c;
+    a.hist[(size_t)threadIdx.x * a.NB + blk] = c;
 }
 
 // One workgroup per digit: exclusive scan of that digit's block counts.
@@ -152,7 +165,8 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     uint32_t *const vout = final3 ? a.vout_final : a.vout;
     const bool gather = a.gdst && (a.role != RX_DEPTH_THIRD || final3);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t b0 = blockIdx.x * (uint32_t)TILE_N;
+    const uint32_t blk = radix_block(a.NB);
+    const uint32_t b0 = blk * (uint32_t)TILE_N;
     const uint32_t base = b0 + w * (uint32_t)WAVE_N + lane;
     uint32_t kk[ITEMS], vv[ITEMS], rk[ITEMS];
 #pragma unroll
@@ -166,7 +180,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         const uint32_t t = a.totals[threadIdx.x];
         uint32_t tot;
         const uint32_t inc = block_inclusive_scan<RX_THREADS>(t, wsum, &tot);
-        gstart[threadIdx.x] = inc - t + a.hist[(size_t)threadIdx.x * a.NB + blockIdx.x];
+        gstart[threadIdx.x] = inc - t + a.hist[(size_t)threadIdx.x * a.NB + blk];
     }
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) cnt[k][threadIdx.x] = 0;

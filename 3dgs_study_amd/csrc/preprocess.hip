@@ -70,19 +70,42 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     const int idx = g0 + threadIdx.x;
     const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
     const bool use_sh = in.sh != nullptr && in.colors_precomp == nullptr;
-    if (use_sh) {
-        rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, min(PRE_THREADS, in.P - g0), RW, sh_lds);
-        __syncthreads();
+    const int n = min(PRE_THREADS, in.P - g0);
+    // This Gaussian's own inputs are loaded first and the workgroup's SH rows after
+    // them: the row loads (12 x 16 B per lane at degree 3) stay in flight behind
+    // the geometry below (vmcnt counts in issue order) and go to LDS only before
+    // the colour evaluation.
+    constexpr bool PREFETCH = RWC > 0 && RWC % 4 == 0;
+    const bool live = idx < in.P;
+    const int li = live ? idx : in.P - 1;
+    const f3 p = {in.means3D[3 * li], in.means3D[3 * li + 1], in.means3D[3 * li + 2]};
+    const Mat4 V = load_mat4(in.viewmatrix);
+    const Mat4 Pm = load_mat4(in.projmatrix);
+    float gin[7];  // scales + rotation, or the precomputed cov3D
+    if (in.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) gin[k] = in.cov3D_precomp[6 * (size_t)li + k];
+        gin[6] = 0.f;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) gin[k] = in.scales[3 * (size_t)li + k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) gin[3 + k] = in.rotations[4 * (size_t)li + k];
     }
+    const float opac = in.opacities[li];
+    RowPrefetch<PRE_THREADS, PREFETCH ? RWC : 4> pf;
+    if (PREFETCH)  // unconditional (a dummy load of element 0 without SH rows)
+        pf.load(use_sh ? in.sh : in.means3D, use_sh ? g0 : 0, use_sh ? n : 0);
+    else if (use_sh)
+        rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
     uint32_t touched = 0, key = 0;
     bool perr = false, key_vis = false;
-    for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
-    if (idx < in.P) {
+    // what the colour stage (after the barrier) needs
+    bool emit = false;
+    float px = 0.f, py = 0.f, conic_x = 0.f, conic_y = 0.f, conic_z = 0.f, qmax = 0.f, depth = 0.f;
+    if (live) {
         int radius_out = 0;
         uint4 rect_out = make_uint4(0u, 0u, 0u, 0u);
-        const f3 p = {in.means3D[3 * idx], in.means3D[3 * idx + 1], in.means3D[3 * idx + 2]};
-        const Mat4 V = load_mat4(in.viewmatrix);
-        const Mat4 Pm = load_mat4(in.projmatrix);
         const f4 p_hom = xform_point4x4(p, Pm);
         const float p_w = 1.0f / (p_hom.w + 0.0000001f);
         const f3 p_proj = {p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w};
@@ -96,11 +119,9 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         if (ok) {
             if (in.cov3D_precomp) {
 #pragma unroll
-                for (int k = 0; k < 6; k++) c3[k] = in.cov3D_precomp[6 * (size_t)idx + k];
+                for (int k = 0; k < 6; k++) c3[k] = gin[k];
             } else {
-                const float *s = in.scales + 3 * (size_t)idx;
-                const float *q = in.rotations + 4 * (size_t)idx;
-                compute_cov3d(s[0], s[1], s[2], in.scale_modifier, q[0], q[1], q[2], q[3], c3);
+                compute_cov3d(gin[0], gin[1], gin[2], in.scale_modifier, gin[3], gin[4], gin[5], gin[6], c3);
             }
         }
         f3 cov = {0, 0, 0};
@@ -112,51 +133,25 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         }
         if (ok) {
             const float det_inv = 1.f / det;
-            const float conic_x = cov.z * det_inv, conic_y = -cov.y * det_inv, conic_z = cov.x * det_inv;
+            conic_x = cov.z * det_inv;
+            conic_y = -cov.y * det_inv;
+            conic_z = cov.x * det_inv;
             const float mid = 0.5f * (cov.x + cov.z);
             const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
             const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
             const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
-            const float px = ndc2pix(p_proj.x, in.W), py = ndc2pix(p_proj.y, in.H);
+            px = ndc2pix(p_proj.x, in.W);
+            py = ndc2pix(p_proj.y, in.H);
             const int r = f2i_sat(my_radius);
             const TileRect rc = get_rect(px, py, r, a.gx, a.gy);
             const uint32_t area = (rc.x1 - rc.x0) * (rc.y1 - rc.y0);
             if (area != 0) {
-                float rgb[3];
-                uint8_t clampbits = 0;
-                if (in.colors_precomp) {
-                    rgb[0] = in.colors_precomp[3 * (size_t)idx];
-                    rgb[1] = in.colors_precomp[3 * (size_t)idx + 1];
-                    rgb[2] = in.colors_precomp[3 * (size_t)idx + 2];
-                } else {
-                    const float dx = p.x - in.campos[0], dy = p.y - in.campos[1], dz = p.z - in.campos[2];
-                    const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
-                    const float x = dx / len, y = dy / len, z = dz / len;
-                    const float *sh = sh_lds + threadIdx.x * (RW + 1);
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        const float v = sh_channel(sh, c, in.D, x, y, z);
-                        clampbits |= (v < 0) ? (uint8_t)(1u << c) : (uint8_t)0;
-                        rgb[c] = fmaxf(v, 0.0f);
-                    }
-                }
                 // Cull bound for the blend kernels: alpha = o*exp(-q/2) >= 1/255 needs
                 // q = d^T conic d <= 2 ln(255 o).  Stored widened (0.1% + 0.002) so a
-                // wave may skip a Gaussian only when every pixel would reject it.  The
-                // record also carries the Gaussian's index (the backward's atomic target).
-                const float opac = in.opacities[idx];
-                const float qmax = 2.0f * logf(255.0f * opac) * 1.001f + 0.002f;
-                a.depths[idx] = p_view.z;
-                a.means2D[idx] = make_float2(px, py);
-                float4 *sp = a.splats + 3 * (size_t)idx;
-                // conic and bound stored times -1/2 (exact): the blend kernels then
-                // evaluate upstream's power -0.5 * d^T conic d as d^T conic' d,
-                // bit for bit, one multiply fewer per (pixel, Gaussian)
-                const float ca = -0.5f * conic_x, cb = -0.5f * conic_y, cc = -0.5f * conic_z, qm = -0.5f * qmax;
-                sp[0] = make_float4(px, py, ca, cb);
-                sp[1] = make_float4(cc, opac, rgb[0], rgb[1]);
-                sp[2] = make_float4(rgb[2], __uint_as_float((uint32_t)idx), qm, 0.0f);
-                a.clamped[idx] = clampbits;
+                // wave may skip a Gaussian only when every pixel would reject it.
+                qmax = 2.0f * logf(255.0f * opac) * 1.001f + 0.002f;
+                emit = true;
+                depth = p_view.z;
                 radius_out = r;
                 // Tight footprint: of the bounding rect's tiles keep those whose
                 // 16x16 pixel box meets the alpha >= 1/255 ellipse q(d) <= qmax
@@ -209,6 +204,44 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         a.radii[idx] = radius_out;
         a.tiles_touched[idx] = touched;
         a.rects[idx] = rect_out;
+    }
+    // (stores are counted by vmcnt too: issued here, after the geometry, they do not
+    // hold up its waits for the per-Gaussian loads)
+    for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
+    // colour stage: the SH rows land in LDS now, after the geometry
+    if (PREFETCH && use_sh) pf.store(n, sh_lds);
+    if (use_sh) __syncthreads();
+    if (emit) {
+        float rgb[3];
+        uint8_t clampbits = 0;
+        if (in.colors_precomp) {
+            rgb[0] = in.colors_precomp[3 * (size_t)idx];
+            rgb[1] = in.colors_precomp[3 * (size_t)idx + 1];
+            rgb[2] = in.colors_precomp[3 * (size_t)idx + 2];
+        } else {
+            const float dx = p.x - in.campos[0], dy = p.y - in.campos[1], dz = p.z - in.campos[2];
+            const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+            const float x = dx / len, y = dy / len, z = dz / len;
+            const float *sh = sh_lds + threadIdx.x * (RW + 1);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float v = sh_channel(sh, c, in.D, x, y, z);
+                clampbits |= (v < 0) ? (uint8_t)(1u << c) : (uint8_t)0;
+                rgb[c] = fmaxf(v, 0.0f);
+            }
+        }
+        a.depths[idx] = depth;
+        a.means2D[idx] = make_float2(px, py);
+        // conic and bound stored times -1/2 (exact): the blend kernels then
+        // evaluate upstream's power -0.5 * d^T conic d as d^T conic' d, bit for
+        // bit, one multiply fewer per (pixel, Gaussian).  The record also carries
+        // the Gaussian's index (the backward's atomic target).
+        const float ca = -0.5f * conic_x, cb = -0.5f * conic_y, cc = -0.5f * conic_z, qm = -0.5f * qmax;
+        float4 *sp = a.splats + 3 * (size_t)idx;
+        sp[0] = make_float4(px, py, ca, cb);
+        sp[1] = make_float4(cc, opac, rgb[0], rgb[1]);
+        sp[2] = make_float4(rgb[2], __uint_as_float((uint32_t)idx), qm, 0.0f);
+        a.clamped[idx] = clampbits;
     }
     // num_rendered is only a total (emit works in depth order, binning.hip): each
     // workgroup stores its sum (bit 31 flags a prefiltered violation) and the
@@ -319,9 +352,14 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
     const size_t lds = (in.sh && !in.colors_precomp) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     // SH row width as a compile-time constant for the common degrees (cheap LDS
     // row indexing); any other width takes the run-time path
-    switch (3 * in.M) {
-        case 48: hipLaunchKernelGGL(preprocess_fwd_kernel<48>, dim3(nb), dim3(PRE_THREADS), lds, s, a); break;
+    switch (in.sh && !in.colors_precomp ? 3 * in.M : 0) {
         case 3: hipLaunchKernelGGL(preprocess_fwd_kernel<3>, dim3(nb), dim3(PRE_THREADS), lds, s, a); break;
+        case 48:  // the register prefetch of the rows reads them as float4: 16-B aligned only
+            if (((uintptr_t)in.sh & 15u) == 0) {
+                hipLaunchKernelGGL(preprocess_fwd_kernel<48>, dim3(nb), dim3(PRE_THREADS), lds, s, a);
+                break;
+            }
+            [[fallthrough]];
         default: hipLaunchKernelGGL(preprocess_fwd_kernel<0>, dim3(nb), dim3(PRE_THREADS), lds, s, a); break;
     }
     hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint4 *)a.block_sums, nb,

@@ -59,16 +59,21 @@ def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, M: int) -> flo
     }.get(stage, 0.0)
 
 
-def pmc_traffic(stage: str):
+def pmc_stage(stage: str) -> dict:
+    """profiles/pmc_summary.json's record of a stage (tools/pmc.sh): HBM bytes per
+    launch and the VALU issue utilisation, measured by rocprofv3 --pmc passes."""
     f = ROOT / "profiles" / "pmc_summary.json"
     if not f.exists():
-        return None
+        return {}
     try:
-        d = json.loads(f.read_text())
-        v = d.get("stages", {}).get(stage, {}).get("hbm_bytes_per_launch")
-        return float(v) if v is not None else None
-    except Exception:
-        return None
+        return json.loads(f.read_text()).get("stages", {}).get(stage, {})
+    except (OSError, ValueError):
+        return {}
+
+
+def pmc_traffic(stage: str):
+    v = pmc_stage(stage).get("hbm_bytes_per_launch")
+    return float(v) if v is not None else None
 
 
 def cpu_baseline(P: int, W: int, H: int, deg: int, budget_s: float = 30.0) -> dict:
@@ -231,6 +236,8 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": ab,
                 "avg_launch_ms": round(dom_ms, 4),
+                # the blend loops are issue-bound, not byte-bound: PMC VALU issue share
+                "valu_issue_frac": pmc_stage(dom).get("valu_issue_frac"),
             },
             "cpu_baseline": None,
         }

@@ -89,7 +89,22 @@ def check_binning(h, r, W):
         assert alpha.max() < 1 / 255, f"a dropped tile instance reaches alpha {alpha.max()}"
 
 
-def check_forward(h, r, rgb_from_sh=True, ncontrib_frac=0.999):
+def alpha_flip_pixel(r, x, y, W):
+    """True if pixel (x, y)'s oracle list holds a Gaussian whose alpha (float64) lies
+    within 1e-4 relative of the 1/255 skip threshold: hardware exp and libm expf
+    can then take opposite decisions, each worth up to colour/255 of the pixel."""
+    gx = (W + 15) // 16
+    t = (y // 16) * gx + x // 16
+    s, e = r["ranges"][t]
+    ids = r["point_list"][s:e]
+    m2, co = r["means2D"][ids].astype(np.float64), r["conic_opacity"][ids].astype(np.float64)
+    dx, dy = m2[:, 0] - x, m2[:, 1] - y
+    pw = -0.5 * (co[:, 0] * dx * dx + co[:, 2] * dy * dy) - co[:, 1] * dx * dy
+    al = np.minimum(0.99, co[:, 3] * np.exp(pw))
+    return bool(np.any(np.abs(al * 255.0 - 1.0) < 1e-4))
+
+
+def check_forward(h, r, rgb_from_sh=True, ncontrib_frac=0.999, flip_frac=0.0):
     H, W = h["final_T"].shape
     np.testing.assert_array_equal(h["radii"], r["radii"])
     vis = r["radii"] > 0
@@ -116,8 +131,18 @@ def check_forward(h, r, rgb_from_sh=True, ncontrib_frac=0.999):
     dbits = r["depths"].view(np.uint32)
     expect = np.lexsort((np.nonzero(vis)[0], dbits[vis]))
     np.testing.assert_array_equal(vis_order, np.nonzero(vis)[0][expect])
-    err = np.abs(h["color"] - r["color"]).max()
-    assert err <= IMG_TOL, f"image max abs err {err}"
+    perr = np.abs(h["color"] - r["color"]).max(axis=0)
+    err = perr.max()
+    if flip_frac > 0:
+        # large renders: a handful of pixels may sit on the alpha = 1/255 threshold
+        bad = np.argwhere(perr > IMG_TOL)
+        assert len(bad) <= flip_frac * perr.size, f"{len(bad)} pixels over {IMG_TOL}"
+        cmax = float(np.abs(r["rgb"]).max()) if rgb_from_sh else 1.0
+        assert err <= cmax / 255.0 + IMG_TOL, f"image max abs err {err}"
+        for y, x in bad:
+            assert alpha_flip_pixel(r, int(x), int(y), W), f"pixel ({x},{y}) err {perr[y, x]} unexplained"
+    else:
+        assert err <= IMG_TOL, f"image max abs err {err}"
     terr = np.abs(h["final_T"] - r["final_T"]).max()
     assert terr <= IMG_TOL, f"final_T max abs err {terr}"
     same = (last_contributor_ids(h, W, H) == last_contributor_ids(r, W, H)).mean()
@@ -323,11 +348,14 @@ def test_config_c_full_size_parity(dev, oracle):
 def test_config_e_full_size_forward_parity(dev, oracle):
     """Forward-only stress config E (5M Gaussians, 3840x2160, SH3; upstream would bin
     110M instances) against the oracle end to end: radii, depths, means2D, the depth
-    order and the tile lists bit-exact, image / final_T within 1e-4, last contributor."""
+    order and the tile lists bit-exact, final_T within 1e-4, the image within 1e-4
+    except on at most 1e-5 of the pixels, each of which must hold a Gaussian whose
+    alpha sits within 1e-4 relative of the 1/255 skip threshold (measured: 7 of
+    8.3M pixels, max 1.06e-3; hardware exp vs libm expf), last contributor."""
     cam, g = case(5_000_000, 3840, 2160, 3, seed=0)
     h = run_hip(cam, g, dev)
     r = run_oracle(oracle, cam, g)
-    check_forward(h, r)
+    check_forward(h, r, flip_frac=1e-5)
     # size-independent invariants: ranges tile the sorted list, depth order inside tiles
     pl, rg = h["point_list"], h["ranges"]
     assert rg[:, 1].max() == h["num_rendered"]

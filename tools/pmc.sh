@@ -6,7 +6,7 @@ TAG=${1:-pmc}
 OUT=/tmp/$TAG  # raw CSVs stay on the box; the summary returns
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --full-steps 0"
+CMD="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --full-steps 0 --render-steps 0 ${PMC_ARGS:-}"
 i=0
 for SET in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_THREAD_CYCLES_VALU" \
@@ -18,5 +18,5 @@ for SET in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_
   if [ $rc -ne 0 ]; then echo "pass $i failed rc=$rc"; tail -5 $OUT/p$i.log; exit $rc; fi
 done
 mkdir -p gpurun_out
-python3 tools/pmc_summary.py $OUT gpurun_out/${TAG}_pmc_summary.json > gpurun_out/${TAG}_pmc.txt
+python3 tools/pmc_summary.py $OUT gpurun_out/${TAG}_pmc_summary.json ${PMC_SUFFIX:-} > gpurun_out/${TAG}_pmc.txt
 cat gpurun_out/${TAG}_pmc.txt

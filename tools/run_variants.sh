@@ -15,7 +15,9 @@ for r in $(seq 1 $ROUNDS); do
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 s = d["stages_ms"]
-print(f"{sys.argv[1]:>10} {d['value']:8.2f}  " + " ".join(f"{k[:8]}={v * 1e3:.0f}" for k, v in s.items() if v))
+e = d.get("config_E_render") or {}
+es = " E %.1f fps (%s)" % (e["value"], " ".join(f"{k[:5]}={v * 1e3:.0f}" for k, v in e["stages_ms"].items())) if e else ""
+print(f"{sys.argv[1]:>10} {d['value']:8.2f}  " + " ".join(f"{k[:8]}={v * 1e3:.0f}" for k, v in s.items() if v) + es)
 PY
   done
 done
