@@ -107,11 +107,21 @@ __device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, 
 
 constexpr int PB_THREADS = 256;
 
-__device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh_row, float *dsh_row);
+// What the SH stage (after the rows reach LDS) needs from the geometry stage.
+struct ShStage {
+    f3 dmean;      // dL/dmean3D so far
+    float dRGB[3];  // clamp-masked colour gradient
+    bool vis;
+};
+__device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 mean, const float gin[7],
+                                       const float4 acc0, const float4 acc1, float accb, int32_t rad, uint32_t cl,
+                                       const Mat4 &V, const Mat4 &Pm);
 
-// One workgroup = PB_THREADS consecutive Gaussians.  SH rows are staged in LDS
-// (coalesced 16-B loads), each thread overwrites its row with dL/dSH, and the
-// rows are streamed back out coalesced.
+// One workgroup = PB_THREADS consecutive Gaussians.  Each thread loads its own
+// inputs first and the workgroup's SH rows after them, into registers: the rows
+// stay in flight while the geometry backward (cov2D, projection, cov3D) runs,
+// then go to LDS, where each thread turns its row into dL/dSH in place before
+// the rows stream back out coalesced.
 template <int RWC>
 __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PB_THREADS][3M + 1]
@@ -120,13 +130,57 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const int n = min(PB_THREADS, in.P - g0);
     const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
     const bool stage = in.sh != nullptr && a.o.dsh != nullptr && in.M > 0;
-    if (stage) {
-        rows_to_lds<PB_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
-        __syncthreads();
+    constexpr bool PREFETCH = RWC > 0 && RWC % 4 == 0;
+    const int idx = g0 + (int)threadIdx.x;
+    const bool live = idx < in.P;
+    const int li = live ? idx : in.P - 1;
+    // per-Gaussian inputs (issued before the rows: vmcnt counts in issue order)
+    const f3 mean = {in.means3D[3 * li], in.means3D[3 * li + 1], in.means3D[3 * li + 2]};
+    const Mat4 V = load_mat4(in.viewmatrix);
+    const Mat4 Pm = load_mat4(in.projmatrix);
+    float gin[7];  // scales + rotation, or the precomputed cov3D
+    if (in.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) gin[k] = in.cov3D_precomp[6 * (size_t)li + k];
+        gin[6] = 0.f;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) gin[k] = in.scales[3 * (size_t)li + k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) gin[3 + k] = in.rotations[4 * (size_t)li + k];
     }
-    if ((int)threadIdx.x < n) {
-        float *row = stage ? sh_lds + threadIdx.x * (RW + 1) : nullptr;
-        preprocess_bwd_one(a, g0 + threadIdx.x, row, row);
+    const float *acc = a.accum + (size_t)li * ACCUM_STRIDE;
+    const float4 acc0 = *reinterpret_cast<const float4 *>(acc);      // mean2D.x, mean2D.y, conic.x, conic.y
+    const float4 acc1 = *reinterpret_cast<const float4 *>(acc + 4);  // conic.w, opacity, color r, color g
+    const float accb = acc[8];                                       // color b
+    const int32_t rad = a.radii[li];
+    const uint32_t cl = a.clamped[li];
+    RowPrefetch<PB_THREADS, PREFETCH ? RWC : 4> pf;
+    if (PREFETCH)  // unconditional (a dummy load of element 0 without SH rows)
+        pf.load(stage ? in.sh : in.means3D, stage ? g0 : 0, stage ? n : 0);
+    else if (stage)
+        rows_to_lds<PB_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
+    // pin the per-Gaussian loads ahead of the rows (the compiler would otherwise
+    // sink them into the branch below, behind the rows, and wait for all of them)
+    asm volatile("" ::"v"(acc0.x), "v"(acc0.y), "v"(acc0.z), "v"(acc0.w), "v"(acc1.x), "v"(acc1.y), "v"(acc1.z),
+                 "v"(acc1.w), "v"(accb), "v"(rad), "v"(cl));
+    ShStage st{};
+    if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, rad, cl, V, Pm);
+    if (PREFETCH && stage) pf.store(n, sh_lds);
+    if (stage) __syncthreads();
+    if (live) {
+        f3 dmean = st.dmean;
+        if (stage) {
+            float *row = sh_lds + threadIdx.x * (RW + 1);
+            if (st.vis)
+                sh_backward(row, row, in.D, in.M, mean.x - in.campos[0], mean.y - in.campos[1],
+                            mean.z - in.campos[2], st.dRGB, dmean);
+            else
+                for (int k = 0; k < RW; k++) row[k] = 0.f;
+        }
+        a.o.dmeans3D[3 * (size_t)idx + 0] = dmean.x;
+        a.o.dmeans3D[3 * (size_t)idx + 1] = dmean.y;
+        a.o.dmeans3D[3 * (size_t)idx + 2] = dmean.z;
     }
     if (stage) {
         __syncthreads();
@@ -134,12 +188,14 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     }
 }
 
-__device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh_row, float *dsh_row) {
+__device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 mean, const float gin[7],
+                                       const float4 acc0, const float4 acc1, float accb, int32_t rad, uint32_t cl,
+                                       const Mat4 &V, const Mat4 &Pm) {
     const gsr_inputs &in = a.in;
     const BwdOutputs &o = a.o;
-    const bool vis = a.radii[idx] > 0;
-    float *dsh = dsh_row;  // LDS row (streamed to o.dsh by the caller) or nullptr
-    if (!vis) {
+    ShStage st{};
+    st.vis = rad > 0;
+    if (!st.vis) {
         for (int k = 0; k < 3; k++) {
             o.dmeans2D[3 * (size_t)idx + k] = 0.f;
             o.dcolors[3 * (size_t)idx + k] = 0.f;
@@ -150,32 +206,22 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
         for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = 0.f;
         if (o.drot)
             for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = 0.f;
-        if (dsh)
-            for (int k = 0; k < 3 * in.M; k++) dsh[k] = 0.f;
-        return;
+        return st;  // dmeans3D (zero) and the dsh row are written by the caller
     }
-    const float *acc = a.accum + (size_t)idx * ACCUM_STRIDE;
-    const float4 acc0 = *reinterpret_cast<const float4 *>(acc);      // mean2D.x, mean2D.y, conic.x, conic.y
-    const float4 acc1 = *reinterpret_cast<const float4 *>(acc + 4);  // conic.w, opacity, color r, color g
-    const float accb = acc[8];                                       // color b
     const float dcol[3] = {acc1.z, acc1.w, accb};
     o.dcolors[3 * (size_t)idx + 0] = dcol[0];
     o.dcolors[3 * (size_t)idx + 1] = dcol[1];
     o.dcolors[3 * (size_t)idx + 2] = dcol[2];
     o.dopacity[idx] = acc1.y;
 
-    const Mat4 V = load_mat4(in.viewmatrix);
-    const Mat4 Pm = load_mat4(in.projmatrix);
-    const f3 mean = {in.means3D[3 * idx], in.means3D[3 * idx + 1], in.means3D[3 * idx + 2]};
-
     // ---- 3D covariance (recomputed exactly as the forward did)
     float c3[6];
     float s[3] = {0, 0, 0}, q[4] = {0, 0, 0, 0};
     if (in.cov3D_precomp) {
-        for (int k = 0; k < 6; k++) c3[k] = in.cov3D_precomp[6 * (size_t)idx + k];
+        for (int k = 0; k < 6; k++) c3[k] = gin[k];
     } else {
-        for (int k = 0; k < 3; k++) s[k] = in.scales[3 * (size_t)idx + k];
-        for (int k = 0; k < 4; k++) q[k] = in.rotations[4 * (size_t)idx + k];
+        for (int k = 0; k < 3; k++) s[k] = gin[k];
+        for (int k = 0; k < 4; k++) q[k] = gin[3 + k];
         compute_cov3d(s[0], s[1], s[2], in.scale_modifier, q[0], q[1], q[2], q[3], c3);
     }
 
@@ -265,17 +311,14 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
     dmean.y += (pm[4] * m_w - pm[7] * mul1) * g2x + (pm[5] * m_w - pm[7] * mul2) * g2y;
     dmean.z += (pm[8] * m_w - pm[11] * mul1) * g2x + (pm[9] * m_w - pm[11] * mul2) * g2y;
 
-    // ---- SH backward (colour gradient masked where the forward clamped)
-    if (in.sh && dsh) {
-        const uint8_t cl = a.clamped[idx];
-        const float dRGB[3] = {dcol[0] * ((cl & 1) ? 0.f : 1.f), dcol[1] * ((cl & 2) ? 0.f : 1.f),
-                               dcol[2] * ((cl & 4) ? 0.f : 1.f)};
-        sh_backward(sh_row, dsh, in.D, in.M, mean.x - in.campos[0], mean.y - in.campos[1], mean.z - in.campos[2],
-                    dRGB, dmean);
+    // ---- SH backward (colour gradient masked where the forward clamped): the caller
+    // runs it once the row is in LDS, and writes dmeans3D
+    {
+        st.dRGB[0] = dcol[0] * ((cl & 1) ? 0.f : 1.f);
+        st.dRGB[1] = dcol[1] * ((cl & 2) ? 0.f : 1.f);
+        st.dRGB[2] = dcol[2] * ((cl & 4) ? 0.f : 1.f);
     }
-    o.dmeans3D[3 * (size_t)idx + 0] = dmean.x;
-    o.dmeans3D[3 * (size_t)idx + 1] = dmean.y;
-    o.dmeans3D[3 * (size_t)idx + 2] = dmean.z;
+    st.dmean = dmean;
 
     // ---- computeCov3D backward: dSigma -> dM = 2 M dSigma -> dscale, drot (q as given)
     if (in.scales && o.dscales && o.drot) {
@@ -316,6 +359,7 @@ __device__ void preprocess_bwd_one(const PreBwdArgs &a, int idx, const float *sh
         if (o.drot)
             for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = 0.f;
     }
+    return st;
 }
 
 hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, const void *geom, const float *accum,
