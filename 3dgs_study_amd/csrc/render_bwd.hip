@@ -44,18 +44,40 @@ __device__ unsigned long long g_bwd_stats[8];
 // Counting sort of the 4T quadrants by the number of Gaussians their forward wave
 // blended, descending (one workgroup: LDS histogram, scan, scatter).  Ties land in
 // any order; only the schedule depends on it, not a result.
+__device__ __forceinline__ uint32_t count_below(uint64_t m) {  // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 constexpr int ORDER_THREADS = 1024;
 constexpr int ORDER_BUCKETS = ORDER_THREADS;
+constexpr int ORDER_BATCH = 16;
 __device__ __forceinline__ int order_bucket(uint32_t work) {
     return ORDER_BUCKETS - 1 - (int)min(work, (uint32_t)ORDER_BUCKETS - 1);
 }
 __global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_t *qwork, int nq, uint32_t *order) {
     __shared__ uint32_t hist[ORDER_BUCKETS];
     __shared__ uint32_t wave_sum[ORDER_THREADS / 64];
-    const int t = threadIdx.x, lane = t & 63;
+    const int t = threadIdx.x, lane = t & 63, wbase = t & ~63;
     hist[t] = 0;
     __syncthreads();
-    for (int q = t; q < nq; q += ORDER_THREADS) atomicAdd(&hist[order_bucket(qwork[q])], 1u);
+    // Wave-uniform loops over batches of ORDER_BATCH independent loads per lane.
+    // Quadrants without work (about half of them: empty or early-saturated tiles)
+    // all share the last bucket: one LDS atomic per wave for them (ballot count +
+    // mbcnt ranks) instead of a 64-way same-address atomic.
+    for (int q0 = wbase; q0 < nq; q0 += ORDER_THREADS * ORDER_BATCH) {
+        uint32_t wv[ORDER_BATCH];
+#pragma unroll
+        for (int b = 0; b < ORDER_BATCH; b++) {
+            const int q = q0 + lane + b * ORDER_THREADS;
+            wv[b] = q < nq ? qwork[q] : 0u;
+        }
+#pragma unroll
+        for (int b = 0; b < ORDER_BATCH; b++) {
+            const bool valid = q0 + lane + b * ORDER_THREADS < nq;
+            const uint64_t zm = __ballot(valid && wv[b] == 0u);
+            if (valid && wv[b] != 0u) atomicAdd(&hist[order_bucket(wv[b])], 1u);
+            if (lane == 0 && zm) atomicAdd(&hist[ORDER_BUCKETS - 1], (uint32_t)__popcll(zm));
+        }
+    }
     __syncthreads();
     const uint32_t v = hist[t];
     uint32_t x = v;  // inclusive wave scan
@@ -70,7 +92,27 @@ __global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_
     for (int i = 0; i < (t >> 6); i++) base += wave_sum[i];
     hist[t] = base + x - v;  // exclusive start of bucket t
     __syncthreads();
-    for (int q = t; q < nq; q += ORDER_THREADS) order[atomicAdd(&hist[order_bucket(qwork[q])], 1u)] = (uint32_t)q;
+    for (int q0 = wbase; q0 < nq; q0 += ORDER_THREADS * ORDER_BATCH) {
+        uint32_t wv[ORDER_BATCH];
+#pragma unroll
+        for (int b = 0; b < ORDER_BATCH; b++) {
+            const int q = q0 + lane + b * ORDER_THREADS;
+            wv[b] = q < nq ? qwork[q] : 0u;
+        }
+#pragma unroll
+        for (int b = 0; b < ORDER_BATCH; b++) {
+            const int q = q0 + lane + b * ORDER_THREADS;
+            const bool valid = q < nq, zero = valid && wv[b] == 0u;
+            const uint64_t zm = __ballot(zero);
+            uint32_t zb = 0;
+            if (lane == 0 && zm) zb = atomicAdd(&hist[ORDER_BUCKETS - 1], (uint32_t)__popcll(zm));
+            zb = __shfl(zb, 0);
+            if (zero)
+                order[zb + count_below(zm)] = (uint32_t)q;
+            else if (valid)
+                order[atomicAdd(&hist[order_bucket(wv[b])], 1u)] = (uint32_t)q;
+        }
+    }
 }
 
 struct RenderBwdArgs {

@@ -7,4 +7,4 @@ mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/ -q -m gpu -p no:cacheprovider -x -k "not config_e" --timeout 200 \
     --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -2 gpurun_out/${TAG}_tests.log
-[ $# -gt 0 ] && ROUNDS=${ROUNDS:-2} bash tools/run_variants.sh "$@"
+if [ $# -gt 0 ]; then ROUNDS=${ROUNDS:-2} bash tools/run_variants.sh "$@"; fi
