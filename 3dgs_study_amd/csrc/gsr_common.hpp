@@ -140,7 +140,7 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H)
 struct ImgLayout {
     size_t off[GSR_IMG_NFIELDS];
     size_t qwork;   // uint32 [4T] Gaussians each 8x8 quadrant's forward wave blended (render_fwd.hip)
-    size_t qorder;  // uint32 [4T] quadrants, most forward work first (the backward's wave order)
+    size_t qorder;  // uint32 [<= 4T + 512] quadrants per XCD, most forward work first (the backward's wave order)
     size_t bytes;
 };
 __host__ __device__ inline ImgLayout img_layout(int W, int H) {
@@ -151,7 +151,7 @@ __host__ __device__ inline ImgLayout img_layout(int W, int H) {
     L.off[GSR_IMG_FINAL_T] = take((size_t)W * H * 4);
     L.off[GSR_IMG_N_CONTRIB] = take((size_t)W * H * 4);
     L.qwork = take((size_t)g.tiles * 16);
-    L.qorder = take((size_t)g.tiles * 16);
+    L.qorder = take((size_t)g.tiles * 16 + 8 * 64 * 4);  // padded per-XCD lists (render_bwd.hip)
     L.bytes = o;
     return L;
 }

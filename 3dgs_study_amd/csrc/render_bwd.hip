@@ -19,6 +19,8 @@
 // wave-instruction per Gaussian adds them to its 64-byte accumulator row: a
 // single memory-side atomic request (splitting it, e.g. one per 32-lane half,
 // doubled the kernel's time).
+#include <algorithm>
+
 #include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
 
@@ -34,35 +36,60 @@ __device__ unsigned long long g_bwd_stats[8];
 #define BWD_STAT(k, v) do { } while (0)
 #endif
 
-// Wave order: most forward work first (GSR_BWD_ORDER=1), so that the longest
-// replays start at once instead of forming the kernel's tail; 0 = the forward's
-// XCD strip order.
+// Wave order: per XCD, most forward work first (GSR_BWD_ORDER=1), so that the
+// longest replays start at once instead of forming the kernel's tail; 0 = the
+// forward's XCD strip order.
 #ifndef GSR_BWD_ORDER
 #define GSR_BWD_ORDER 1
 #endif
 
 // Counting sort of the 4T quadrants by the number of Gaussians their forward wave
-// blended, descending (one workgroup: LDS histogram, scan, scatter).  Ties land in
-// any order; only the schedule depends on it, not a result.
+// blended, descending, separately for each XCD: quadrant q keeps the XCD the
+// forward's strip order gave it (xcd_tile: strips of 16 quadrants dealt round-
+// robin), so each L2 still sees the same neighbouring tiles, and position
+// 8 r + x of the order (workgroup 8 r + x lands on XCD x, a speed hint only) is
+// XCD x's r-th heaviest quadrant; the shorter XCD lists are padded with
+// ORDER_NONE.  One workgroup: LDS histogram, scan, scatter.  Ties land in any
+// order; only the schedule depends on it, never a result.
+constexpr int ORDER_THREADS = 1024;
+constexpr int ORDER_WB = 1024;                  // work buckets per XCD
+constexpr int ORDER_NB = 8 * ORDER_WB;          // buckets
+constexpr int ORDER_PER_T = ORDER_NB / ORDER_THREADS;
+constexpr int ORDER_BATCH = 16;
+constexpr int ORDER_STRIP = 4 * XCD_STRIP;      // quadrants per strip (render_fwd.hip's blend_grid)
+constexpr uint32_t ORDER_NONE = 0xffffffffu;
+__device__ __forceinline__ int quad_xcd(int q) { return (q / ORDER_STRIP) & 7; }
+__device__ __forceinline__ int order_bucket(int q, uint32_t work) {
+    return quad_xcd(q) * ORDER_WB + ORDER_WB - 1 - (int)min(work, (uint32_t)ORDER_WB - 1);
+}
 __device__ __forceinline__ uint32_t count_below(uint64_t m) {  // set bits of m below this lane
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-constexpr int ORDER_THREADS = 1024;
-constexpr int ORDER_BUCKETS = ORDER_THREADS;
-constexpr int ORDER_BATCH = 16;
-__device__ __forceinline__ int order_bucket(uint32_t work) {
-    return ORDER_BUCKETS - 1 - (int)min(work, (uint32_t)ORDER_BUCKETS - 1);
+// host: the per-XCD list length the grid is padded to
+inline int order_max_per_xcd(int nq) {
+    int mx = 0;
+    for (int x = 0; x < 8; x++) {
+        int c = 0;
+        for (int q0 = x * ORDER_STRIP; q0 < nq; q0 += 8 * ORDER_STRIP) c += std::min(ORDER_STRIP, nq - q0);
+        mx = std::max(mx, c);
+    }
+    return mx;
 }
-__global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_t *qwork, int nq, uint32_t *order) {
-    __shared__ uint32_t hist[ORDER_BUCKETS];
+
+__global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_t *qwork, int nq, int maxc,
+                                                                   uint32_t *order) {
+    __shared__ uint32_t hist[ORDER_NB];
     __shared__ uint32_t wave_sum[ORDER_THREADS / 64];
+    __shared__ uint32_t seg[9];  // start of each XCD's buckets; seg[8] = nq
     const int t = threadIdx.x, lane = t & 63, wbase = t & ~63;
-    hist[t] = 0;
+#pragma unroll
+    for (int k = 0; k < ORDER_PER_T; k++) hist[k * ORDER_THREADS + t] = 0;
     __syncthreads();
     // Wave-uniform loops over batches of ORDER_BATCH independent loads per lane.
-    // Quadrants without work (about half of them: empty or early-saturated tiles)
-    // all share the last bucket: one LDS atomic per wave for them (ballot count +
-    // mbcnt ranks) instead of a 64-way same-address atomic.
+    // Quadrants without work (about half: empty or early-saturated tiles) share
+    // their XCD's last bucket; each 16-lane group (16 consecutive quadrants, one
+    // XCD) adds them with one LDS atomic (ballot count) instead of a same-address
+    // atomic per lane.
     for (int q0 = wbase; q0 < nq; q0 += ORDER_THREADS * ORDER_BATCH) {
         uint32_t wv[ORDER_BATCH];
 #pragma unroll
@@ -72,15 +99,23 @@ __global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_
         }
 #pragma unroll
         for (int b = 0; b < ORDER_BATCH; b++) {
-            const bool valid = q0 + lane + b * ORDER_THREADS < nq;
+            const int q = q0 + lane + b * ORDER_THREADS;
+            const bool valid = q < nq;
             const uint64_t zm = __ballot(valid && wv[b] == 0u);
-            if (valid && wv[b] != 0u) atomicAdd(&hist[order_bucket(wv[b])], 1u);
-            if (lane == 0 && zm) atomicAdd(&hist[ORDER_BUCKETS - 1], (uint32_t)__popcll(zm));
+            if (valid && wv[b] != 0u) atomicAdd(&hist[order_bucket(q, wv[b])], 1u);
+            const uint32_t gm = (uint32_t)(zm >> (lane & 48)) & 0xffffu;
+            if ((lane & 15) == 0 && gm) atomicAdd(&hist[order_bucket(q, 0u)], (uint32_t)__popc(gm));
         }
     }
     __syncthreads();
-    const uint32_t v = hist[t];
-    uint32_t x = v;  // inclusive wave scan
+    // exclusive scan of the buckets, ORDER_PER_T consecutive ones per thread
+    uint32_t v[ORDER_PER_T], sum = 0;
+#pragma unroll
+    for (int k = 0; k < ORDER_PER_T; k++) {
+        v[k] = hist[ORDER_PER_T * t + k];
+        sum += v[k];
+    }
+    uint32_t x = sum;  // inclusive wave scan
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o);
@@ -88,9 +123,15 @@ __global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_
     }
     if (lane == 63) wave_sum[t >> 6] = x;
     __syncthreads();
-    uint32_t base = 0;
-    for (int i = 0; i < (t >> 6); i++) base += wave_sum[i];
-    hist[t] = base + x - v;  // exclusive start of bucket t
+    uint32_t run = x - sum;
+    for (int i = 0; i < (t >> 6); i++) run += wave_sum[i];
+    if ((ORDER_PER_T * t) % ORDER_WB == 0) seg[ORDER_PER_T * t / ORDER_WB] = run;
+    if (t == 0) seg[8] = (uint32_t)nq;
+#pragma unroll
+    for (int k = 0; k < ORDER_PER_T; k++) {
+        hist[ORDER_PER_T * t + k] = run;
+        run += v[k];
+    }
     __syncthreads();
     for (int q0 = wbase; q0 < nq; q0 += ORDER_THREADS * ORDER_BATCH) {
         uint32_t wv[ORDER_BATCH];
@@ -104,14 +145,23 @@ __global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_
             const int q = q0 + lane + b * ORDER_THREADS;
             const bool valid = q < nq, zero = valid && wv[b] == 0u;
             const uint64_t zm = __ballot(zero);
+            const uint32_t gm = (uint32_t)(zm >> (lane & 48)) & 0xffffu;
             uint32_t zb = 0;
-            if (lane == 0 && zm) zb = atomicAdd(&hist[ORDER_BUCKETS - 1], (uint32_t)__popcll(zm));
-            zb = __shfl(zb, 0);
+            if ((lane & 15) == 0 && gm) zb = atomicAdd(&hist[order_bucket(q, 0u)], (uint32_t)__popc(gm));
+            zb = __shfl(zb, lane & 48);
+            const int xq = quad_xcd(q);
+            uint32_t pos = 0;
             if (zero)
-                order[zb + count_below(zm)] = (uint32_t)q;
+                pos = zb + (uint32_t)__popc(gm & ((1u << (lane & 15)) - 1u));
             else if (valid)
-                order[atomicAdd(&hist[order_bucket(wv[b])], 1u)] = (uint32_t)q;
+                pos = atomicAdd(&hist[order_bucket(q, wv[b])], 1u);
+            if (valid) order[8 * (pos - seg[xq]) + xq] = (uint32_t)q;
         }
+    }
+    // pad the shorter XCD lists
+    for (int i = t; i < 8 * maxc; i += ORDER_THREADS) {
+        const int xq = i & 7, r = i >> 3;
+        if (r >= (int)(seg[xq + 1] - seg[xq])) order[i] = ORDER_NONE;
     }
 }
 
@@ -159,6 +209,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
 #if GSR_BWD_ORDER
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
     const uint32_t quad = a.order[blockIdx.x];
+    if (quad == ORDER_NONE) return;
     const int tile = (int)(quad >> 2), w = (int)(quad & 3), lane = threadIdx.x & 63;
 #else
     const QuadSlot qs = quad_slot(a.tiles);
@@ -420,9 +471,10 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
 #if GSR_BWD_ORDER
     uint32_t *order = at<uint32_t>(const_cast<void *>(img), Im.qorder);
     a.order = order;
+    const int maxc = order_max_per_xcd(4 * g.tiles);
     hipLaunchKernelGGL(quad_order_kernel, dim3(1), dim3(ORDER_THREADS), 0, s, at<uint32_t>(img, Im.qwork), 4 * g.tiles,
-                       order);
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(4 * g.tiles), dim3(BLEND_THREADS), 0, s, a);
+                       maxc, order);
+    hipLaunchKernelGGL(render_bwd_kernel, dim3(8 * maxc), dim3(BLEND_THREADS), 0, s, a);
 #else
     a.order = nullptr;
     hipLaunchKernelGGL(render_bwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
