@@ -137,4 +137,29 @@ __host__ inline int blend_grid(int tiles) {
     return BLEND_WAVES == 4 ? xcd_grid(tiles) : xcd_grid<4 * XCD_STRIP>(4 * tiles);
 }
 
+// ---- backward wave order (render_fwd.hip fills it, render_bwd.hip reads it)
+// The backward starts each XCD's heaviest quadrants first.  A quadrant keeps the
+// XCD of the forward's strip order (xcd_tile: strips of ORDER_STRIP quadrants
+// dealt round-robin over the 8 XCDs), so each L2 sees the same neighbouring
+// tiles in both passes.  Each forward wave files its quadrant under
+// (XCD, work bucket) with one atomic; backward workgroup 8 r + x (XCD x under
+// round-robin placement: a speed hint only) takes XCD x's r-th entry in
+// bucket order.
+constexpr int ORDER_STRIP = 4 * XCD_STRIP;  // quadrants per strip
+constexpr int ORDER_NBUCKET = 32;           // work buckets per XCD, heaviest first
+__host__ __device__ inline int quad_xcd(int q) { return (q / ORDER_STRIP) & 7; }
+__device__ __forceinline__ int order_bucket(uint32_t work) {  // 16 blended Gaussians per bucket
+    return ORDER_NBUCKET - 1 - (int)min(work >> 4, (uint32_t)ORDER_NBUCKET - 1);
+}
+// quadrants per XCD list (the longest): the backward grid is 8 times this
+__host__ inline int order_max_per_xcd(int nq) {
+    int mx = 0;
+    for (int x = 0; x < 8; x++) {
+        int c = 0;
+        for (int q0 = x * ORDER_STRIP; q0 < nq; q0 += 8 * ORDER_STRIP) c += (nq - q0 < ORDER_STRIP) ? nq - q0 : ORDER_STRIP;
+        mx = c > mx ? c : mx;
+    }
+    return mx;
+}
+
 }  // namespace gsr

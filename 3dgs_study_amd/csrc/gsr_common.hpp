@@ -85,6 +85,7 @@ struct GeomLayout {
     size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, DSORT_ITEMS)]
     size_t dsort_totals;  // uint32 [RADIX]
     size_t emit_sums;     // uint32 [emit_blocks(P)] rank-order instance offsets per emit block
+    size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts (zeroed by preprocess)
     size_t bytes;
 };
 __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
@@ -110,6 +111,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_hist = take((size_t)RADIX * radix_blocks(P, DSORT_ITEMS) * 4);
     L.dsort_totals = take((size_t)RADIX * 4);
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
+    L.order_cnt = take(8 * 32 * 4);
     L.bytes = o;
     return L;
 }
@@ -139,8 +141,7 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H)
 
 struct ImgLayout {
     size_t off[GSR_IMG_NFIELDS];
-    size_t qwork;   // uint32 [4T] Gaussians each 8x8 quadrant's forward wave blended (render_fwd.hip)
-    size_t qorder;  // uint32 [<= 4T + 512] quadrants per XCD, most forward work first (the backward's wave order)
+    size_t qlist;   // uint32 [8][32][maxc] quadrants filed by XCD and forward work (gsr_blend.hpp)
     size_t bytes;
 };
 __host__ __device__ inline ImgLayout img_layout(int W, int H) {
@@ -150,8 +151,8 @@ __host__ __device__ inline ImgLayout img_layout(int W, int H) {
     auto take = [&](size_t b) { size_t r = o; o = align_up(o + b, 256); return r; };
     L.off[GSR_IMG_FINAL_T] = take((size_t)W * H * 4);
     L.off[GSR_IMG_N_CONTRIB] = take((size_t)W * H * 4);
-    L.qwork = take((size_t)g.tiles * 16);
-    L.qorder = take((size_t)g.tiles * 16 + 8 * 64 * 4);  // padded per-XCD lists (render_bwd.hip)
+    // per (XCD, bucket) room for every quadrant of the XCD (the longest list <= T / 2 + 16)
+    L.qlist = take((size_t)8 * 32 * ((size_t)g.tiles / 2 + 16) * 4);
     L.bytes = o;
     return L;
 }

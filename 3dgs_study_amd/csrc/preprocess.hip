@@ -32,6 +32,7 @@ struct PreArgs {
     int tiles;
     uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, key min, key max, 0}
     int32_t *radii;
+    uint32_t *order_cnt;
 };
 
 // SH -> RGB for one Gaussian, per channel (forward.cu computeColorFromSH).
@@ -208,6 +209,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     // (stores are counted by vmcnt too: issued here, after the geometry, they do not
     // hold up its waits for the per-Gaussian loads)
     for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
+    if (idx < 8 * ORDER_NBUCKET) a.order_cnt[idx] = 0u;  // the backward wave-order buckets (render_fwd.hip)
     // colour stage: the SH rows land in LDS now, after the geometry
     if (PREFETCH && use_sh) pf.store(n, sh_lds);
     if (use_sh) __syncthreads();
@@ -348,6 +350,7 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
     a.tiles = g.tiles;
     a.block_sums = at<uint4>(geom, L.block_sums);
     a.radii = radii;
+    a.order_cnt = at<uint32_t>(geom, L.order_cnt);
     const int nb = pre_blocks(in.P);
     const size_t lds = (in.sh && !in.colors_precomp) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     // SH row width as a compile-time constant for the common degrees (cheap LDS

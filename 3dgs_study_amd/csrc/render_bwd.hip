@@ -19,8 +19,6 @@
 // wave-instruction per Gaussian adds them to its 64-byte accumulator row: a
 // single memory-side atomic request (splitting it, e.g. one per 32-lane half,
 // doubled the kernel's time).
-#include <algorithm>
-
 #include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
 
@@ -36,138 +34,18 @@ __device__ unsigned long long g_bwd_stats[8];
 #define BWD_STAT(k, v) do { } while (0)
 #endif
 
-// Wave order: per XCD, most forward work first (GSR_BWD_ORDER=1), so that the
-// longest replays start at once instead of forming the kernel's tail; 0 = the
-// forward's XCD strip order.
+// Wave order: per XCD, most forward work first (GSR_BWD_ORDER=1; the buckets
+// the forward filed, gsr_blend.hpp), so that the longest replays start at once
+// instead of forming the kernel's tail; 0 = the forward's XCD strip order.
 #ifndef GSR_BWD_ORDER
 #define GSR_BWD_ORDER 1
 #endif
 
-// Counting sort of the 4T quadrants by the number of Gaussians their forward wave
-// blended, descending, separately for each XCD: quadrant q keeps the XCD the
-// forward's strip order gave it (xcd_tile: strips of 16 quadrants dealt round-
-// robin), so each L2 still sees the same neighbouring tiles, and position
-// 8 r + x of the order (workgroup 8 r + x lands on XCD x, a speed hint only) is
-// XCD x's r-th heaviest quadrant; the shorter XCD lists are padded with
-// ORDER_NONE.  One workgroup: LDS histogram, scan, scatter.  Ties land in any
-// order; only the schedule depends on it, never a result.
-constexpr int ORDER_THREADS = 1024;
-constexpr int ORDER_WB = 1024;                  // work buckets per XCD
-constexpr int ORDER_NB = 8 * ORDER_WB;          // buckets
-constexpr int ORDER_PER_T = ORDER_NB / ORDER_THREADS;
-constexpr int ORDER_BATCH = 16;
-constexpr int ORDER_STRIP = 4 * XCD_STRIP;      // quadrants per strip (render_fwd.hip's blend_grid)
-constexpr uint32_t ORDER_NONE = 0xffffffffu;
-__device__ __forceinline__ int quad_xcd(int q) { return (q / ORDER_STRIP) & 7; }
-__device__ __forceinline__ int order_bucket(int q, uint32_t work) {
-    return quad_xcd(q) * ORDER_WB + ORDER_WB - 1 - (int)min(work, (uint32_t)ORDER_WB - 1);
-}
-__device__ __forceinline__ uint32_t count_below(uint64_t m) {  // set bits of m below this lane
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-// host: the per-XCD list length the grid is padded to
-inline int order_max_per_xcd(int nq) {
-    int mx = 0;
-    for (int x = 0; x < 8; x++) {
-        int c = 0;
-        for (int q0 = x * ORDER_STRIP; q0 < nq; q0 += 8 * ORDER_STRIP) c += std::min(ORDER_STRIP, nq - q0);
-        mx = std::max(mx, c);
-    }
-    return mx;
-}
-
-__global__ void __launch_bounds__(ORDER_THREADS) quad_order_kernel(const uint32_t *qwork, int nq, int maxc,
-                                                                   uint32_t *order) {
-    __shared__ uint32_t hist[ORDER_NB];
-    __shared__ uint32_t wave_sum[ORDER_THREADS / 64];
-    __shared__ uint32_t seg[9];  // start of each XCD's buckets; seg[8] = nq
-    const int t = threadIdx.x, lane = t & 63, wbase = t & ~63;
-#pragma unroll
-    for (int k = 0; k < ORDER_PER_T; k++) hist[k * ORDER_THREADS + t] = 0;
-    __syncthreads();
-    // Wave-uniform loops over batches of ORDER_BATCH independent loads per lane.
-    // Quadrants without work (about half: empty or early-saturated tiles) share
-    // their XCD's last bucket; each 16-lane group (16 consecutive quadrants, one
-    // XCD) adds them with one LDS atomic (ballot count) instead of a same-address
-    // atomic per lane.
-    for (int q0 = wbase; q0 < nq; q0 += ORDER_THREADS * ORDER_BATCH) {
-        uint32_t wv[ORDER_BATCH];
-#pragma unroll
-        for (int b = 0; b < ORDER_BATCH; b++) {
-            const int q = q0 + lane + b * ORDER_THREADS;
-            wv[b] = q < nq ? qwork[q] : 0u;
-        }
-#pragma unroll
-        for (int b = 0; b < ORDER_BATCH; b++) {
-            const int q = q0 + lane + b * ORDER_THREADS;
-            const bool valid = q < nq;
-            const uint64_t zm = __ballot(valid && wv[b] == 0u);
-            if (valid && wv[b] != 0u) atomicAdd(&hist[order_bucket(q, wv[b])], 1u);
-            const uint32_t gm = (uint32_t)(zm >> (lane & 48)) & 0xffffu;
-            if ((lane & 15) == 0 && gm) atomicAdd(&hist[order_bucket(q, 0u)], (uint32_t)__popc(gm));
-        }
-    }
-    __syncthreads();
-    // exclusive scan of the buckets, ORDER_PER_T consecutive ones per thread
-    uint32_t v[ORDER_PER_T], sum = 0;
-#pragma unroll
-    for (int k = 0; k < ORDER_PER_T; k++) {
-        v[k] = hist[ORDER_PER_T * t + k];
-        sum += v[k];
-    }
-    uint32_t x = sum;  // inclusive wave scan
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        x += lane >= o ? y : 0u;
-    }
-    if (lane == 63) wave_sum[t >> 6] = x;
-    __syncthreads();
-    uint32_t run = x - sum;
-    for (int i = 0; i < (t >> 6); i++) run += wave_sum[i];
-    if ((ORDER_PER_T * t) % ORDER_WB == 0) seg[ORDER_PER_T * t / ORDER_WB] = run;
-    if (t == 0) seg[8] = (uint32_t)nq;
-#pragma unroll
-    for (int k = 0; k < ORDER_PER_T; k++) {
-        hist[ORDER_PER_T * t + k] = run;
-        run += v[k];
-    }
-    __syncthreads();
-    for (int q0 = wbase; q0 < nq; q0 += ORDER_THREADS * ORDER_BATCH) {
-        uint32_t wv[ORDER_BATCH];
-#pragma unroll
-        for (int b = 0; b < ORDER_BATCH; b++) {
-            const int q = q0 + lane + b * ORDER_THREADS;
-            wv[b] = q < nq ? qwork[q] : 0u;
-        }
-#pragma unroll
-        for (int b = 0; b < ORDER_BATCH; b++) {
-            const int q = q0 + lane + b * ORDER_THREADS;
-            const bool valid = q < nq, zero = valid && wv[b] == 0u;
-            const uint64_t zm = __ballot(zero);
-            const uint32_t gm = (uint32_t)(zm >> (lane & 48)) & 0xffffu;
-            uint32_t zb = 0;
-            if ((lane & 15) == 0 && gm) zb = atomicAdd(&hist[order_bucket(q, 0u)], (uint32_t)__popc(gm));
-            zb = __shfl(zb, lane & 48);
-            const int xq = quad_xcd(q);
-            uint32_t pos = 0;
-            if (zero)
-                pos = zb + (uint32_t)__popc(gm & ((1u << (lane & 15)) - 1u));
-            else if (valid)
-                pos = atomicAdd(&hist[order_bucket(q, wv[b])], 1u);
-            if (valid) order[8 * (pos - seg[xq]) + xq] = (uint32_t)q;
-        }
-    }
-    // pad the shorter XCD lists
-    for (int i = t; i < 8 * maxc; i += ORDER_THREADS) {
-        const int xq = i & 7, r = i >> 3;
-        if (r >= (int)(seg[xq + 1] - seg[xq])) order[i] = ORDER_NONE;
-    }
-}
-
 struct RenderBwdArgs {
     int W, H, gx, tiles;
-    const uint32_t *order;  // [4T] quadrant per workgroup (GSR_BWD_ORDER)
+    const uint32_t *order_cnt;  // [8][ORDER_NBUCKET] quadrants per (XCD, work bucket) (GSR_BWD_ORDER)
+    const uint32_t *qlist;      // [8][ORDER_NBUCKET][maxc]
+    int maxc;
     const uint2 *ranges;
     const uint32_t *point_list;
     const float4 *splats;
@@ -208,9 +86,20 @@ __device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
 __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs a) {
 #if GSR_BWD_ORDER
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
-    const uint32_t quad = a.order[blockIdx.x];
-    if (quad == ORDER_NONE) return;
-    const int tile = (int)(quad >> 2), w = (int)(quad & 3), lane = threadIdx.x & 63;
+    // workgroup 8 r + x: XCD x's r-th quadrant in bucket order (gsr_blend.hpp)
+    const int lane = threadIdx.x & 63;
+    uint32_t quad;
+    {
+        const int x = blockIdx.x & 7, rr = blockIdx.x >> 3;
+        const uint32_t c = lane < ORDER_NBUCKET ? a.order_cnt[x * ORDER_NBUCKET + lane] : 0u;
+        const uint32_t incl = wave_inclusive_scan(c);
+        const uint64_t past = __ballot(incl <= (uint32_t)rr);  // buckets wholly before entry rr
+        const int b = __builtin_popcountll(past);
+        if (b >= ORDER_NBUCKET) return;  // a shorter XCD list
+        const uint32_t start = (uint32_t)__shfl((int)(incl - c), b);
+        quad = a.qlist[(size_t)(x * ORDER_NBUCKET + b) * a.maxc + (rr - start)];
+    }
+    const int tile = (int)(quad >> 2), w = (int)(quad & 3);
 #else
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
@@ -469,14 +358,12 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.dL_dpix = dL_dpix;
     a.accum = accum;
 #if GSR_BWD_ORDER
-    uint32_t *order = at<uint32_t>(const_cast<void *>(img), Im.qorder);
-    a.order = order;
-    const int maxc = order_max_per_xcd(4 * g.tiles);
-    hipLaunchKernelGGL(quad_order_kernel, dim3(1), dim3(ORDER_THREADS), 0, s, at<uint32_t>(img, Im.qwork), 4 * g.tiles,
-                       maxc, order);
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(8 * maxc), dim3(BLEND_THREADS), 0, s, a);
+    a.order_cnt = at<uint32_t>(geom, G.order_cnt);
+    a.qlist = at<uint32_t>(img, Im.qlist);
+    a.maxc = order_max_per_xcd(4 * g.tiles);
+    hipLaunchKernelGGL(render_bwd_kernel, dim3(8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);
 #else
-    a.order = nullptr;
+    a.order_cnt = a.qlist = nullptr;
     hipLaunchKernelGGL(render_bwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
 #endif
     return hipGetLastError();

@@ -28,7 +28,9 @@ struct RenderFwdArgs {
     float *out_color;
     float *final_T;
     uint32_t *n_contrib;
-    uint32_t *qwork;  // [4T] Gaussians this quadrant blended: the backward's wave-order key
+    uint32_t *order_cnt;  // [8][ORDER_NBUCKET] (geom, zeroed by preprocess)
+    uint32_t *qlist;      // [8][ORDER_NBUCKET][maxc] (img)
+    int maxc;
 };
 
 #ifndef GSR_FWD_GROUP
@@ -138,7 +140,10 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
             if ((pos += 64) >= n) break;
         }
     }
-    if (lane == 0) a.qwork[4 * tile + w] = work;
+    if (lane == 0) {  // file this quadrant for the backward's wave order (gsr_blend.hpp)
+        const int q = 4 * tile + w, cell = quad_xcd(q) * ORDER_NBUCKET + order_bucket(work);
+        a.qlist[(size_t)cell * a.maxc + atomicAdd(&a.order_cnt[cell], 1u)] = (uint32_t)q;
+    }
     if (inside) {
         const size_t pix = (size_t)a.W * py + px;
         const size_t HW = (size_t)a.W * a.H;
@@ -167,7 +172,9 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
     a.out_color = out_color;
     a.final_T = at<float>(img, Im.off[GSR_IMG_FINAL_T]);
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
-    a.qwork = at<uint32_t>(img, Im.qwork);
+    a.order_cnt = at<uint32_t>(const_cast<void *>(geom), G.order_cnt);
+    a.qlist = at<uint32_t>(img, Im.qlist);
+    a.maxc = order_max_per_xcd(4 * g.tiles);
     hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
