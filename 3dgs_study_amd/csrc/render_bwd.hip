@@ -88,17 +88,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
     // workgroup 8 r + x: XCD x's r-th quadrant in bucket order (gsr_blend.hpp)
     const int lane = threadIdx.x & 63;
-    uint32_t quad;
-    {
-        const int x = blockIdx.x & 7, rr = blockIdx.x >> 3;
-        const uint32_t c = lane < ORDER_NBUCKET ? a.order_cnt[x * ORDER_NBUCKET + lane] : 0u;
-        const uint32_t incl = wave_inclusive_scan(c);
-        const uint64_t past = __ballot(incl <= (uint32_t)rr);  // buckets wholly before entry rr
-        const int b = __builtin_popcountll(past);
-        if (b >= ORDER_NBUCKET) return;  // a shorter XCD list
-        const uint32_t start = (uint32_t)__shfl((int)(incl - c), b);
-        quad = a.qlist[(size_t)(x * ORDER_NBUCKET + b) * a.maxc + (rr - start)];
-    }
+    const int quad = ordered_quad(a.order_cnt, a.qlist, a.maxc);
+    if (quad < 0) return;
     const int tile = (int)(quad >> 2), w = (int)(quad & 3);
 #else
     const QuadSlot qs = quad_slot(a.tiles);
