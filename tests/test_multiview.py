@@ -61,6 +61,41 @@ def test_grad_all_reduce_gloo_world2():
     assert nb == 5 * (3 + 3 + 45 + 1 + 3 + 4) * 4
 
 
+def _cpu_overlap_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    shapes = [(5, 3), (5, 1, 3), (5, 15, 3), (5, 1), (5, 3), (5, 4)]
+    params = [torch.randn(s, requires_grad=True) for s in shapes]
+    ar = GradAllReduce(params)  # hooks: each gradient's all-reduce starts inside backward
+    w = float(rank + 1)
+    loss = sum((w * (i + 1) * p * p).sum() for i, p in enumerate(params))
+    loss.backward()
+    pending = len(ar._works)
+    ar()
+    out[rank] = ([p.detach().clone() for p in params], [p.grad.clone() for p in params], pending)
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+def test_grad_all_reduce_overlapped_gloo_world2():
+    """Overlapped mode: the all-reduces launch from post-accumulate-grad hooks during
+    backward; after the wait every rank holds the sum of the ranks' gradients."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_cpu_overlap_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    p0, g0, n0 = res[0]
+    p1, g1, n1 = res[1]
+    assert n0 == n1 == 6  # one async all-reduce per parameter, launched during backward
+    for i, (a, b, p) in enumerate(zip(g0, g1, p0)):
+        assert torch.equal(a, b)
+        # d/dp sum_r (r+1)(i+1) p^2 = 2 p (i+1) (1 + 2)
+        torch.testing.assert_close(a, 2 * p * (i + 1) * 3.0)
+
+
 def _gpu_worker(rank, world, port, out):
     _init(rank, world, port)
     import synthetic
@@ -71,8 +106,10 @@ def _gpu_worker(rank, world, port, out):
     cam = synthetic.make_camera(160, 120, view=rank).to(dev)
     g = synthetic.make_gaussians(20_000, 3, seed=0).to(dev, requires_grad=True)
     target = synthetic.make_target(160, 120).to(dev)
+    reducer = GradAllReduce(g.params())  # overlapped: the all-reduces start inside backward
     train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
-    GradAllReduce(g.params())()
+    assert len(reducer._works) == 6
+    reducer()
     out[rank] = [p.grad.detach().cpu() for p in g.params()]
     dist.destroy_process_group()
 
