@@ -201,17 +201,17 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
     return step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s); }), "render", dbg, s);
 }
 
-int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning, const void *img,
-                 int64_t num_rendered, const float *dL_dout_color, void *accum, float *dmeans2D, float *dcolors,
-                 float *dopacity, float *dmeans3D, float *dcov3D, float *dsh, float *dscales, float *drot,
-                 void *stream) {
+static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                         const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                         float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
+                         float *drgb, float *dscales, float *drot, void *stream) {
     if (int rc = validate(in, false)) return rc;
     if (in->P == 0) return GSR_OK;
     if (!radii || !geom || !img || !accum || !dL_dout_color || (num_rendered > 0 && !binning))
         return fail(GSR_ERR_ARGS, "backward scratch/inputs are NULL");
     if (!dmeans2D || !dcolors || !dopacity || !dmeans3D || !dcov3D)
         return fail(GSR_ERR_ARGS, "backward outputs are NULL");
-    if (in->sh && in->M > 0 && !dsh) return fail(GSR_ERR_ARGS, "dsh is NULL");
+    if (in->sh && in->M > 0 && !dsh && !drgb) return fail(GSR_ERR_ARGS, "dsh is NULL");
     if (in->scales && (!dscales || !drot)) return fail(GSR_ERR_ARGS, "dscales/drot are NULL");
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
@@ -222,8 +222,41 @@ int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, c
                           "render backward", dbg, s))
             return rc;
     }
-    BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot};
+    BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot, drgb};
     return step(timed(GSR_STAGE_PREPROCESS_BWD, s, [&] { return launch_preprocess_bwd(*in, radii, geom, acc, o, s); }), "preprocess backward", dbg, s);
+}
+
+int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning, const void *img,
+                 int64_t num_rendered, const float *dL_dout_color, void *accum, float *dmeans2D, float *dcolors,
+                 float *dopacity, float *dmeans3D, float *dcov3D, float *dsh, float *dscales, float *drot,
+                 void *stream) {
+    return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
+                         dopacity, dmeans3D, dcov3D, dsh, nullptr, dscales, drot, stream);
+}
+
+int gsr_backward_colors(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                        const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *drgb,
+                        float *dscales, float *drot, void *stream) {
+    if (in && in->P > 0 && in->sh && in->M > 0 && !drgb) return fail(GSR_ERR_ARGS, "drgb is NULL");
+    if (in && in->sh && in->D > 3) return fail(GSR_ERR_ARGS, "sh_degree > 3 is not supported");
+    return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
+                         dopacity, dmeans3D, dcov3D, nullptr, drgb, dscales, drot, stream);
+}
+
+int64_t gsr_sh_record_floats(int32_t P) { return P < 0 ? -1 : 4 + (((int64_t)3 * P + 3) / 4) * 4; }
+
+int gsr_sh_grad_from_colors(int32_t P, int32_t M, int32_t nviews, const float *means3D, const float *records,
+                            float *dsh_dc, float *dsh_rest, void *stream) {
+    if (P < 0 || nviews < 0) return fail(GSR_ERR_ARGS, "sh_grad_from_colors: negative size");
+    if (M != 1 && M != 4 && M != 9 && M != 16) return fail(GSR_ERR_ARGS, "sh_grad_from_colors: M must be 1, 4, 9 or 16");
+    if (P == 0) return GSR_OK;
+    if (!means3D || !dsh_dc || (M > 1 && !dsh_rest) || (nviews > 0 && !records))
+        return fail(GSR_ERR_ARGS, "sh_grad_from_colors: NULL pointer");
+    hipStream_t s = (hipStream_t)stream;
+    return check_hip(launch_sh_grad_from_colors(P, M, nviews, gsr_sh_record_floats(P), means3D, records, dsh_dc,
+                                                dsh_rest, s),
+                     "sh_grad_from_colors");
 }
 
 int gsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,

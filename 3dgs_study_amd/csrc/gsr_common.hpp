@@ -196,6 +196,36 @@ __device__ constexpr float SH_C3_4 = -0.4570457994644658f;
 __device__ constexpr float SH_C3_5 = 1.445305721320277f;
 __device__ constexpr float SH_C3_6 = -0.5900435899266435f;
 
+// The SH basis at the unit direction (x, y, z) for degree <= 3 (coefficients
+// past (deg+1)^2 are left alone): dL/dsh[k][c] = b[k] * dL/dRGB[c] is the SH
+// part of backward.cu computeColorFromSH.  Shared by preprocess_bwd (one view)
+// and sh_exchange (the sum over views), so both form bit-identical products.
+__device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, float b[16]) {
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    b[0] = SH_C0;
+    if (deg > 0) {
+        b[1] = -SH_C1 * y;
+        b[2] = SH_C1 * z;
+        b[3] = -SH_C1 * x;
+        if (deg > 1) {
+            b[4] = SH_C2_0 * xy;
+            b[5] = SH_C2_1 * yz;
+            b[6] = SH_C2_2 * (2.f * zz - xx - yy);
+            b[7] = SH_C2_3 * xz;
+            b[8] = SH_C2_4 * (xx - yy);
+            if (deg > 2) {
+                b[9] = SH_C3_0 * y * (3.f * xx - yy);
+                b[10] = SH_C3_1 * xy * z;
+                b[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
+                b[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                b[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
+                b[14] = SH_C3_5 * z * (xx - yy);
+                b[15] = SH_C3_6 * x * (xx - 3.f * yy);
+            }
+        }
+    }
+}
+
 // 4x4 matrices arrive as 16 floats (row-major storage of the transposed
 // matrix); like upstream they are read column-major.
 struct Mat4 {

@@ -30,9 +30,14 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
 // preprocess_bwd.hip
 struct BwdOutputs {
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *dsh, *dscales, *drot;
+    float *drgb;  // instead of dsh: the clamp-masked colour gradient [P,3] (view-parallel exchange)
 };
 hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, const void *geom, const float *accum,
                                  const BwdOutputs &o, hipStream_t s);
+
+// sh_exchange.hip
+hipError_t launch_sh_grad_from_colors(int P, int M, int nviews, int64_t view_stride, const float *means3D,
+                                      const float *records, float *dsh_dc, float *dsh_rest, hipStream_t s);
 
 // train_ops.hip
 size_t l1_ssim_scratch_floats(int C, int H, int W);

@@ -63,31 +63,14 @@ __device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, 
         }
 #undef SH
     }
+    float b[16];
+    sh_basis(deg, x, y, z, b);
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         const float d = dRGB[c];
-        dsh[c] = SH_C0 * d;
-        if (deg > 0) {
-            dsh[3 * 1 + c] = (-SH_C1 * y) * d;
-            dsh[3 * 2 + c] = (SH_C1 * z) * d;
-            dsh[3 * 3 + c] = (-SH_C1 * x) * d;
-            if (deg > 1) {
-                dsh[3 * 4 + c] = (SH_C2_0 * xy) * d;
-                dsh[3 * 5 + c] = (SH_C2_1 * yz) * d;
-                dsh[3 * 6 + c] = (SH_C2_2 * (2.f * zz - xx - yy)) * d;
-                dsh[3 * 7 + c] = (SH_C2_3 * xz) * d;
-                dsh[3 * 8 + c] = (SH_C2_4 * (xx - yy)) * d;
-                if (deg > 2) {
-                    dsh[3 * 9 + c] = (SH_C3_0 * y * (3.f * xx - yy)) * d;
-                    dsh[3 * 10 + c] = (SH_C3_1 * xy * z) * d;
-                    dsh[3 * 11 + c] = (SH_C3_2 * y * (4.f * zz - xx - yy)) * d;
-                    dsh[3 * 12 + c] = (SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy)) * d;
-                    dsh[3 * 13 + c] = (SH_C3_4 * x * (4.f * zz - xx - yy)) * d;
-                    dsh[3 * 14 + c] = (SH_C3_5 * z * (xx - yy)) * d;
-                    dsh[3 * 15 + c] = (SH_C3_6 * x * (xx - 3.f * yy)) * d;
-                }
-            }
-        }
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (k < ncoef) dsh[3 * k + c] = b[k] * d;
     }
     for (int k = ncoef; k < M; k++) {
         dsh[3 * k + 0] = 0.f;
@@ -129,7 +112,9 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const int g0 = blockIdx.x * PB_THREADS;
     const int n = min(PB_THREADS, in.P - g0);
     const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
-    const bool stage = in.sh != nullptr && a.o.dsh != nullptr && in.M > 0;
+    // the rows are needed for dL/dmean3D's view-direction term even when the
+    // exchange takes the colour gradient instead of dsh
+    const bool stage = in.sh != nullptr && (a.o.dsh != nullptr || a.o.drgb != nullptr) && in.M > 0;
     constexpr bool PREFETCH = RWC > 0 && RWC % 4 == 0;
     const int idx = g0 + (int)threadIdx.x;
     const bool live = idx < in.P;
@@ -182,7 +167,7 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
         a.o.dmeans3D[3 * (size_t)idx + 1] = dmean.y;
         a.o.dmeans3D[3 * (size_t)idx + 2] = dmean.z;
     }
-    if (stage) {
+    if (stage && a.o.dsh) {
         __syncthreads();
         lds_to_rows<PB_THREADS, RWC>(sh_lds, g0, n, RW, a.o.dsh);
     }
@@ -203,6 +188,8 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
             if (o.dscales) o.dscales[3 * (size_t)idx + k] = 0.f;
         }
         o.dopacity[idx] = 0.f;
+        if (o.drgb)
+            for (int k = 0; k < 3; k++) o.drgb[3 * (size_t)idx + k] = 0.f;
         for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = 0.f;
         if (o.drot)
             for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = 0.f;
@@ -317,6 +304,8 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
         st.dRGB[0] = dcol[0] * ((cl & 1) ? 0.f : 1.f);
         st.dRGB[1] = dcol[1] * ((cl & 2) ? 0.f : 1.f);
         st.dRGB[2] = dcol[2] * ((cl & 4) ? 0.f : 1.f);
+        if (o.drgb)
+            for (int k = 0; k < 3; k++) o.drgb[3 * (size_t)idx + k] = st.dRGB[k];
     }
     st.dmean = dmean;
 
@@ -373,7 +362,7 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     a.clamped = at<uint8_t>(geom, G.off[GSR_GEOM_CLAMPED]);
     a.accum = accum;
     a.o = o;
-    const bool stage = in.sh && o.dsh && in.M > 0;
+    const bool stage = in.sh && (o.dsh || o.drgb) && in.M > 0;
     const size_t lds = stage ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     const dim3 grid((in.P + PB_THREADS - 1) / PB_THREADS);
     switch (3 * in.M) {  // see launch_preprocess

@@ -1,0 +1,102 @@
+// sh_exchange.hip — dL/dSH summed over views from the views' colour gradients.
+//
+// View-parallel training (3dgs_study_amd/multiview.py) needs
+// every rank to hold sum_v dL_v/dsh.  Per view, upstream's SH backward
+// (backward.cu computeColorFromSH) makes that gradient the outer product
+//     dL_v/dsh[k][c] = basis_k(dir_v) * dRGB_v[c],   dir_v = normalize(mean - campos_v)
+// with dRGB_v the clamp-masked colour gradient (zero for culled Gaussians).
+// So instead of all-reducing 12·M bytes per Gaussian (192 B at SH3: 76 % of
+// the gradient), the ranks all-gather the 12-byte dRGB_v of their views plus
+// each view's camera centre, and this kernel rebuilds the sum locally — the
+// same products as preprocess_bwd (shared sh_basis, fp contraction off), added
+// in view order, so every rank computes bit-identical gradients.
+//
+// records: nviews rows of view_stride floats:
+//   [campos.x, campos.y, campos.z, (float)sh_degree, dRGB [P][3], padding]
+// Outputs are the two leaf gradients of GaussianModel's SH storage
+// (scene/gaussian_model.py:106-110): dsh_dc [P,1,3] and dsh_rest [P,M-1,3].
+#pragma clang fp contract(off)
+
+#include "gsr_kernels.hpp"
+#include "gsr_math.hpp"
+#include "gsr_rows.hpp"
+
+namespace gsr {
+
+constexpr int SX_THREADS = 128;
+
+// One thread per Gaussian; 3·M sums in registers; the f_rest rows leave through
+// LDS (coalesced 16-B stores) like the SH rows of preprocess_bwd.
+template <int MC>
+__global__ void __launch_bounds__(SX_THREADS) sh_from_colors_kernel(int P, int nviews, int64_t stride,
+                                                                     const float *__restrict__ means3D,
+                                                                     const float *__restrict__ rec,
+                                                                     float *__restrict__ dsh_dc,
+                                                                     float *__restrict__ dsh_rest) {
+    constexpr int RW = 3 * (MC - 1);  // f_rest row width
+    __shared__ __attribute__((aligned(16))) float lds[RW > 0 ? SX_THREADS * (RW + 1) : 1];
+    const int g0 = blockIdx.x * SX_THREADS;
+    const int n = min(SX_THREADS, P - g0);
+    const int idx = g0 + (int)threadIdx.x;
+    const bool live = idx < P;
+    const int li = live ? idx : P - 1;
+    const float mx = means3D[3 * (size_t)li], my = means3D[3 * (size_t)li + 1], mz = means3D[3 * (size_t)li + 2];
+    float acc[3 * MC];
+#pragma unroll
+    for (int k = 0; k < 3 * MC; k++) acc[k] = 0.f;
+    for (int v = 0; v < nviews; v++) {
+        const float *r = rec + (size_t)v * (size_t)stride;
+        const int deg = (int)r[3];
+        const float *d3 = r + 4 + 3 * (size_t)li;
+        const float d[3] = {d3[0], d3[1], d3[2]};
+        const float ox = mx - r[0], oy = my - r[1], oz = mz - r[2];
+        const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
+        float b[16];
+        sh_basis(deg, ox / len, oy / len, oz / len, b);
+        const int ncoef = min((deg + 1) * (deg + 1), MC);
+#pragma unroll
+        for (int k = 0; k < MC; k++)
+            if (k < ncoef) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) acc[3 * k + c] += b[k] * d[c];
+            }
+    }
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) dsh_dc[3 * (size_t)idx + c] = acc[c];
+    }
+    if constexpr (RW > 0) {
+        float *row = lds + threadIdx.x * (RW + 1);
+#pragma unroll
+        for (int k = 0; k < RW; k++) row[k] = acc[3 + k];
+        __syncthreads();
+        lds_to_rows<SX_THREADS, RW>(lds, g0, n, RW, dsh_rest);
+    }
+}
+
+hipError_t launch_sh_grad_from_colors(int P, int M, int nviews, int64_t view_stride, const float *means3D,
+                                      const float *records, float *dsh_dc, float *dsh_rest, hipStream_t s) {
+    const dim3 grid((P + SX_THREADS - 1) / SX_THREADS);
+    switch (M) {
+        case 16:
+            hipLaunchKernelGGL(sh_from_colors_kernel<16>, grid, dim3(SX_THREADS), 0, s, P, nviews, view_stride,
+                               means3D, records, dsh_dc, dsh_rest);
+            break;
+        case 9:
+            hipLaunchKernelGGL(sh_from_colors_kernel<9>, grid, dim3(SX_THREADS), 0, s, P, nviews, view_stride,
+                               means3D, records, dsh_dc, dsh_rest);
+            break;
+        case 4:
+            hipLaunchKernelGGL(sh_from_colors_kernel<4>, grid, dim3(SX_THREADS), 0, s, P, nviews, view_stride,
+                               means3D, records, dsh_dc, dsh_rest);
+            break;
+        case 1:
+            hipLaunchKernelGGL(sh_from_colors_kernel<1>, grid, dim3(SX_THREADS), 0, s, P, nviews, view_stride,
+                               means3D, records, dsh_dc, dsh_rest);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace gsr

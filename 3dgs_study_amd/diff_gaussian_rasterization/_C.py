@@ -52,6 +52,7 @@ EXPORTED = (
     "gsr_timing_enable", "gsr_timing_read", "gsr_stage_name",
     "gsr_l1_ssim_scratch_bytes", "gsr_l1_ssim", "gsr_adam_step", "gsr_densify_stats",
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
+    "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors",
 )
 
 
@@ -62,7 +63,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 
@@ -98,6 +99,12 @@ def load_library():
     lib.gsr_forward_render.restype = ctypes.c_int
     lib.gsr_backward.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward.restype = ctypes.c_int
+    lib.gsr_backward_colors.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
+    lib.gsr_backward_colors.restype = ctypes.c_int
+    lib.gsr_sh_record_floats.argtypes = [i32]
+    lib.gsr_sh_record_floats.restype = i64
+    lib.gsr_sh_grad_from_colors.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
+    lib.gsr_sh_grad_from_colors.restype = ctypes.c_int
     lib.gsr_mark_visible.argtypes = [i32, vp, vp, vp, vp, vp]
     lib.gsr_mark_visible.restype = ctypes.c_int
     for name in ("gsr_geom_layout", "gsr_binning_layout", "gsr_img_layout"):
@@ -213,8 +220,13 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                  viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
-                                 geomBuffer, R, binningBuffer, imageBuffer, debug):
-    """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)"""
+                                 geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None):
+    """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)
+
+    ``drgb_out`` (not upstream; the view-parallel SH exchange, multiview.py): a
+    float32 device tensor of at least 3P elements.  When given, the library writes
+    the clamp-masked colour gradient [P,3] there (gsr_backward_colors) and the
+    returned ``dsh`` is None."""
     lib = load_library()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     s, keep, device, M = _inputs(background, means3D, colors, None, scales, rotations, scale_modifier, cov3D_precomp,
@@ -226,7 +238,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dopacity = torch.empty((P, 1), **f32)
     dmeans3D = torch.empty((P, 3), **f32)
     dcov3D = torch.empty((P, 6), **f32)
-    dsh = torch.empty((P, M, 3), **f32)
+    dsh = torch.empty((P, M, 3), **f32) if drgb_out is None else None
     dscales = torch.empty((P, 3), **f32)
     drot = torch.empty((P, 4), **f32)
     if P == 0:
@@ -234,13 +246,44 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     accum = torch.empty((lib.gsr_accum_bytes(P),), dtype=torch.uint8, device=device)
     grad = _prep(dL_dout_color, "dL_dout_color", device)
     radii = radii.contiguous()
-    _check(lib.gsr_backward(ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),
-                            binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
-                            int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), dcolors.data_ptr(),
-                            dopacity.data_ptr(), dmeans3D.data_ptr(), dcov3D.data_ptr(), _ptr(dsh),
-                            dscales.data_ptr(), drot.data_ptr(), _stream(device)),
+    if drgb_out is not None:
+        if (drgb_out.dtype != torch.float32 or drgb_out.device != device or not drgb_out.is_contiguous()
+                or drgb_out.numel() < 3 * P):
+            raise RuntimeError("drgb_out must be a contiguous float32 tensor of >= 3P elements on the input device")
+        fn, last = lib.gsr_backward_colors, drgb_out.data_ptr()
+    else:
+        fn, last = lib.gsr_backward, _ptr(dsh)
+    _check(fn(ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),
+              binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+              int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), dcolors.data_ptr(),
+              dopacity.data_ptr(), dmeans3D.data_ptr(), dcov3D.data_ptr(), last,
+              dscales.data_ptr(), drot.data_ptr(), _stream(device)),
            "rasterize_gaussians_backward")
     return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
+
+
+def sh_record_floats(P: int) -> int:
+    """Floats per view record of the SH exchange: [campos(3), degree, drgb(3P), pad]."""
+    return int(load_library().gsr_sh_record_floats(int(P)))
+
+
+def sh_grad_from_colors(means3D, records, nviews: int, dsh_dc, dsh_rest):
+    """dsh_dc [P,1,3], dsh_rest [P,M-1,3] <- sum over the nviews records of
+    basis(normalize(mean - campos_v)) (x) drgb_v (gsr_sh_grad_from_colors)."""
+    lib = load_library()
+    device = means3D.device
+    P = means3D.size(0)
+    M = dsh_dc.size(1) + (dsh_rest.size(1) if dsh_rest is not None else 0)
+    m = _prep(means3D, "means3D", device)
+    rec = _prep(records, "records", device)
+    if rec.numel() < nviews * sh_record_floats(P):
+        raise RuntimeError("sh_grad_from_colors: records hold fewer than nviews records")
+    for t, name in ((dsh_dc, "dsh_dc"), (dsh_rest, "dsh_rest")):
+        if t is not None and (not t.is_contiguous() or t.dtype != torch.float32 or t.device != device
+                              or t.size(0) != P):
+            raise RuntimeError(f"{name} must be a contiguous float32 [P,*,3] tensor on the input device")
+    _check(lib.gsr_sh_grad_from_colors(P, M, int(nviews), _ptr(m), _ptr(rec), _ptr(dsh_dc), _ptr(dsh_rest),
+                                       _stream(device)), "sh_grad_from_colors")
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

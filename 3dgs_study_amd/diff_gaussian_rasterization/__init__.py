@@ -17,6 +17,12 @@ Autograd: ``backward`` maps the 8 native gradients onto the 9 inputs
 cov3Ds_precomp, raster_settings)``; ``means2D.grad[:, :2]`` (NDC-scaled screen-space
 gradient) feeds densification at ``scene/gaussian_model.py:576-580``.
 
+View-parallel SH exchange (not upstream; ``3dgs_study_amd/multiview.py``): while a
+sink is installed with ``set_sh_grad_sink``, a backward with SH input hands the
+sink the view's colour gradient instead of returning dsh (the ``sh`` input then
+gets no gradient through autograd; the sink rebuilds the SH leaf gradients summed
+over all ranks' views).  ``set_sh_grad_sink(None)`` restores upstream behaviour.
+
 Debug mode (``raster_settings.debug``): the native side synchronises after every
 kernel; on failure a CPU copy of the arguments is written to
 ``snapshot_fw.dump`` / ``snapshot_bw.dump`` before the exception propagates.
@@ -30,7 +36,18 @@ import torch.nn as nn
 
 from . import _C
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians"]
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "set_sh_grad_sink"]
+
+_sh_grad_sink = None
+
+
+def set_sh_grad_sink(sink):
+    """Install (or with None remove) the view-parallel SH-gradient sink.  The sink
+    provides ``accepts(sh, means3D) -> bool``, ``record(P) -> float32 tensor`` of
+    ``_C.sh_record_floats(P)`` elements, and ``push(record, campos, sh_degree)``."""
+    global _sh_grad_sink
+    prev, _sh_grad_sink = _sh_grad_sink, sink
+    return prev
 
 
 def _cpu_snapshot(args):
@@ -73,8 +90,17 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree, rs.campos,
                 geom, ctx.num_rendered, binning, img, rs.debug)
-        (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales,
-         d_rotations) = _call_native(_C.rasterize_gaussians_backward, args, rs.debug, "snapshot_bw.dump", "backward")
+        sink = _sh_grad_sink
+        if sink is not None and sh.numel() > 0 and colors_precomp.numel() == 0 and sink.accepts(sh, means3D):
+            rec = sink.record(means3D.size(0))
+            (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
+                lambda *a: _C.rasterize_gaussians_backward(*a, drgb_out=rec[4:]), args, rs.debug,
+                "snapshot_bw.dump", "backward")
+            sink.push(rec, rs.campos, rs.sh_degree)
+        else:
+            (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales,
+             d_rotations) = _call_native(_C.rasterize_gaussians_backward, args, rs.debug, "snapshot_bw.dump",
+                                         "backward")
         return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
 
 

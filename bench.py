@@ -119,6 +119,9 @@ def main():
                     help="0 = L1-only headline unit; 0.2 = the reference's L1+SSIM loss")
     ap.add_argument("--full-steps", type=int, default=20,
                     help="timed iterations of the full train.py step (L1+SSIM, Adam), torch vs fused; 0 = skip")
+    ap.add_argument("--grad-exchange", default="sh-colour", choices=["sh-colour", "allreduce"],
+                    help="N>1: 'sh-colour' all-gathers per-view colour gradients for the SH block and all-reduces "
+                         "the rest (multiview.py); 'allreduce' all-reduces all 59 floats/Gaussian")
     ap.add_argument("--render-steps", type=int, default=20,
                     help="timed forward-only renders of config E (5M, 4K) reported beside the C line; 0 = skip")
     args = ap.parse_args()
@@ -152,14 +155,15 @@ def main():
     target = synthetic.make_target(W, H, seed=1).to(dev)
     bg = torch.zeros(3, device=dev)
     params = g.params()
-    reducer = GradAllReduce(params)
+    sh = (params[0], params[1], params[2]) if args.grad_exchange == "sh-colour" else None
+    reducer = GradAllReduce(params, sh=sh)  # exchange engages only when world > 1
 
     def one_step():
         for p in params:
             p.grad = None
         out = train_step.train_step(cam, g, target, bg, lambda_dssim=args.lambda_dssim)
         if world > 1:
-            reducer()  # one RCCL all-reduce of the flat 59-float/Gaussian gradient bucket
+            reducer()  # wait for the exchange started inside backward (+ rebuild the SH gradients)
         return out
 
     # Warm-up; its last steps carry events on every stage for the breakdown
@@ -221,8 +225,11 @@ def main():
                 "gaussians": P, "width": W, "height": H, "sh_degree": deg,
                 "num_rendered": I, "views_per_step": world,
                 "loss": "L1" if not args.lambda_dssim else f"L1+{args.lambda_dssim}*(1-SSIM)",
-                "parallelism": f"view-parallel x{world}" + (f", RCCL all-reduce {reducer.nbytes / 1e6:.0f} MB/step"
-                                                            if world > 1 else ""),
+                "parallelism": f"view-parallel x{world}" + (
+                    (f", RCCL all-gather of per-view colour-gradient records + all-reduce of xyz/opacity/scaling/"
+                     f"rotation, {reducer.nbytes / 1e6:.0f} MB sent per rank per step"
+                     if reducer.sh_exchange else f", RCCL all-reduce {reducer.nbytes / 1e6:.0f} MB/step")
+                    if world > 1 else ""),
             },
             "mpix_per_s": round(value * W * H / 1e6, 2),
             "stages_ms": {k: round(v[0], 4) for k, v in per_stage.items()},

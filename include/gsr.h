@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 3
+#define GSR_ABI_VERSION 4
 
 enum gsr_status {
     GSR_OK = 0,
@@ -111,6 +111,34 @@ int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, c
                  int64_t num_rendered, const float *dL_dout_color, void *accum, float *dmeans2D, float *dcolors,
                  float *dopacity, float *dmeans3D, float *dcov3D, float *dsh, float *dscales, float *drot,
                  void *stream);
+
+/* View-parallel exchange of the SH gradient (3dgs_study_amd/multiview.py;
+ * SURVEY.md §8e).  Upstream has no multi-GPU path; these two calls split
+ * backward.cu computeColorFromSH's dL/dsh = basis(dir) (x) dL/dRGB so that
+ * ranks exchange the 12-byte colour gradient per Gaussian and view instead of
+ * all-reducing the 12·M-byte dsh.
+ *
+ * gsr_backward_colors: gsr_backward, except that instead of dsh it writes drgb
+ * [P,3], the clamp-masked colour gradient (zero for culled Gaussians); dmeans3D
+ * still includes the view-direction term of the SH backward (sh is read).
+ * sh_degree must be <= 3.
+ *
+ * gsr_sh_record_floats(P): floats per view record = 4 + 3P rounded up to a
+ * multiple of 4.  A record is [campos.x, campos.y, campos.z, (float)sh_degree,
+ * drgb [P][3], padding]; drgb starts 16 B into the record.
+ *
+ * gsr_sh_grad_from_colors: dsh_dc [P,1,3] and dsh_rest [P,M-1,3] (the leaf
+ * gradients of GaussianModel._features_dc / _features_rest) = the sum over the
+ * nviews consecutive records of basis_v(normalize(mean - campos_v)) (x) drgb_v,
+ * added in record order with preprocess_bwd's exact products (M in {1,4,9,16};
+ * dsh_rest may be NULL when M = 1).  Outputs are overwritten. */
+int gsr_backward_colors(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                        const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *drgb,
+                        float *dscales, float *drot, void *stream);
+int64_t gsr_sh_record_floats(int32_t P);
+int gsr_sh_grad_from_colors(int32_t P, int32_t M, int32_t nviews, const float *means3D, const float *records,
+                            float *dsh_dc, float *dsh_rest, void *stream);
 
 /* Replaces markVisible (rasterize_points.cu) / checkFrustum:
  * present[i] = (viewmatrix * means3D[i]).z > 0.2.  present is [P] bytes. */

@@ -697,3 +697,25 @@ void oracle_sh_to_rgb(int P, int deg, int max_coeffs, const float *means, const 
 void oracle_cov3d(int P, const float *scales, float mod, const float *rotations, float *cov3D) {
     for (int idx = 0; idx < P; idx++) computeCov3D(scales + 3 * (size_t)idx, mod, rotations + 4 * (size_t)idx, cov3D + 6 * (size_t)idx);
 }
+
+/* View-parallel SH exchange (3dgs_study_amd/multiview.py; not upstream): the sum
+ * over views of backward.cu computeColorFromSH's dL/dsh for colour gradients
+ * that are already clamp-masked, added in view order.  dsh_sum [P][M][3]. */
+void oracle_sh_grad_sum(int P, int nviews, int M, const float *means, const float *campos, const int *degs,
+                        const float *drgb, float *dsh_sum) {
+    float *zeros_sh = (float *)calloc((size_t)P * M * 3, sizeof(float));
+    uint8_t *noclamp = (uint8_t *)calloc((size_t)P * 3, 1);
+    float *dmean = (float *)calloc((size_t)P * 3, sizeof(float));
+    float *dsh = (float *)calloc((size_t)P * M * 3, sizeof(float));
+    for (size_t i = 0; i < (size_t)P * M * 3; i++) dsh_sum[i] = 0.f;
+    for (int v = 0; v < nviews; v++) {
+        memset(dsh, 0, (size_t)P * M * 3 * sizeof(float));
+        for (int i = 0; i < P; i++)
+            sh_backward(i, degs[v], M, means, campos + 3 * v, zeros_sh, noclamp, drgb + (size_t)v * P * 3, dmean, dsh);
+        for (size_t i = 0; i < (size_t)P * M * 3; i++) dsh_sum[i] += dsh[i];
+    }
+    free(zeros_sh);
+    free(noclamp);
+    free(dmean);
+    free(dsh);
+}

@@ -208,6 +208,23 @@ def sh_to_rgb(means, campos, shs, deg):
     return rgb, clamped.astype(bool)
 
 
+def sh_grad_sum(means, campos, degs, drgb, M):
+    """Sum over views of backward.cu computeColorFromSH's dL/dsh for clamp-masked
+    colour gradients (the view-parallel SH exchange's contract, multiview.py):
+    campos [V,3], degs [V], drgb [V,P,3] -> dsh [P,M,3], added in view order."""
+    lib = _load()
+    means = _f32(means).reshape(-1, 3)
+    P = means.shape[0]
+    campos = _f32(campos).reshape(-1, 3)
+    V = campos.shape[0]
+    degs = np.ascontiguousarray(np.asarray(degs, np.int32).reshape(V))
+    drgb = _f32(drgb).reshape(V, P, 3)
+    out = np.zeros((P, M, 3), np.float32)
+    lib.oracle_sh_grad_sum(ctypes.c_int(P), ctypes.c_int(V), ctypes.c_int(M), _p(means), _p(campos), _p(degs),
+                           _p(drgb), _p(out))
+    return out
+
+
 def cov3d(scales, scale_modifier, rotations):
     """forward.cu computeCov3D on its own: [P,6] upper triangle."""
     lib = _load()

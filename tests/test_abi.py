@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 3
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 4
     # 10 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 40 + 11 * 8
     assert _C.GsrInputs.bg.offset == 40
@@ -94,6 +94,22 @@ def test_zero_gaussians_is_a_host_side_no_op(lib):
     assert n.value == 0
     assert lib.gsr_backward(ctypes.byref(s), None, None, None, None, 0, *([None] * 11)) == 0
     assert lib.gsr_mark_visible(0, None, None, None, None, None) == 0
+
+
+def test_sh_exchange_entry_points_validate(lib):
+    """gsr_backward_colors / gsr_sh_record_floats / gsr_sh_grad_from_colors: host-side
+    checks only (no device work without a GPU)."""
+    assert lib.gsr_sh_record_floats(0) == 4
+    assert lib.gsr_sh_record_floats(1) == 8 and lib.gsr_sh_record_floats(4) == 16
+    assert lib.gsr_sh_record_floats(1_000_000) == 3_000_004
+    assert lib.gsr_sh_record_floats(-1) == -1
+    assert lib.gsr_sh_grad_from_colors(10, 5, 1, None, None, None, None, None) != 0
+    assert "M must be" in lib.gsr_last_error().decode()
+    assert lib.gsr_sh_grad_from_colors(10, 16, 1, None, None, None, None, None) != 0
+    assert "NULL" in lib.gsr_last_error().decode()
+    assert lib.gsr_sh_grad_from_colors(0, 16, 1, None, None, None, None, None) == 0
+    s = _inputs(P=0)
+    assert lib.gsr_backward_colors(ctypes.byref(s), None, None, None, None, 0, *([None] * 11)) == 0
 
 
 def test_stage_names(lib):

@@ -96,7 +96,96 @@ def test_grad_all_reduce_overlapped_gloo_world2():
         torch.testing.assert_close(a, 2 * p * (i + 1) * 3.0)
 
 
-def _gpu_worker(rank, world, port, out):
+def _records_rebuild(oracle_mod, P, M):
+    """CPU stand-in for the HIP rebuild kernel (tests only): parse the gathered
+    records and sum the views' SH gradients with the C oracle."""
+    def rebuild(xyz, recs, nviews, dc, rest):
+        from diff_gaussian_rasterization import _C
+        stride = _C.sh_record_floats(P)
+        r = recs.reshape(nviews, stride).numpy()
+        dsh = oracle_mod.sh_grad_sum(xyz.numpy(), r[:, 0:3], r[:, 3].astype(np.int32), r[:, 4:4 + 3 * P], M)
+        dc.copy_(torch.from_numpy(dsh[:, :1]))
+        rest.copy_(torch.from_numpy(dsh[:, 1:]))
+    return rebuild
+
+
+def _sh_view(rank, P):
+    g = torch.Generator().manual_seed(100 + rank)
+    drgb = torch.randn(P, 3, generator=g)
+    drgb[::7] = 0.0  # culled / clamped entries
+    campos = torch.tensor([6.0 * np.cos(rank), 0.5 * rank, 6.0 * np.sin(rank)], dtype=torch.float32)
+    return drgb, campos
+
+
+def _cpu_sh_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+    from oracle import oracle as orc
+
+    P, M = 37, 16
+    torch.manual_seed(0)
+    shapes = [(P, 3), (P, 1, 3), (P, M - 1, 3), (P, 1), (P, 3), (P, 4)]
+    params = [torch.randn(s, requires_grad=True) for s in shapes]
+    ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), rebuild=_records_rebuild(orc, P, M))
+    for i in (0, 3, 4, 5):  # the all-reduced gradients, assigned by hand (flat mode)
+        params[i].grad = torch.full(shapes[i], float(rank + 1) * (i + 1))
+    drgb, campos = _sh_view(rank, P)
+    sh = torch.empty(P, M, 3)
+    assert ar.sh_exchange and ar.accepts(sh, params[0])
+    rec = ar.record(P)
+    rec[4:4 + 3 * P] = drgb.reshape(-1)  # what the rasterizer's backward writes
+    ar.push(rec, campos, 3)
+    ar()
+    out[rank] = ([p.grad.clone() for p in params], params[0].detach().clone(), ar.nbytes)
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+def test_sh_colour_exchange_gloo_world2(oracle):
+    """SH exchange: ranks gather (campos, colour gradient) records; every rank's
+    f_dc / f_rest gradients equal the oracle's sum over both views' SH gradients."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_cpu_sh_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    (g0, xyz, nb), (g1, _, _) = res[0], res[1]
+    P, M = 37, 16
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
+    for i in (0, 3, 4, 5):
+        assert torch.all(g0[i] == 3.0 * (i + 1))
+    views = [_sh_view(r, P) for r in (0, 1)]
+    ref = oracle.sh_grad_sum(xyz.numpy(), np.stack([v[1].numpy() for v in views]), [3, 3],
+                             np.stack([v[0].numpy() for v in views]), M)
+    assert np.array_equal(g0[1].numpy(), ref[:, :1]) and np.array_equal(g0[2].numpy(), ref[:, 1:])
+    assert np.abs(ref).sum() > 0
+    stride = 4 + ((3 * P + 3) // 4) * 4
+    assert nb == P * (3 + 1 + 3 + 4) * 4 + stride * 4
+
+
+def test_oracle_sh_grad_sum_matches_preprocess_backward(oracle):
+    """The oracle's per-view SH gradient sum equals upstream's SH backward run view by view."""
+    rng = np.random.default_rng(5)
+    P, M = 50, 16
+    means = rng.normal(size=(P, 3)).astype(np.float32)
+    campos = rng.normal(size=(2, 3)).astype(np.float32) * 5
+    drgb = rng.normal(size=(2, P, 3)).astype(np.float32)
+    got = oracle.sh_grad_sum(means, campos, [3, 1], drgb, M)
+    # degree 1 leaves coefficients 4..15 of that view untouched
+    one = [oracle.sh_grad_sum(means, campos[v:v + 1], [d], drgb[v:v + 1], M) for v, d in ((0, 3), (1, 1))]
+    assert np.array_equal(got, one[0] + one[1])
+    assert np.all(one[1][:, 4:] == 0)
+    # basis(dir) . dRGB contracted with sh = d(rgb)/d(sh) . dRGB: check via eval_sh linearity
+    shs = rng.normal(size=(P, M, 3)).astype(np.float32)
+    rgb0, cl = oracle.sh_to_rgb(means, campos[0], shs, 3)
+    lin = (one[0] * shs).sum(axis=1)  # sum_k basis_k sh[k][c] * drgb[c]
+    expect = (rgb0 - 0.5) * drgb[0]
+    ok = ~cl  # unclamped channels: rgb = basis . sh + 0.5
+    assert np.allclose(lin[ok], expect[ok], atol=1e-4)
+
+
+def _gpu_worker(rank, world, port, out, sh_exchange=False):
     _init(rank, world, port)
     import synthetic
     import train_step
@@ -106,23 +195,27 @@ def _gpu_worker(rank, world, port, out):
     cam = synthetic.make_camera(160, 120, view=rank).to(dev)
     g = synthetic.make_gaussians(20_000, 3, seed=0).to(dev, requires_grad=True)
     target = synthetic.make_target(160, 120).to(dev)
-    reducer = GradAllReduce(g.params())  # overlapped: the all-reduces start inside backward
+    params = g.params()
+    # overlapped: the all-reduces (and the SH record gather) start inside backward
+    reducer = GradAllReduce(params, sh=(params[0], params[1], params[2]) if sh_exchange else None)
     train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
-    assert len(reducer._works) == 6
+    assert len(reducer._works) == (4 if sh_exchange else 6)
+    assert len(reducer._gathers) == (1 if sh_exchange else 0)
     reducer()
     out[rank] = [p.grad.detach().cpu() for p in g.params()]
     dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-def test_view_parallel_grads_equal_sum_of_views(dev):
+@pytest.mark.parametrize("sh_exchange", [False, True], ids=["allreduce", "sh_colour_exchange"])
+def test_view_parallel_grads_equal_sum_of_views(dev, sh_exchange):
     import synthetic
     import train_step
 
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_gpu_worker, args=(2, port, out), nprocs=2, join=True)
+        mp.spawn(_gpu_worker, args=(2, port, out, sh_exchange), nprocs=2, join=True)
         res = dict(out)
     # single process: sum of the two views' gradients
     g = synthetic.make_gaussians(20_000, 3, seed=0).to(dev, requires_grad=True)
@@ -139,3 +232,105 @@ def test_view_parallel_grads_equal_sum_of_views(dev):
         assert torch.equal(a, b)  # replicas receive identical gradients
         rel = (a - ref).norm() / ref.norm().clamp_min(1e-30)
         assert rel < 1e-5, float(rel)
+
+
+@pytest.mark.gpu
+def test_sh_rebuild_bit_identical_to_preprocess_backward(dev):
+    """One native backward: rebuilding dsh from that call's colour gradient (masked by
+    the forward's clamp bits) through the HIP kernel gives preprocess_bwd's dsh bit
+    for bit (shared sh_basis products, no fp contraction)."""
+    import synthetic
+    from diff_gaussian_rasterization import _C
+
+    W, H, P = 200, 150, 30_000
+    cam = synthetic.make_camera(W, H, view=3).to(dev)
+    g = synthetic.make_gaussians(P, 3, seed=4).to(dev)
+    bg = torch.zeros(3, device=dev)
+    e = torch.empty(0, device=dev)
+    sh = g.get_features.contiguous()
+    tx, ty = float(np.tan(cam.FoVx * 0.5)), float(np.tan(cam.FoVy * 0.5))
+    fw = (bg, g.get_xyz, e, g.get_opacity, g.get_scaling, g.get_rotation, 1.0, e, cam.world_view_transform,
+          cam.full_proj_transform, tx, ty, H, W, sh, 3, cam.camera_center, False, False)
+    R, color, radii, geom, binning, img = _C.rasterize_gaussians(*fw)
+    dpix = torch.randn(3, H, W, device=dev, generator=torch.Generator(device=dev).manual_seed(2)) * 1e-3
+    bw = (bg, g.get_xyz, radii, e, g.get_scaling, g.get_rotation, 1.0, e, cam.world_view_transform,
+          cam.full_proj_transform, tx, ty, dpix, sh, 3, cam.camera_center, geom, R, binning, img,
+          False)
+    out = _C.rasterize_gaussians_backward(*bw)
+    dcolors, dsh = out[1], out[5]
+    off = _C.layouts(P, W, H, R)[0]["clamped"]
+    cl = geom[off:off + P].to(torch.int32)
+    bits = torch.stack([(cl >> c) & 1 for c in range(3)], dim=1)
+    drgb = dcolors * (1 - bits).to(torch.float32)
+    rec = torch.zeros(_C.sh_record_floats(P), device=dev)
+    rec[0:3] = cam.camera_center
+    rec[3] = 3
+    rec[4:4 + 3 * P] = drgb.reshape(-1)
+    dc = torch.empty(P, 1, 3, device=dev)
+    rest = torch.empty(P, 15, 3, device=dev)
+    _C.sh_grad_from_colors(g.get_xyz, rec, 1, dc, rest)
+    assert torch.equal(torch.cat([dc, rest], dim=1), dsh)
+    assert dsh.abs().sum() > 0
+    # the colours-only backward writes that same masked colour gradient
+    rec2 = torch.zeros_like(rec)
+    out2 = _C.rasterize_gaussians_backward(*bw, drgb_out=rec2[4:])
+    assert out2[5] is None
+    got = rec2[4:4 + 3 * P].view(P, 3)
+    rel = (got - drgb).norm() / drgb.norm()  # atomics order differs between the two backward calls
+    assert rel < 1e-5, float(rel)
+    assert torch.equal(got == 0, drgb == 0) or rel < 1e-6
+
+
+@pytest.mark.gpu
+def test_sh_exchange_single_rank_matches_plain_step(dev):
+    """One rank, exchange forced on, through autograd: no SH gradient flows through
+    autograd, and after the exchange every gradient matches the plain step (to the
+    atomics-order tolerance)."""
+    import synthetic
+    import train_step
+    from multiview import GradAllReduce
+
+    cam = synthetic.make_camera(200, 150, view=3).to(dev)
+    target = synthetic.make_target(200, 150).to(dev)
+    res = []
+    for force in (False, True):
+        g = synthetic.make_gaussians(30_000, 3, seed=4).to(dev, requires_grad=True)
+        params = g.params()
+        ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), sh_force=force)
+        assert ar.sh_exchange == force
+        train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
+        if force:
+            assert params[1].grad is None and params[2].grad is None  # no dsh through autograd
+        ar()
+        ar.remove_hooks()
+        res.append([p.grad.detach().cpu().clone() for p in params])
+    for i, (a, b) in enumerate(zip(*res)):
+        rel = (a - b).norm() / b.norm().clamp_min(1e-30)
+        assert rel < 1e-5, (i, float(rel))
+    assert res[0][2].abs().sum() > 0
+
+
+@pytest.mark.gpu
+def test_sh_grad_from_colors_kernel_vs_oracle(dev, oracle):
+    """The rebuild kernel over 5 records (mixed SH degrees, zero rows) against the
+    C oracle's view-ordered sum."""
+    from diff_gaussian_rasterization import _C
+
+    rng = np.random.default_rng(9)
+    P, V = 4_099, 5
+    for M in (16, 9, 4, 1):
+        means = rng.normal(size=(P, 3)).astype(np.float32)
+        campos = (rng.normal(size=(V, 3)) * 6).astype(np.float32)
+        degs = [min(d, int(np.sqrt(M)) - 1) for d in (3, 2, 0, 1, 3)]
+        drgb = rng.normal(size=(V, P, 3)).astype(np.float32)
+        drgb[:, ::11] = 0
+        stride = _C.sh_record_floats(P)
+        rec = np.zeros((V, stride), np.float32)
+        rec[:, :3], rec[:, 3], rec[:, 4:4 + 3 * P] = campos, degs, drgb.reshape(V, -1)
+        dc = torch.empty(P, 1, 3, device=dev)
+        rest = torch.empty(P, M - 1, 3, device=dev) if M > 1 else None
+        _C.sh_grad_from_colors(torch.from_numpy(means).to(dev), torch.from_numpy(rec).to(dev), V, dc, rest)
+        ref = oracle.sh_grad_sum(means, campos, degs, drgb, M)
+        got = dc.cpu().numpy() if rest is None else np.concatenate([dc.cpu().numpy(), rest.cpu().numpy()], axis=1)
+        err = np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30)
+        assert err <= 1e-6, (M, err)
