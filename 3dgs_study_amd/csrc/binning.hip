@@ -401,7 +401,7 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     const GeomLayout L = geom_layout(P, W, H);
     RadixPass a;
     a.n = (uint32_t)P;
-    a.NB = radix_blocks(P, DSORT_ITEMS);
+    a.NB = radix_blocks(P, dsort_items(P));
     a.hist = at<uint32_t>(geom, L.dsort_hist);
     a.totals = at<uint32_t>(geom, L.dsort_totals);
     const uint32_t *depth_bits = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTHS]);
@@ -431,6 +431,10 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     return a;
 }
 
+static hipError_t depth_radix_pass(int P, const RadixPass &a, hipStream_t s) {
+    return dsort_items(P) == DSORT_ITEMS_BIG ? radix_pass<DSORT_ITEMS_BIG>(a, s) : radix_pass<DSORT_ITEMS>(a, s);
+}
+
 static hipError_t launch_rank_offsets(int P, int W, int H, void *geom, hipStream_t s) {
     // rank-order exclusive offsets of the instances, per EMIT block
     const GeomLayout L = geom_layout(P, W, H);
@@ -447,7 +451,7 @@ static hipError_t launch_rank_offsets(int P, int W, int H, void *geom, hipStream
 // rare four-pass case the tail redoes the offsets after the fourth pass.
 hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
     for (int p = 0; p < 3; p++) {
-        hipError_t e = radix_pass<DSORT_ITEMS>(depth_pass(P, W, H, geom, p), s);
+        hipError_t e = depth_radix_pass(P, depth_pass(P, W, H, geom, p), s);
         if (e != hipSuccess) return e;
     }
     return launch_rank_offsets(P, W, H, geom, s);
@@ -455,7 +459,7 @@ hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
 
 hipError_t launch_depth_sort_tail(int P, int W, int H, void *geom, bool fourth_pass, hipStream_t s) {
     if (!fourth_pass) return hipSuccess;
-    hipError_t e = radix_pass<DSORT_ITEMS>(depth_pass(P, W, H, geom, 3), s);
+    hipError_t e = depth_radix_pass(P, depth_pass(P, W, H, geom, 3), s);
     if (e != hipSuccess) return e;
     return launch_rank_offsets(P, W, H, geom, s);
 }
@@ -491,7 +495,8 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
     int cur = npass & 1;
     RadixPass a;
     a.n = (uint32_t)I;
-    a.NB = radix_blocks(I, TSORT_ITEMS);
+    const int items = tsort_items(I);
+    a.NB = radix_blocks(I, items);
     a.gsrc = nullptr;
     a.gdst = nullptr;
     a.ctrl = nullptr;
@@ -510,7 +515,7 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
         a.shift = lo_bits;
         a.nbits = hi_bits - lo_bits;
         a.dmask = (1u << a.nbits) - 1u;
-        hipError_t e = radix_pass<TSORT_ITEMS>(a, s);
+        hipError_t e = items == TSORT_ITEMS_BIG ? radix_pass<TSORT_ITEMS_BIG>(a, s) : radix_pass<TSORT_ITEMS>(a, s);
         if (e != hipSuccess) return e;
         cur ^= 1;
     }

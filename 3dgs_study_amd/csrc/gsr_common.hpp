@@ -31,7 +31,19 @@ constexpr int RX_THREADS = 256;
 #define GSR_TSORT_ITEMS 8
 #endif
 constexpr int DSORT_ITEMS = GSR_DSORT_ITEMS;
+// The depth sort of many Gaussians (config E: 5M) likewise takes 8 items per
+// thread: 285 -> 256 us at E; 1M (config C) is unchanged either way.
+constexpr int DSORT_ITEMS_BIG = 8;
+constexpr int DSORT_BIG_N = 2 << 20;
+__host__ __device__ inline int dsort_items(int P) { return P > DSORT_BIG_N ? DSORT_ITEMS_BIG : DSORT_ITEMS; }
 constexpr int TSORT_ITEMS = GSR_TSORT_ITEMS;
+// Long instance lists (config E: 60M) sort in bigger radix blocks: longer
+// contiguous per-digit output runs and half the blocks for the digit scan
+// (tile sort 875 -> 730 us at E); short ones (config C: 4.9M) keep more
+// workgroups in flight (8 items: 85 us vs 91 us with 16).
+constexpr int TSORT_ITEMS_BIG = 16;
+constexpr int64_t TSORT_BIG_N = 16 << 20;
+__host__ __device__ inline int tsort_items(int64_t n) { return n > TSORT_BIG_N ? TSORT_ITEMS_BIG : TSORT_ITEMS; }
 constexpr int EMIT_BLOCK = 256;  // Gaussians per rank-order emit workgroup
 constexpr int PRE_THREADS = 256;          // preprocess block (scan granule)
 
@@ -82,7 +94,7 @@ struct GeomLayout {
     size_t dsort_keys_b;
     size_t dsort_vals_b;
     size_t dsort_vals_c;
-    size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, DSORT_ITEMS)]
+    size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, dsort_items(P))]
     size_t dsort_totals;  // uint32 [RADIX]
     size_t emit_sums;     // uint32 [emit_blocks(P)] rank-order instance offsets per emit block
     size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts (zeroed by preprocess)
@@ -108,7 +120,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_keys_b = take((size_t)P * 4);
     L.dsort_vals_b = take((size_t)P * 4);
     L.dsort_vals_c = take((size_t)P * 4);
-    L.dsort_hist = take((size_t)RADIX * radix_blocks(P, DSORT_ITEMS) * 4);
+    L.dsort_hist = take((size_t)RADIX * radix_blocks(P, dsort_items(P)) * 4);
     L.dsort_totals = take((size_t)RADIX * 4);
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
     L.order_cnt = take(8 * 32 * 4);
@@ -120,7 +132,7 @@ struct BinningLayout {
     size_t off[GSR_BIN_NFIELDS];
     size_t keys_b;  // uint32 [I] tile-sort ping-pong
     size_t vals_b;  // uint32 [I]
-    size_t hist;    // uint32 [RADIX][radix_blocks(I, TSORT_ITEMS)]
+    size_t hist;    // uint32 [RADIX][radix_blocks(I, tsort_items(I))]
     size_t totals;  // uint32 [RADIX]
     size_t bytes;
 };
@@ -133,7 +145,7 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H)
     L.off[GSR_BIN_POINT_LIST] = take(n * 4);
     L.keys_b = take(n * 4);
     L.vals_b = take(n * 4);
-    L.hist = take((size_t)RADIX * radix_blocks((int64_t)n, TSORT_ITEMS) * 4);
+    L.hist = take((size_t)RADIX * radix_blocks((int64_t)n, tsort_items((int64_t)n)) * 4);
     L.totals = take((size_t)RADIX * 4);
     L.bytes = o;
     return L;

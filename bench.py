@@ -139,10 +139,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+    # GSR_DIST_BACKEND=gloo rehearses the N>1 path with ranks sharing the visible
+    # GPUs (a 1-GPU box); the measured configuration is "nccl" (RCCL over xGMI),
+    # one rank per GPU
+    backend = os.environ.get("GSR_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     if not synthetic.CONFIGS[args.config]["backward"]:
         render_main(args, dev, world, rank)
@@ -207,6 +213,7 @@ def main():
         ab = algorithmic_bytes(dom, P, I, W, H, M)
         achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         traffic = pmc_traffic(dom)
+        coll = "RCCL" if backend == "nccl" else backend
         line = {
             "metric": "train iters/sec (fwd+bwd) + Mpix/sec, 1080p, 1M Gaussians @1/2/4/8 GPU",
             "value": round(value, 3),
@@ -226,10 +233,11 @@ def main():
                 "num_rendered": I, "views_per_step": world,
                 "loss": "L1" if not args.lambda_dssim else f"L1+{args.lambda_dssim}*(1-SSIM)",
                 "parallelism": f"view-parallel x{world}" + (
-                    (f", RCCL all-gather of per-view colour-gradient records + all-reduce of xyz/opacity/scaling/"
+                    (f", {coll} all-gather of per-view colour-gradient records + all-reduce of xyz/opacity/scaling/"
                      f"rotation, {reducer.nbytes / 1e6:.0f} MB sent per rank per step"
-                     if reducer.sh_exchange else f", RCCL all-reduce {reducer.nbytes / 1e6:.0f} MB/step")
+                     if reducer.sh_exchange else f", {coll} all-reduce {reducer.nbytes / 1e6:.0f} MB/step")
                     if world > 1 else ""),
+                **({"collective_backend": backend} if world > 1 else {}),
             },
             "mpix_per_s": round(value * W * H / 1e6, 2),
             "stages_ms": {k: round(v[0], 4) for k, v in per_stage.items()},
