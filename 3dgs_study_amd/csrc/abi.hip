@@ -204,7 +204,7 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
 static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
                          const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
                          float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
-                         float *drgb, float *dscales, float *drot, void *stream) {
+                         float *drgb, float *dscales, float *drot, void *stream, int dsh_planar = 0) {
     if (int rc = validate(in, false)) return rc;
     if (in->P == 0) return GSR_OK;
     if (!radii || !geom || !img || !accum || !dL_dout_color || (num_rendered > 0 && !binning))
@@ -222,7 +222,7 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
                           "render backward", dbg, s))
             return rc;
     }
-    BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot, drgb};
+    BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot, drgb, dsh_planar};
     return step(timed(GSR_STAGE_PREPROCESS_BWD, s, [&] { return launch_preprocess_bwd(*in, radii, geom, acc, o, s); }), "preprocess backward", dbg, s);
 }
 
@@ -232,6 +232,14 @@ int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, c
                  void *stream) {
     return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
                          dopacity, dmeans3D, dcov3D, dsh, nullptr, dscales, drot, stream);
+}
+
+int gsr_backward_planar(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                        const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
+                        float *dscales, float *drot, void *stream) {
+    return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
+                         dopacity, dmeans3D, dcov3D, dsh, nullptr, dscales, drot, stream, 1);
 }
 
 int gsr_backward_colors(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,

@@ -31,6 +31,7 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
 struct BwdOutputs {
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *dsh, *dscales, *drot;
     float *drgb;  // instead of dsh: the clamp-masked colour gradient [P,3] (view-parallel exchange)
+    int dsh_planar;  // dsh laid out [M][P][3] (coefficient planes) instead of [P][M][3]
 };
 hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, const void *geom, const float *accum,
                                  const BwdOutputs &o, hipStream_t s);

@@ -129,4 +129,36 @@ __device__ inline void lds_to_rows(const float *lds, int g0, int n, int RW_, flo
     }
 }
 
+
+// The reverse into M coefficient planes: LDS rows (stride RW + 1, RW = 3M) of
+// Gaussians [g0, g0 + n) -> plane k = dst + k * plane_stride, floats
+// [3 g0, 3 (g0 + n)) of each, i.e. dL/dsh laid out [M][P][3] (the tensor
+// [P,M,3] with strides (3, 3P, 1); diff_gaussian_rasterization hands that view
+// to autograd so the SH cat backward's f_dc slice needs no copy).  16-B stores
+// when the planes are 16-B aligned.
+template <int THREADS>
+__device__ inline void lds_to_planes(const float *lds, int g0, int n, int M, size_t plane_stride,
+                                     float *__restrict__ dst) {
+    const int RW1 = 3 * M + 1;
+    const int cnt = 3 * n;
+    const bool vec = (plane_stride & 3) == 0 && ((uintptr_t)dst & 15u) == 0;  // 3 g0 is a multiple of 4
+    auto at_e = [&](int e, int k) {
+        const int g = (int)(((uint32_t)e * 43691u) >> 17);  // e / 3 for e < 98304
+        return lds[g * RW1 + 3 * k + (e - 3 * g)];
+    };
+    for (int k = 0; k < M; k++) {
+        float *base = dst + (size_t)k * plane_stride + (size_t)g0 * 3;
+        int e0 = 0;
+        if (vec) {
+            const int n4 = cnt >> 2;
+            for (int i = threadIdx.x; i < n4; i += THREADS) {
+                const int e = i << 2;
+                reinterpret_cast<float4 *>(base)[i] = make_float4(at_e(e, k), at_e(e + 1, k), at_e(e + 2, k), at_e(e + 3, k));
+            }
+            e0 = n4 << 2;
+        }
+        for (int e = e0 + threadIdx.x; e < cnt; e += THREADS) base[e] = at_e(e, k);
+    }
+}
+
 }  // namespace gsr

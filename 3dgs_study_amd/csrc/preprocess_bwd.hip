@@ -169,7 +169,10 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     }
     if (stage && a.o.dsh) {
         __syncthreads();
-        lds_to_rows<PB_THREADS, RWC>(sh_lds, g0, n, RW, a.o.dsh);
+        if (a.o.dsh_planar)
+            lds_to_planes<PB_THREADS>(sh_lds, g0, n, in.M, (size_t)3 * in.P, a.o.dsh);
+        else
+            lds_to_rows<PB_THREADS, RWC>(sh_lds, g0, n, RW, a.o.dsh);
     }
 }
 

@@ -52,7 +52,7 @@ EXPORTED = (
     "gsr_timing_enable", "gsr_timing_read", "gsr_stage_name",
     "gsr_l1_ssim_scratch_bytes", "gsr_l1_ssim", "gsr_adam_step", "gsr_densify_stats",
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
-    "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors",
+    "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
 )
 
 
@@ -99,6 +99,8 @@ def load_library():
     lib.gsr_forward_render.restype = ctypes.c_int
     lib.gsr_backward.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward.restype = ctypes.c_int
+    lib.gsr_backward_planar.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
+    lib.gsr_backward_planar.restype = ctypes.c_int
     lib.gsr_backward_colors.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward_colors.restype = ctypes.c_int
     lib.gsr_sh_record_floats.argtypes = [i32]
@@ -220,13 +222,15 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                  viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
-                                 geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None):
+                                 geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None, dsh_planar=False):
     """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)
 
-    ``drgb_out`` (not upstream; the view-parallel SH exchange, multiview.py): a
-    float32 device tensor of at least 3P elements.  When given, the library writes
-    the clamp-masked colour gradient [P,3] there (gsr_backward_colors) and the
-    returned ``dsh`` is None."""
+    Not upstream (keyword-only extensions; the defaults are upstream's behaviour):
+    ``drgb_out`` — the view-parallel SH exchange (multiview.py): a float32 device
+    tensor of at least 3P elements; the library writes the clamp-masked colour
+    gradient [P,3] there (gsr_backward_colors) and the returned ``dsh`` is None.
+    ``dsh_planar`` — dsh is the [P,M,3] view of [M,P,3] coefficient planes
+    (strides (3, 3P, 1); gsr_backward_planar), same values."""
     lib = load_library()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     s, keep, device, M = _inputs(background, means3D, colors, None, scales, rotations, scale_modifier, cov3D_precomp,
@@ -238,7 +242,12 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dopacity = torch.empty((P, 1), **f32)
     dmeans3D = torch.empty((P, 3), **f32)
     dcov3D = torch.empty((P, 6), **f32)
-    dsh = torch.empty((P, M, 3), **f32) if drgb_out is None else None
+    if drgb_out is not None:
+        dsh = None
+    elif dsh_planar:
+        dsh = torch.empty((M, P, 3), **f32).permute(1, 0, 2)
+    else:
+        dsh = torch.empty((P, M, 3), **f32)
     dscales = torch.empty((P, 3), **f32)
     drot = torch.empty((P, 4), **f32)
     if P == 0:
@@ -251,6 +260,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                 or drgb_out.numel() < 3 * P):
             raise RuntimeError("drgb_out must be a contiguous float32 tensor of >= 3P elements on the input device")
         fn, last = lib.gsr_backward_colors, drgb_out.data_ptr()
+    elif dsh_planar and M > 0 and P > 0:
+        fn, last = lib.gsr_backward_planar, dsh.data_ptr()
     else:
         fn, last = lib.gsr_backward, _ptr(dsh)
     _check(fn(ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),

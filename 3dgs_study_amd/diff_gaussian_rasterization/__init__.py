@@ -98,9 +98,12 @@ class _RasterizeGaussians(torch.autograd.Function):
                 "snapshot_bw.dump", "backward")
             sink.push(rec, rs.campos, rs.sh_degree)
         else:
-            (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales,
-             d_rotations) = _call_native(_C.rasterize_gaussians_backward, args, rs.debug, "snapshot_bw.dump",
-                                         "backward")
+            # dsh as the [P,M,3] view of coefficient planes: the reference's SH cat
+            # backward (get_features) then slices an f_dc gradient that already has
+            # _features_dc's layout, and AccumulateGrad keeps it without a copy
+            (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
+                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True), args, rs.debug, "snapshot_bw.dump",
+                "backward")
         return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
 
 

@@ -112,6 +112,17 @@ int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, c
                  float *dopacity, float *dmeans3D, float *dcov3D, float *dsh, float *dscales, float *drot,
                  void *stream);
 
+/* gsr_backward_planar: gsr_backward with dsh written as M coefficient planes
+ * [M][P][3] (plane k at dsh + 3 P k), i.e. the [P,M,3] tensor with strides
+ * (3, 3P, 1).  Not an upstream layout: the autograd wrapper returns that strided
+ * view, so the f_dc slice the reference's SH `cat` backward hands to
+ * AccumulateGrad is already laid out like _features_dc (no copy; scene/
+ * gaussian_model.py:106-110 get_features).  Values are gsr_backward's. */
+int gsr_backward_planar(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                        const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
+                        float *dscales, float *drot, void *stream);
+
 /* View-parallel exchange of the SH gradient (3dgs_study_amd/multiview.py;
  * SURVEY.md §8e).  Upstream has no multi-GPU path; these two calls split
  * backward.cu computeColorFromSH's dL/dsh = basis(dir) (x) dL/dRGB so that

@@ -35,7 +35,7 @@ def activated(g, python_branch=False, scale_modifier=1.0):
 
 
 def run_hip(cam, g, dev, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=None, python_branch=False,
-            dL=None, debug=False):
+            dL=None, debug=False, dsh_planar=False):
     from diff_gaussian_rasterization import _C
 
     a = activated(g, python_branch, scale_modifier)
@@ -57,7 +57,11 @@ def run_hip(cam, g, dev, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=
         bargs = (bg_t, args[1], radii, colors, args[4], args[5], float(scale_modifier), args[7], args[8], args[9],
                  args[10], args[11], g_, shs, g.active_sh_degree, args[16], geom, I, binning, img, debug)
         names = ("dmeans2D", "dcolors", "dopacity", "dmeans3D", "dcov3D", "dsh", "dscales", "drot")
-        grads = _C.rasterize_gaussians_backward(*bargs)
+        grads = _C.rasterize_gaussians_backward(*bargs, dsh_planar=dsh_planar)
+        if dsh_planar and shs.numel():
+            M = shs.size(1)
+            assert grads[5].shape == shs.shape and grads[5].stride() == (3, 3 * shs.size(0), 1), grads[5].stride()
+            assert grads[5].permute(1, 0, 2).is_contiguous() and M == grads[5].size(1)
         torch.cuda.synchronize()
         out["grads"] = {n: x.cpu().numpy() for n, x in zip(names, grads)}
     return out

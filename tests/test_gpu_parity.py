@@ -165,12 +165,16 @@ def check_backward(h, rb, tol=GRAD_TOL, names=("dmeans2D", "dcolors", "dopacity"
 @pytest.mark.parametrize("cfg", [
     dict(P=10_000, W=256, H=256, deg=0, view=0),                  # config A
     dict(P=20_000, W=333, H=201, deg=3, view=3, active=2),        # ragged image, D < max degree
+    dict(P=20_003, W=160, H=120, deg=3, view=5),                  # P % 4 != 0: unaligned coefficient planes
     dict(P=100_000, W=800, H=800, deg=3, view=0),                 # config B
 ])
-def test_forward_backward_parity(dev, oracle, cfg):
+@pytest.mark.parametrize("planar", [False, True], ids=["dsh_rows", "dsh_planes"])
+def test_forward_backward_parity(dev, oracle, cfg, planar):
+    """planar: dsh as coefficient planes (gsr_backward_planar, the autograd path's
+    layout); P = 20,003 leaves the planes unaligned (scalar stores)."""
     cam, g = case(cfg["P"], cfg["W"], cfg["H"], cfg["deg"], seed=1, view=cfg["view"], active=cfg.get("active"))
     dL = random_dL(cfg["H"], cfg["W"])
-    h = run_hip(cam, g, dev, dL=dL)
+    h = run_hip(cam, g, dev, dL=dL, dsh_planar=planar)
     r = run_oracle(oracle, cam, g)
     check_forward(h, r)
     rb = oracle.backward(r, dL)

@@ -56,13 +56,18 @@ class OracleC:
 
     def rasterize_gaussians_backward(self, bg, means3D, radii, colors, scales, rotations, scale_modifier,
                                      cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh,
-                                     degree, campos, geomBuffer, R, binningBuffer, imageBuffer, debug):
+                                     degree, campos, geomBuffer, R, binningBuffer, imageBuffer, debug,
+                                     dsh_planar=False):
         self.calls.append("bwd")
         f = self.states[int(geomBuffer[0])]
         assert R == f["num_rendered"]
         b = self.o.backward(f, dL_dout_color.detach().cpu().numpy())
         self.last_grads = b
-        return tuple(torch.from_numpy(b[k]) for k in NAMES)
+        out = [torch.from_numpy(b[k]) for k in NAMES]
+        if dsh_planar:  # the library's coefficient-plane layout: same values, strides (3, 3P, 1)
+            i = NAMES.index("dsh")
+            out[i] = out[i].permute(1, 0, 2).contiguous().permute(1, 0, 2)
+        return tuple(out)
 
     def mark_visible(self, means3D, viewmatrix, projmatrix):
         return torch.from_numpy(self.o.mark_visible(self._np(means3D), self._np(viewmatrix)))
