@@ -204,7 +204,11 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
 static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
                          const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
                          float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
-                         float *drgb, float *dscales, float *drot, void *stream, int dsh_planar = 0) {
+                         float *drgb, float *dscales, float *drot, void *stream, int dsh_planar = 0,
+                         int phases = 3) {
+    // phases: bit 0 = accumulator memset + render_bwd (+ the colour gradient into
+    // drgb), bit 1 = preprocess_bwd.  The view-parallel exchange runs them as two
+    // calls and starts its all-gather of drgb in between.
     if (int rc = validate(in, false)) return rc;
     if (in->P == 0) return GSR_OK;
     if (!radii || !geom || !img || !accum || !dL_dout_color || (num_rendered > 0 && !binning))
@@ -216,13 +220,27 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
     float *acc = (float *)accum;
-    if (int rc = check_hip(hipMemsetAsync(acc, 0, gsr_accum_bytes(in->P), s), "accumulator memset")) return rc;
-    if (num_rendered > 0) {
-        if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, num_rendered, img, dL_dout_color, acc, s); }),
-                          "render backward", dbg, s))
-            return rc;
+    const bool colors = drgb && in->sh && in->M > 0;
+    if (phases & 1) {
+        if (int rc = check_hip(hipMemsetAsync(acc, 0, gsr_accum_bytes(in->P), s), "accumulator memset")) return rc;
+        if (num_rendered > 0) {
+            if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, num_rendered, img, dL_dout_color, acc, s); }),
+                              "render backward", dbg, s))
+                return rc;
+        }
+        if (colors) {
+            const GeomLayout G = geom_layout(in->P, in->W, in->H);
+            if (int rc = step(launch_colors_from_accum(in->P, radii, at<uint8_t>(const_cast<void *>(geom), G.off[GSR_GEOM_CLAMPED]),
+                                                       acc, drgb, s),
+                              "colour gradient", dbg, s))
+                return rc;
+        }
     }
-    BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot, drgb, dsh_planar};
+    if (!(phases & 2)) return GSR_OK;
+    // with the colour gradient taken by the exchange, preprocess_bwd still reads the
+    // SH rows for dL/dmean3D's view-direction term but writes no dsh
+    BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, colors ? nullptr : dsh, dscales, drot, nullptr,
+                 dsh_planar, colors ? 1 : 0};
     return step(timed(GSR_STAGE_PREPROCESS_BWD, s, [&] { return launch_preprocess_bwd(*in, radii, geom, acc, o, s); }), "preprocess backward", dbg, s);
 }
 
@@ -250,6 +268,32 @@ int gsr_backward_colors(const gsr_inputs *in, const int32_t *radii, const void *
     if (in && in->sh && in->D > 3) return fail(GSR_ERR_ARGS, "sh_degree > 3 is not supported");
     return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
                          dopacity, dmeans3D, dcov3D, nullptr, drgb, dscales, drot, stream);
+}
+
+static int colors_phase(int phases, const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                        const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *drgb,
+                        float *dscales, float *drot, void *stream) {
+    if (in && in->P > 0 && in->sh && in->M > 0 && !drgb) return fail(GSR_ERR_ARGS, "drgb is NULL");
+    if (in && in->sh && in->D > 3) return fail(GSR_ERR_ARGS, "sh_degree > 3 is not supported");
+    return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
+                         dopacity, dmeans3D, dcov3D, nullptr, drgb, dscales, drot, stream, 0, phases);
+}
+
+int gsr_backward_colors_render(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                               const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                               float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D,
+                               float *drgb, float *dscales, float *drot, void *stream) {
+    return colors_phase(1, in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
+                        dopacity, dmeans3D, dcov3D, drgb, dscales, drot, stream);
+}
+
+int gsr_backward_colors_finish(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                               const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                               float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D,
+                               float *drgb, float *dscales, float *drot, void *stream) {
+    return colors_phase(2, in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
+                        dopacity, dmeans3D, dcov3D, drgb, dscales, drot, stream);
 }
 
 int64_t gsr_sh_record_floats(int32_t P) { return P < 0 ? -1 : 4 + (((int64_t)3 * P + 3) / 4) * 4; }

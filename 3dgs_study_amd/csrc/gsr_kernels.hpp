@@ -32,11 +32,14 @@ struct BwdOutputs {
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *dsh, *dscales, *drot;
     float *drgb;  // instead of dsh: the clamp-masked colour gradient [P,3] (view-parallel exchange)
     int dsh_planar;  // dsh laid out [M][P][3] (coefficient planes) instead of [P][M][3]
+    int sh_dir;      // read the SH rows for dL/dmean3D's direction term although dsh and drgb are NULL
 };
 hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, const void *geom, const float *accum,
                                  const BwdOutputs &o, hipStream_t s);
 
 // sh_exchange.hip
+hipError_t launch_colors_from_accum(int P, const int32_t *radii, const uint8_t *clamped, const float *accum,
+                                    float *drgb, hipStream_t s);
 hipError_t launch_sh_grad_from_colors(int P, int M, int nviews, int64_t view_stride, const float *means3D,
                                       const float *records, float *dsh_dc, float *dsh_rest, hipStream_t s);
 

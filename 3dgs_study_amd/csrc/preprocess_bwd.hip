@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
     // the rows are needed for dL/dmean3D's view-direction term even when the
     // exchange takes the colour gradient instead of dsh
-    const bool stage = in.sh != nullptr && (a.o.dsh != nullptr || a.o.drgb != nullptr) && in.M > 0;
+    const bool stage = in.sh != nullptr && (a.o.dsh != nullptr || a.o.drgb != nullptr || a.o.sh_dir) && in.M > 0;
     constexpr bool PREFETCH = RWC > 0 && RWC % 4 == 0;
     const int idx = g0 + (int)threadIdx.x;
     const bool live = idx < in.P;
@@ -365,7 +365,7 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     a.clamped = at<uint8_t>(geom, G.off[GSR_GEOM_CLAMPED]);
     a.accum = accum;
     a.o = o;
-    const bool stage = in.sh && (o.dsh || o.drgb) && in.M > 0;
+    const bool stage = in.sh && (o.dsh || o.drgb || o.sh_dir) && in.M > 0;
     const size_t lds = stage ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     const dim3 grid((in.P + PB_THREADS - 1) / PB_THREADS);
     switch (3 * in.M) {  // see launch_preprocess

@@ -83,7 +83,12 @@ __device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
-__global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs a) {
+#ifdef GSR_BWD_WPE  // experiment: minimum waves per SIMD (caps the VGPR budget)
+#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_BWD_WPE)))
+#else
+#define GSR_BWD_ATTR
+#endif
+__global__ void __launch_bounds__(BLEND_THREADS) GSR_BWD_ATTR render_bwd_kernel(RenderBwdArgs a) {
 #if GSR_BWD_ORDER
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
     // workgroup 8 r + x: XCD x's r-th quadrant in bucket order (gsr_blend.hpp)

@@ -74,6 +74,30 @@ __global__ void __launch_bounds__(SX_THREADS) sh_from_colors_kernel(int P, int n
     }
 }
 
+// The clamp-masked colour gradient of one view straight from render_bwd's
+// accumulator rows (dcolor at floats 6..8), before preprocess_bwd runs, so the
+// exchange can start while preprocess_bwd computes: preprocess_bwd's own masking
+// (dcol * (clamped ? 0 : 1), zero for culled Gaussians), bit for bit.
+__global__ void __launch_bounds__(256) colors_from_accum_kernel(int P, const int32_t *__restrict__ radii,
+                                                                const uint8_t *__restrict__ clamped,
+                                                                const float *__restrict__ accum,
+                                                                float *__restrict__ drgb) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    const bool vis = radii[i] > 0;
+    const uint32_t cl = clamped[i];
+    const float *row = accum + (size_t)i * ACCUM_STRIDE;
+#pragma unroll
+    for (int c = 0; c < 3; c++) drgb[3 * (size_t)i + c] = vis ? row[6 + c] * ((cl >> c) & 1u ? 0.f : 1.f) : 0.f;
+}
+
+hipError_t launch_colors_from_accum(int P, const int32_t *radii, const uint8_t *clamped, const float *accum,
+                                    float *drgb, hipStream_t s) {
+    hipLaunchKernelGGL(colors_from_accum_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, radii, clamped, accum,
+                       drgb);
+    return hipGetLastError();
+}
+
 hipError_t launch_sh_grad_from_colors(int P, int M, int nviews, int64_t view_stride, const float *means3D,
                                       const float *records, float *dsh_dc, float *dsh_rest, hipStream_t s) {
     const dim3 grid((P + SX_THREADS - 1) / SX_THREADS);

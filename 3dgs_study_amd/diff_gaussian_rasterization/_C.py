@@ -53,6 +53,7 @@ EXPORTED = (
     "gsr_l1_ssim_scratch_bytes", "gsr_l1_ssim", "gsr_adam_step", "gsr_densify_stats",
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
+    "gsr_backward_colors_render", "gsr_backward_colors_finish",
 )
 
 
@@ -101,8 +102,9 @@ def load_library():
     lib.gsr_backward.restype = ctypes.c_int
     lib.gsr_backward_planar.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward_planar.restype = ctypes.c_int
-    lib.gsr_backward_colors.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
-    lib.gsr_backward_colors.restype = ctypes.c_int
+    for name in ("gsr_backward_colors", "gsr_backward_colors_render", "gsr_backward_colors_finish"):
+        getattr(lib, name).argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
+        getattr(lib, name).restype = ctypes.c_int
     lib.gsr_sh_record_floats.argtypes = [i32]
     lib.gsr_sh_record_floats.restype = i64
     lib.gsr_sh_grad_from_colors.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
@@ -222,7 +224,8 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                  viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
-                                 geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None, dsh_planar=False):
+                                 geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None, dsh_planar=False,
+                                 on_drgb=None):
     """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)
 
     Not upstream (keyword-only extensions; the defaults are upstream's behaviour):
@@ -230,7 +233,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     tensor of at least 3P elements; the library writes the clamp-masked colour
     gradient [P,3] there (gsr_backward_colors) and the returned ``dsh`` is None.
     ``dsh_planar`` — dsh is the [P,M,3] view of [M,P,3] coefficient planes
-    (strides (3, 3P, 1); gsr_backward_planar), same values."""
+    (strides (3, 3P, 1); gsr_backward_planar), same values.
+    ``on_drgb`` (with ``drgb_out``) — called once drgb is queued on the stream and
+    before the per-Gaussian backward is (gsr_backward_colors_render / _finish), so
+    the caller can start exchanging drgb under it."""
     lib = load_library()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     s, keep, device, M = _inputs(background, means3D, colors, None, scales, rotations, scale_modifier, cov3D_precomp,
@@ -264,12 +270,17 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         fn, last = lib.gsr_backward_planar, dsh.data_ptr()
     else:
         fn, last = lib.gsr_backward, _ptr(dsh)
-    _check(fn(ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),
-              binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
-              int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), dcolors.data_ptr(),
-              dopacity.data_ptr(), dmeans3D.data_ptr(), dcov3D.data_ptr(), last,
-              dscales.data_ptr(), drot.data_ptr(), _stream(device)),
-           "rasterize_gaussians_backward")
+    call = lambda f: f(ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),  # noqa: E731
+                       binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+                       int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), dcolors.data_ptr(),
+                       dopacity.data_ptr(), dmeans3D.data_ptr(), dcov3D.data_ptr(), last,
+                       dscales.data_ptr(), drot.data_ptr(), _stream(device))
+    if drgb_out is not None and on_drgb is not None:
+        _check(call(lib.gsr_backward_colors_render), "rasterize_gaussians_backward")
+        on_drgb()
+        _check(call(lib.gsr_backward_colors_finish), "rasterize_gaussians_backward")
+    else:
+        _check(call(fn), "rasterize_gaussians_backward")
     return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
 
 

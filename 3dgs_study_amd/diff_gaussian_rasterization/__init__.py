@@ -93,10 +93,12 @@ class _RasterizeGaussians(torch.autograd.Function):
         sink = _sh_grad_sink
         if sink is not None and sh.numel() > 0 and colors_precomp.numel() == 0 and sink.accepts(sh, means3D):
             rec = sink.record(means3D.size(0))
+            # the record's exchange starts as soon as the colour gradient is queued,
+            # under the per-Gaussian backward
+            push = lambda: sink.push(rec, rs.campos, rs.sh_degree)  # noqa: E731
             (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
-                lambda *a: _C.rasterize_gaussians_backward(*a, drgb_out=rec[4:]), args, rs.debug,
+                lambda *a: _C.rasterize_gaussians_backward(*a, drgb_out=rec[4:], on_drgb=push), args, rs.debug,
                 "snapshot_bw.dump", "backward")
-            sink.push(rec, rs.campos, rs.sh_degree)
         else:
             # dsh as the [P,M,3] view of coefficient planes: the reference's SH cat
             # backward (get_features) then slices an f_dc gradient that already has

@@ -147,6 +147,18 @@ int gsr_backward_colors(const gsr_inputs *in, const int32_t *radii, const void *
                         const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
                         float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *drgb,
                         float *dscales, float *drot, void *stream);
+/* The two halves of gsr_backward_colors, so the caller can start exchanging
+ * drgb while the per-Gaussian backward runs: _render = accumulator memset,
+ * render backward and drgb; _finish = the per-Gaussian backward (same
+ * arguments, on the same stream, in that order). */
+int gsr_backward_colors_render(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                               const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                               float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D,
+                               float *drgb, float *dscales, float *drot, void *stream);
+int gsr_backward_colors_finish(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                               const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                               float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D,
+                               float *drgb, float *dscales, float *drot, void *stream);
 int64_t gsr_sh_record_floats(int32_t P);
 int gsr_sh_grad_from_colors(int32_t P, int32_t M, int32_t nviews, const float *means3D, const float *records,
                             float *dsh_dc, float *dsh_rest, void *stream);
