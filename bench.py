@@ -37,10 +37,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 WORKLOADS = {
     "C": "1M Gaussians, 1920x1080, SH deg 3, render->L1->backward, one view per GPU per step",
     "B": "100k Gaussians, 800x800, SH deg 3, render->L1->backward, one view per GPU per step",
-    "A": "10k Gaussians, 256x256, SH deg 0, render->L1->backward, one view per GPU per step",
+    "A": "10k Gaussians, 256x256, SH deg 0, render() forward only (no grad), one view per GPU per step",
     "E": "5M Gaussians, 3840x2160, SH deg 3, render() forward only (no grad), one view per GPU per step",
 }
 RENDER_METRIC = "render frames/sec (fwd-only) + Mpix/sec, 4K (3840x2160), 5M Gaussians, SH3"
+
+
+def render_metric(cfg_name: str) -> str:
+    """The forward-only metric of a config (E is BASELINE.json's; A is the CPU-plumbing case)."""
+    if cfg_name == "E":
+        return RENDER_METRIC
+    import synthetic
+    c = synthetic.CONFIGS[cfg_name]
+    return f"render frames/sec (fwd-only) + Mpix/sec, {c['W']}x{c['H']}, {c['P']} Gaussians, SH{c['sh_degree']}"
 
 
 def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, M: int) -> float:
@@ -306,7 +315,7 @@ def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0) -> 
     achieved = ab / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
     fps = steps / dt
     res = {
-        "metric": RENDER_METRIC, "value": round(fps, 3), "unit": "frames/s", "ms_per_frame": round(1e3 * dt / steps, 4),
+        "metric": render_metric(cfg_name), "value": round(fps, 3), "unit": "frames/s", "ms_per_frame": round(1e3 * dt / steps, 4),
         "mpix_per_s": round(fps * W * H / 1e6, 2), "steps": steps, "warmup": warmup,
         "config": {"workload": f"{cfg_name}: {WORKLOADS[cfg_name]}", "gaussians": P, "width": W, "height": H,
                    "sh_degree": deg, "num_rendered": I},
@@ -341,7 +350,7 @@ def render_main(args, dev, world: int, rank: int) -> None:
     if rank == 0:
         W, H = r["config"]["width"], r["config"]["height"]
         value = world * args.steps / elapsed
-        line = {"metric": RENDER_METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world,
+        line = {"metric": render_metric(args.config), "value": round(value, 3), "unit": "frames/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic (seeded Gaussians in a radius-2 ball, camera at distance 6, SURVEY.md §8d)",
