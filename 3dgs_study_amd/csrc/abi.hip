@@ -95,6 +95,8 @@ int validate(const gsr_inputs *in, bool forward) {
     if (in->W <= 0 || in->H <= 0) return fail(GSR_ERR_ARGS, "image size must be positive (got %dx%d)", in->W, in->H);
     if ((int64_t)in->W * in->H > (int64_t)1 << 30 || in->W > 65535 * TILE_X || in->H > 65535 * TILE_Y)
         return fail(GSR_ERR_CAPACITY, "image too large");
+    if (in->footprint != GSR_FOOTPRINT_RECT && in->footprint != GSR_FOOTPRINT_TIGHT)
+        return fail(GSR_ERR_ARGS, "footprint must be GSR_FOOTPRINT_RECT or GSR_FOOTPRINT_TIGHT (got %d)", in->footprint);
     if (in->P == 0) return GSR_OK;
     if (!in->means3D || !in->viewmatrix || !in->projmatrix || !in->bg || (forward && !in->opacities))
         return fail(GSR_ERR_ARGS, "missing required input (means3D/opacities/viewmatrix/projmatrix/bg)");
@@ -142,6 +144,15 @@ int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap) {
     int n = 0;
     for (; n < cap && n < GSR_IMG_NFIELDS; n++) offsets[n] = L.off[n];
     return n;
+}
+
+int gsr_point_list_keys(int32_t P, int32_t W, int32_t H, const void *geom, const void *binning,
+                        int64_t num_rendered, uint64_t *keys, void *stream) {
+    if (P < 0 || W <= 0 || H <= 0 || num_rendered < 0) return fail(GSR_ERR_ARGS, "point_list_keys: bad sizes");
+    if (num_rendered == 0) return GSR_OK;
+    if (!geom || !binning || !keys) return fail(GSR_ERR_ARGS, "point_list_keys: NULL buffer");
+    return check_hip(launch_point_list_keys(P, W, H, geom, binning, num_rendered, keys, (hipStream_t)stream),
+                     "point_list_keys");
 }
 
 const char *gsr_last_error(void) { return g_err.c_str(); }

@@ -256,11 +256,12 @@ static hipError_t radix_pass(const RadixPass &a, hipStream_t s) {
 __device__ __forceinline__ uint32_t rect_area(uint4 q) {
     return ((q.x >> 16) - (q.x & 0xffffu)) * ((q.y >> 16) - (q.y & 0xffffu));
 }
-// instances of a Gaussian: the set bits of its tile mask (preprocess.hip), or the
-// whole rect when it spans more than 64 tiles
+// instances of a Gaussian: the whole rect when its tile mask (preprocess.hip) is
+// all ones (the upstream footprint, and every rect of more than 64 tiles), else
+// the set bits of the mask (a tight rect of at most 64 tiles: never all ones
+// below 64 tiles, and equal to the area at 64)
 __device__ __forceinline__ uint32_t rect_count(uint4 q) {
-    const uint32_t area = rect_area(q);
-    return area <= 64 ? (uint32_t)(__builtin_popcount(q.z) + __builtin_popcount(q.w)) : area;
+    return (q.z & q.w) == ~0u ? rect_area(q) : (uint32_t)(__builtin_popcount(q.z) + __builtin_popcount(q.w));
 }
 // index of the k-th set bit (k < popcount) of the 64-bit mask {lo, hi}
 __device__ __forceinline__ uint32_t kth_set_bit(uint32_t lo, uint32_t hi, uint32_t k) {
@@ -332,7 +333,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
     if (threadIdx.x == EMIT_BLOCK - 1) loff[EMIT_BLOCK] = tot;
     if (v) {
         rect[threadIdx.x] = make_uint4(q.x & 0xffffu, (q.x >> 16) - (q.x & 0xffffu), q.y & 0xffffu, id);
-        mask[threadIdx.x] = rect_area(q) <= 64 ? make_uint2(q.z, q.w) : make_uint2(~0u, ~0u);
+        mask[threadIdx.x] = make_uint2(q.z, q.w);
     }
     __syncthreads();
     const uint32_t base = a.block_prefix[blockIdx.x];
@@ -388,6 +389,26 @@ __global__ void __launch_bounds__(RANGE_THREADS) identify_ranges_kernel(const ui
         prev = i < n ? v[j] : prev;
     }
     if (i0 + 4 >= n) ranges[prev].y = n;
+}
+
+// upstream's sorted 64-bit keys (binningState.point_list_keys of
+// rasterizer_impl.cu): (tile << 32) | depth bits of the entry's Gaussian
+__global__ void point_list_keys_kernel(const uint32_t *tile_keys, const uint32_t *point_list, const uint32_t *depths,
+                                       uint32_t n, uint64_t *keys) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = ((uint64_t)tile_keys[i] << 32) | depths[point_list[i]];
+}
+
+hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const void *binning, int64_t I,
+                                  uint64_t *keys, hipStream_t s) {
+    if (I <= 0) return hipSuccess;
+    const GeomLayout L = geom_layout(P, W, H);
+    const BinningLayout B = binning_layout(I, W, H);
+    hipLaunchKernelGGL(point_list_keys_kernel, dim3((unsigned)((I + 255) / 256)), dim3(256), 0, s,
+                       at<const uint32_t>(binning, B.off[GSR_BIN_KEYS]),
+                       at<const uint32_t>(binning, B.off[GSR_BIN_POINT_LIST]),
+                       at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTHS]), (uint32_t)I, keys);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------ launchers

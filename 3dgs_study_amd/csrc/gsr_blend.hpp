@@ -61,6 +61,60 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
     return box_hit(mx, my, ca, cb, cc, qmax, x0, y0, 7.0f);
 }
 
+// power and G = exp(power) of one (pixel, Gaussian), for upstream's
+// `power > 0` skip and alpha = min(0.99, opacity * expf(power)) with its
+// `alpha < 1/255` skip.  The blend loops evaluate power as d^T conic' d
+// (conic' = -conic/2, contracted) and exp in hardware (v_exp_f32 of
+// power * log2 e): both within a few ulp of upstream's float expression and
+// libm's expf.  Where that could move a skip decision — alpha within 2^-12
+// relative of 1/255 (the combined error is below 2^-16), or a positive power
+// (the conic is positive definite, so only rounding makes one) — the pair is
+// redone exactly as the CPU restatement does it: upstream's expression in
+// upstream's operation order without contraction, and exp in double rounded
+// once (the correctly rounded expf, which libm's expf returns except within
+// 0.002 ulp of a rounding tie).  So every skip decision, and with it
+// n_contrib, matches the oracle's.  The branch is lane-masked and taken for
+// ~1e-4 of the pairs; the forward and backward share it (same decisions).
+struct BlendG {
+    float power, G;
+};
+// exp(x) for |x| <= 16 in double, Taylor to degree 13 on |r| <= ln2/2
+// (truncation < 2^-55 relative), rounded once to float.  Not inlined: the
+// rarely taken re-check then adds a call instead of its double-precision
+// registers to every iteration of the blend loops (inlined, the library exp
+// cost render_fwd 54 -> 73 VGPRs, render_bwd 68 -> 92).
+__device__ __attribute__((noinline)) float exp_rn_f32(float x) {
+    const double xd = (double)x;
+    const double n = __builtin_rint(xd * 1.4426950408889634);
+    const double r = __builtin_fma(-n, 1.9082149292705877e-10, __builtin_fma(-n, 0.6931471803691238, xd));
+    double p = 1.0 / 6227020800.0;
+    p = __builtin_fma(p, r, 1.0 / 479001600.0);
+    p = __builtin_fma(p, r, 1.0 / 39916800.0);
+    p = __builtin_fma(p, r, 1.0 / 3628800.0);
+    p = __builtin_fma(p, r, 1.0 / 362880.0);
+    p = __builtin_fma(p, r, 1.0 / 40320.0);
+    p = __builtin_fma(p, r, 1.0 / 5040.0);
+    p = __builtin_fma(p, r, 1.0 / 720.0);
+    p = __builtin_fma(p, r, 1.0 / 120.0);
+    p = __builtin_fma(p, r, 1.0 / 24.0);
+    p = __builtin_fma(p, r, 1.0 / 6.0);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return (float)__builtin_ldexp(p, (int)n);
+}
+__device__ __forceinline__ BlendG blend_g(float pw, float dx, float dy, float ca, float cb, float cc, float opacity) {
+    BlendG r{pw, __expf(pw)};
+    const float a = opacity * r.G;
+    if (__builtin_expect(pw > 0.0f || fabsf(a * 255.0f - 1.0f) < 0x1p-12f, 0)) {
+#pragma clang fp contract(off)
+        const float cx = -2.0f * ca, cy = -2.0f * cb, cz = -2.0f * cc;  // exact
+        r.power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
+        r.G = exp_rn_f32(r.power);
+    }
+    return r;
+}
+
 // s_waitcnt vmcnt(4) expcnt(7) lgkmcnt(15): everything but the 4 youngest
 // vector-memory ops (the chunk prefetch) has completed.  Issued as the builtin so
 // that the compiler's waitcnt pass sees it and marks the older loads as landed.

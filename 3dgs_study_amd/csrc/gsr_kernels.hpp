@@ -18,6 +18,8 @@ hipError_t launch_depth_sort_tail(int P, int W, int H, void *geom, bool fourth_p
 hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
                        hipStream_t s);
 hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, hipStream_t s);
+hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const void *binning, int64_t I,
+                                  uint64_t *keys, hipStream_t s);
 
 // render_fwd.hip
 hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,

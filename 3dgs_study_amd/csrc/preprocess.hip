@@ -154,18 +154,22 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 emit = true;
                 depth = p_view.z;
                 radius_out = r;
-                // Tight footprint: of the bounding rect's tiles keep those whose
-                // 16x16 pixel box meets the alpha >= 1/255 ellipse q(d) <= qmax
-                // (qmax already widened, above).  Per tile row the ellipse's
-                // x-extent over the row's band of pixel centres is exact: the
-                // leftmost / rightmost points of the ellipse clamped into the band
-                // (the boundary's x is convex / concave in y).  Dropped tiles hold
-                // only pixels that every blend would skip, so images and gradients
-                // are unchanged while ~40% fewer instances are binned (config C).
-                // Rects of more than 64 tiles, and NaN bounds, keep every tile.
+                // Tile mask of the rect (row-major bit per tile); all ones = every
+                // tile of the rect, whatever its area (upstream's getRect
+                // footprint, GSR_FOOTPRINT_RECT).
+                // Tight footprint (GSR_FOOTPRINT_TIGHT): of the bounding rect's
+                // tiles keep those whose 16x16 pixel box meets the alpha >= 1/255
+                // ellipse q(d) <= qmax (qmax already widened, above).  Per tile row
+                // the ellipse's x-extent over the row's band of pixel centres is
+                // exact: the leftmost / rightmost points of the ellipse clamped into
+                // the band (the boundary's x is convex / concave in y).  Dropped
+                // tiles hold only pixels that every blend would skip, so images and
+                // gradients are unchanged while ~40% fewer instances are binned
+                // (config C).  Rects of more than 64 tiles, and NaN bounds, keep
+                // every tile.
                 uint64_t m = ~0ull;
                 touched = area;
-                if (area <= 64 && !(qmax != qmax)) {
+                if (in.footprint == GSR_FOOTPRINT_TIGHT && area <= 64 && !(qmax != qmax)) {
                     m = 0;
                     const float ka = conic_x, kb = conic_y, kc = conic_z;
                     const float kdet = ka * kc - kb * kb;
@@ -190,7 +194,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                         const int n = tb - ta + 1, sh = (ty - rc.y0) * w + (ta - rc.x0);
                         m |= (n >= 64 ? ~0ull : ((1ull << n) - 1ull)) << sh;
                     }
-                    touched = (uint32_t)__builtin_popcountll(m);
+                    touched = m == ~0ull ? area : (uint32_t)__builtin_popcountll(m);
                 }
                 rect_out = make_uint4(rc.x0 | (rc.x1 << 16), rc.y0 | (rc.y1 << 16), (uint32_t)m, (uint32_t)(m >> 32));
             }

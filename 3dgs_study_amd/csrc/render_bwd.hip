@@ -24,26 +24,13 @@
 
 namespace gsr {
 
-#ifdef GSR_BWD_STATS
-// Work counters for tuning (tools/bwd_stats.py): waves, chunks, pairs walked,
-// pairs with a contributing pixel, quadrant hits, end entries, valid lanes.
-__device__ unsigned long long g_bwd_stats[8];
-#define BWD_STAT(k, v) \
-    do { if (lane == 0) atomicAdd(&g_bwd_stats[k], (unsigned long long)(v)); } while (0)
-#else
-#define BWD_STAT(k, v) do { } while (0)
-#endif
-
-// Wave order: per XCD, most forward work first (GSR_BWD_ORDER=1; the buckets
-// the forward filed, gsr_blend.hpp), so that the longest replays start at once
-// instead of forming the kernel's tail; 0 = the forward's XCD strip order.
-#ifndef GSR_BWD_ORDER
-#define GSR_BWD_ORDER 1
-#endif
+// Wave order: per XCD, most forward work first (the buckets the forward filed,
+// gsr_blend.hpp), so that the longest replays start at once instead of forming
+// the kernel's tail.
 
 struct RenderBwdArgs {
     int W, H, gx, tiles;
-    const uint32_t *order_cnt;  // [8][ORDER_NBUCKET] quadrants per (XCD, work bucket) (GSR_BWD_ORDER)
+    const uint32_t *order_cnt;  // [8][ORDER_NBUCKET] quadrants per (XCD, work bucket)
     const uint32_t *qlist;      // [8][ORDER_NBUCKET][maxc]
     int maxc;
     const uint2 *ranges;
@@ -83,24 +70,13 @@ __device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
-#ifdef GSR_BWD_WPE  // experiment: minimum waves per SIMD (caps the VGPR budget)
-#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_BWD_WPE)))
-#else
-#define GSR_BWD_ATTR
-#endif
-__global__ void __launch_bounds__(BLEND_THREADS) GSR_BWD_ATTR render_bwd_kernel(RenderBwdArgs a) {
-#if GSR_BWD_ORDER
+__global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs a) {
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
     // workgroup 8 r + x: XCD x's r-th quadrant in bucket order (gsr_blend.hpp)
     const int lane = threadIdx.x & 63;
     const int quad = ordered_quad(a.order_cnt, a.qlist, a.maxc);
     if (quad < 0) return;
     const int tile = (int)(quad >> 2), w = (int)(quad & 3);
-#else
-    const QuadSlot qs = quad_slot(a.tiles);
-    const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
-    if (tile < 0) return;
-#endif
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
@@ -124,8 +100,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) GSR_BWD_ATTR render_bwd_kernel(
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) end = max(end, __shfl_xor(end, o));
     if (end <= 0) return;
-    BWD_STAT(0, 1);
-    BWD_STAT(5, end);
 
     __shared__ ChunkStage stage[BLEND_WAVES];
     ChunkStage &st = stage[BLEND_WAVES == 1 ? 0 : w];
@@ -166,14 +140,12 @@ __global__ void __launch_bounds__(BLEND_THREADS) GSR_BWD_ATTR render_bwd_kernel(
         q.dy = p0.y - fy;
         const float ux = p0.z * q.dx + p0.w * q.dy;  // conic' * d with conic' = -conic/2 (splat record)
         const float uy = p0.w * q.dx + p1.x * q.dy;
-        const float power = q.dx * ux + q.dy * uy;  // upstream's power; == render_fwd.hip, bit for bit
-#ifdef GSR_EXP_NO_EXP  // timing experiment only
-        q.G = 1.0f + power * (1.0f + 0.5f * power);
-#else
-        q.G = __expf(power);
-#endif
+        // power and G bit for bit as render_fwd.hip computes them (same expression,
+        // same exact re-check near the skip thresholds)
+        const BlendG e = blend_g(q.dx * ux + q.dy * uy, q.dx, q.dy, p0.z, p0.w, p1.x, p1.y);
+        q.G = e.G;
         q.alpha = fminf(0.99f, p1.y * q.G);
-        q.valid = live && k < lim && !(power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
+        q.valid = live && k < lim && !(e.power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
         return q;
     };
     // The per-pixel quantities the nine sums of one Gaussian are made of.
@@ -228,10 +200,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) GSR_BWD_ATTR render_bwd_kernel(
             return keep + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send),
                                                                                 0x1F | (16 << 10)));
         };
-#ifdef GSR_EXP_NO_REDUCE  // timing experiment only
-        const float v = k0 + s0 + k1 + s1 + k0 * kx + s0 * sx + k0 * ky + s0 * sy + k1 * ky + s1 * sy + k5 + s5 +
-                        kt * dpx0 + st_ * dpx1 + kt * dpx2;
-#else
         const float o0 = x16(k0, s0);
         const float o1 = x16(k1, s1);
         const float o2 = x16(k0 * kx, s0 * sx);
@@ -253,15 +221,10 @@ __global__ void __launch_bounds__(BLEND_THREADS) GSR_BWD_ATTR render_bwd_kernel(
         const float w1 = swz_stage<2>(u2, 0.f, lane);
         const float x0 = swz_stage<1>(w0, w1, lane);
         const float v = swap32_sum(x0, x0);  // both halves: the full sum
-#endif
         // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
         // compiler's atomic optimizer (a wave-scan loop) out
-#ifdef GSR_EXP_NO_ATOMIC  // timing experiment only
-        if (v == 1234.5f) a.accum[lane] = v;
-#else
         if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, v);
         if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
-#endif
     };
 
     // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l),
@@ -273,8 +236,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) GSR_BWD_ATTR render_bwd_kernel(
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         const uint64_t mask = __ballot(rel);
         const int ns = stage_survivors(st, lane, rel, mask, A, B, C, 1);
-        BWD_STAT(1, 1);
-        BWD_STAT(4, ns);
         const int lim = last_contrib - lo;  // entry lo + l replays for this pixel iff l < lim
         // byte offset of record b = k - 1 + 1 in a VGPR (asm barrier: keep it there)
         uint32_t boff = (uint32_t)(ns - 1) * (uint32_t)sizeof(st.rec[0]);
@@ -291,16 +252,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) GSR_BWD_ATTR render_bwd_kernel(
             const int la = __float_as_int(a2.w), lb = __float_as_int(b2.w);
             const Pre qa = prepare(a0, a1, la, lim, true);  // entry lo + l = upstream `contributor`
             const Pre qb = prepare(b0, b1, lb, lim, two);
-            BWD_STAT(2, 1);
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
-#ifdef GSR_BWD_STATS
-            {
-                const uint64_t va = __builtin_amdgcn_ballot_w64(qa.valid), vb = __builtin_amdgcn_ballot_w64(qb.valid);
-                BWD_STAT(3, (va | vb) != 0);
-                BWD_STAT(6, __builtin_popcountll(va) + __builtin_popcountll(vb));
-            }
-#endif
             const Part pa = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: a before b
             const Part pb = replay(qb, b1.y, b1.z, b1.w, b2.x);
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.y));
@@ -353,25 +306,11 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
     a.dL_dpix = dL_dpix;
     a.accum = accum;
-#if GSR_BWD_ORDER
     a.order_cnt = at<uint32_t>(geom, G.order_cnt);
     a.qlist = at<uint32_t>(img, Im.qlist);
     a.maxc = order_max_per_xcd(4 * g.tiles);
     hipLaunchKernelGGL(render_bwd_kernel, dim3(8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);
-#else
-    a.order_cnt = a.qlist = nullptr;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
-#endif
     return hipGetLastError();
 }
 
 }  // namespace gsr
-
-#ifdef GSR_BWD_STATS
-extern "C" int gsr_debug_bwd_stats(unsigned long long *out) {
-    hipDeviceSynchronize();
-    hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_bwd_stats), sizeof(gsr::g_bwd_stats));
-    const unsigned long long z[8] = {};
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_bwd_stats), z, sizeof z);
-}
-#endif

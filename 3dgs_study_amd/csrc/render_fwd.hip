@@ -81,8 +81,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
                     // conic' = -conic/2 (splat record): pw is upstream's power; render_bwd.hip
                     // recomputes it bit for bit
                     const float ux = r0.z * dx + r0.w * dy, uy = r0.w * dx + r1.x * dy;
-                    pw[g] = dx * ux + dy * uy;
-                    al[g] = fminf(0.99f, r1.y * __expf(pw[g]));
+                    const BlendG e = blend_g(dx * ux + dy * uy, dx, dy, r0.z, r0.w, r1.x, r1.y);
+                    pw[g] = e.power;
+                    al[g] = fminf(0.99f, r1.y * e.G);
                     cr[g] = r1.z;
                     cg[g] = r1.w;
                 }

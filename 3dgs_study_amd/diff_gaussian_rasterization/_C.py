@@ -37,6 +37,7 @@ class GsrInputs(ctypes.Structure):
         ("W", ctypes.c_int32), ("H", ctypes.c_int32),
         ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float), ("scale_modifier", ctypes.c_float),
         ("prefiltered", ctypes.c_int32), ("debug", ctypes.c_int32),
+        ("footprint", ctypes.c_int32), ("reserved", ctypes.c_int32),
         ("bg", ctypes.c_void_p), ("means3D", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
         ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p), ("rotations", ctypes.c_void_p),
         ("cov3D_precomp", ctypes.c_void_p), ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
@@ -53,8 +54,32 @@ EXPORTED = (
     "gsr_l1_ssim_scratch_bytes", "gsr_l1_ssim", "gsr_adam_step", "gsr_densify_stats",
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
-    "gsr_backward_colors_render", "gsr_backward_colors_finish",
+    "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys",
 )
+
+# gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
+FOOTPRINTS = {"rect": 0, "tight": 1}
+_footprint = os.environ.get("GSR_FOOTPRINT", "rect")
+if _footprint not in FOOTPRINTS:
+    raise ImportError(f"GSR_FOOTPRINT={_footprint!r}: expected one of {sorted(FOOTPRINTS)}")
+
+
+def set_footprint(mode: str) -> str:
+    """Select the tile footprint of later forwards; returns the previous mode.
+
+    "rect" (default): upstream's getRect footprint — num_rendered, the sorted keys,
+    point_list, ranges and n_contrib are upstream's.  "tight": only the rect tiles
+    the Gaussian's alpha >= 1/255 ellipse reaches (same image and gradients,
+    ~40 % fewer list entries; num_rendered counts the shorter lists)."""
+    global _footprint
+    if mode not in FOOTPRINTS:
+        raise ValueError(f"footprint must be one of {sorted(FOOTPRINTS)} (got {mode!r})")
+    prev, _footprint = _footprint, mode
+    return prev
+
+
+def get_footprint() -> str:
+    return _footprint
 
 
 class GsrAdamSegment(ctypes.Structure):
@@ -64,7 +89,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib = None
 
@@ -109,6 +134,8 @@ def load_library():
     lib.gsr_sh_record_floats.restype = i64
     lib.gsr_sh_grad_from_colors.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
     lib.gsr_sh_grad_from_colors.restype = ctypes.c_int
+    lib.gsr_point_list_keys.argtypes = [i32, i32, i32, vp, vp, i64, vp, vp]
+    lib.gsr_point_list_keys.restype = ctypes.c_int
     lib.gsr_mark_visible.argtypes = [i32, vp, vp, vp, vp, vp]
     lib.gsr_mark_visible.restype = ctypes.c_int
     for name in ("gsr_geom_layout", "gsr_binning_layout", "gsr_img_layout"):
@@ -172,7 +199,7 @@ def _stream(device):
 
 
 def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
-            tan_fovx, tan_fovy, H, W, sh, degree, campos, prefiltered, debug):
+            tan_fovx, tan_fovy, H, W, sh, degree, campos, prefiltered, debug, footprint=None):
     if means3D.ndim != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     device = means3D.device
@@ -189,6 +216,7 @@ def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov
     M = sh_t.size(1) if (sh_t is not None and sh_t.size(0) != 0) else 0
     s = GsrInputs(P=P, D=int(degree), M=M, W=int(W), H=int(H), tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
                   scale_modifier=float(scale_modifier), prefiltered=int(bool(prefiltered)), debug=int(bool(debug)),
+                  footprint=FOOTPRINTS[footprint or _footprint],
                   bg=_ptr(keep["background"]), means3D=_ptr(keep["means3D"]), colors_precomp=_ptr(keep["colors"]),
                   opacities=_ptr(keep["opacity"]), scales=_ptr(keep["scales"]), rotations=_ptr(keep["rotations"]),
                   cov3D_precomp=_ptr(keep["cov3D_precomp"]), viewmatrix=_ptr(keep["viewmatrix"]),
@@ -198,13 +226,18 @@ def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, debug):
-    """-> (num_rendered, color [3,H,W], radii [P] int32, geomBuffer, binningBuffer, imgBuffer)"""
+                        prefiltered, debug, footprint=None):
+    """-> (num_rendered, color [3,H,W], radii [P] int32, geomBuffer, binningBuffer, imgBuffer)
+
+    ``footprint`` (keyword, not upstream): "rect" | "tight" for this call; None =
+    the module setting (``set_footprint``, env GSR_FOOTPRINT, default "rect")."""
     lib = load_library()
     H, W = int(image_height), int(image_width)
+    if footprint is not None and footprint not in FOOTPRINTS:
+        raise ValueError(f"footprint must be one of {sorted(FOOTPRINTS)} (got {footprint!r})")
     s, keep, device, M = _inputs(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos,
-                                 prefiltered, debug)
+                                 prefiltered, debug, footprint)
     P = s.P
     u8 = dict(dtype=torch.uint8, device=device)
     out_color = torch.empty((3, H, W), dtype=torch.float32, device=device)
@@ -350,6 +383,18 @@ def timing_read() -> dict:
 
 
 # ------------------------------------------------------------------ test hooks
+def point_list_keys(P, W, H, geomBuffer, binningBuffer, num_rendered):
+    """upstream's sorted 64-bit keys (tile << 32 | depth bits) of a forward's lists,
+    as an int64 tensor holding the uint64 bit patterns (gsr_point_list_keys)."""
+    lib = load_library()
+    keys = torch.empty((max(int(num_rendered), 0),), dtype=torch.int64, device=geomBuffer.device)
+    if keys.numel():
+        _check(lib.gsr_point_list_keys(int(P), int(W), int(H), geomBuffer.data_ptr(), binningBuffer.data_ptr(),
+                                       int(num_rendered), keys.data_ptr(), _stream(geomBuffer.device)),
+               "point_list_keys")
+    return keys
+
+
 def layouts(P, W, H, num_rendered):
     """Byte offsets of the named scratch sub-arrays (parity tests read intermediates)."""
     lib = load_library()

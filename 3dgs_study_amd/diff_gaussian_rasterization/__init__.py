@@ -23,6 +23,11 @@ sink the view's colour gradient instead of returning dsh (the ``sh`` input then
 gets no gradient through autograd; the sink rebuilds the SH leaf gradients summed
 over all ranks' views).  ``set_sh_grad_sink(None)`` restores upstream behaviour.
 
+Tile footprint (not upstream; ``set_footprint``, env ``GSR_FOOTPRINT``): "rect"
+(default) bins every tile of upstream's getRect rect, so ``num_rendered`` and the
+binning buffer's lists are upstream's; "tight" bins only the tiles the alpha >=
+1/255 ellipse reaches — same image, radii and gradients from shorter lists.
+
 Debug mode (``raster_settings.debug``): the native side synchronises after every
 kernel; on failure a CPU copy of the arguments is written to
 ``snapshot_fw.dump`` / ``snapshot_bw.dump`` before the exception propagates.
@@ -36,7 +41,10 @@ import torch.nn as nn
 
 from . import _C
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "set_sh_grad_sink"]
+from ._C import get_footprint, set_footprint  # noqa: E402
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "set_sh_grad_sink",
+           "set_footprint", "get_footprint"]
 
 _sh_grad_sink = None
 

@@ -131,6 +131,10 @@ def main():
     ap.add_argument("--grad-exchange", default="sh-colour", choices=["sh-colour", "allreduce"],
                     help="N>1: 'sh-colour' all-gathers per-view colour gradients for the SH block and all-reduces "
                          "the rest (multiview.py); 'allreduce' all-reduces all 59 floats/Gaussian")
+    ap.add_argument("--footprint-steps", type=int, default=100,
+                    help="timed steps of the same unit with the other tile footprint (gsr.h gsr_footprint); 0 = skip")
+    ap.add_argument("--stage-events", default="all", choices=["all", "none"],
+                    help="HIP events around every rasterizer stage in the timed region (stages_ms, roofline)")
     ap.add_argument("--render-steps", type=int, default=20,
                     help="timed forward-only renders of config E (5M, 4K) reported beside the C line; 0 = skip")
     args = ap.parse_args()
@@ -181,23 +185,17 @@ def main():
             reducer()  # wait for the exchange started inside backward (+ rebuild the SH gradients)
         return out
 
-    # Warm-up; its last steps carry events on every stage for the breakdown
-    # (stages_ms) and to find the dominant kernel.
-    nprobe = min(5, args.warmup)
-    for i in range(args.warmup):
-        if i == args.warmup - nprobe:
-            _C.timing_enable(True)
+    # the instances of this rank's view (the byte model), found before the warm-up
+    I = _last_num_rendered(cam, g, bg)
+    for _ in range(args.warmup):
         out = one_step()
     torch.cuda.synchronize()
-    stages = _C.timing_read() if nprobe else {}
-    _C.timing_enable(False)
-    per_stage = {k: (ms / n if n else 0.0, n) for k, (ms, n) in stages.items()}
-    dom = max(per_stage, key=lambda k: per_stage[k][0] * per_stage[k][1]) if per_stage else "render_bwd"
     if world > 1:
         dist.barrier()
-    # Timed region: events only around the dominant kernel (its live average
-    # launch time prices the roofline); every other stage runs unobserved.
-    _C.timing_enable([dom])
+    # Timed region.  Every rasterizer stage carries HIP events on the launch stream
+    # (gsr_timing_*): stages_ms and the dominant stage's live average launch time
+    # (the roofline) come from these K steps.
+    _C.timing_enable(args.stage_events == "all")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -206,14 +204,16 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    dom_live = _C.timing_read()[dom]
+    stages = _C.timing_read()
     _C.timing_enable(False)
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    I = _last_num_rendered(cam, g, bg)  # measured instances of this rank's view (byte model)
+    per_stage = {k: (ms / n if n else 0.0, n) for k, (ms, n) in stages.items() if n}
+    dom = max(per_stage, key=lambda k: per_stage[k][0] * per_stage[k][1]) if per_stage else "render_bwd"
+    dom_live = stages.get(dom, (0.0, 0))
 
     if rank == 0:
         steps = args.steps
@@ -239,7 +239,7 @@ def main():
             "config": {
                 "workload": f"{args.config}: {WORKLOADS[args.config]}",
                 "gaussians": P, "width": W, "height": H, "sh_degree": deg,
-                "num_rendered": I, "views_per_step": world,
+                "footprint": _C.get_footprint(), "num_rendered": I, "views_per_step": world,
                 "loss": "L1" if not args.lambda_dssim else f"L1+{args.lambda_dssim}*(1-SSIM)",
                 "parallelism": f"view-parallel x{world}" + (
                     (f", {coll} all-gather of per-view colour-gradient records + all-reduce of xyz/opacity/scaling/"
@@ -250,6 +250,7 @@ def main():
             },
             "mpix_per_s": round(value * W * H / 1e6, 2),
             "stages_ms": {k: round(v[0], 4) for k, v in per_stage.items()},
+            "stages_source": "HIP events around every rasterizer stage inside the timed region (mean per launch)",
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -265,6 +266,9 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if world == 1 and args.footprint_steps > 0:
+            line["footprint_" + ("tight" if _C.get_footprint() == "rect" else "rect")] = footprint_rates(
+                one_step, cam, g, bg, args.footprint_steps, args.warmup)
         if world == 1 and args.full_steps > 0:
             line["full_step"] = full_step_rates(cam, P, deg, target, bg, args.full_steps)
         if world == 1 and args.render_steps > 0:
@@ -275,6 +279,34 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
+    """The headline unit again with the other tile footprint (rect <-> tight):
+    same image and gradients from lists of a different length."""
+    import torch
+    from diff_gaussian_rasterization import _C, set_footprint
+
+    mode = "tight" if _C.get_footprint() == "rect" else "rect"
+    prev = set_footprint(mode)
+    try:
+        I = _last_num_rendered(cam, g, bg)
+        for _ in range(warmup):
+            one_step()
+        torch.cuda.synchronize()
+        _C.timing_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one_step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        stages = _C.timing_read()
+        _C.timing_enable(False)
+    finally:
+        set_footprint(prev)
+    return {"footprint": mode, "value": round(steps / dt, 3), "unit": "train-iters/s",
+            "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps, "num_rendered": I,
+            "stages_ms": {k: round(ms / n, 4) for k, (ms, n) in stages.items() if n}}
 
 
 def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0) -> dict:
@@ -293,36 +325,36 @@ def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0) -> 
     cam = synthetic.make_camera(W, H, view=view).to(dev)
     g = synthetic.make_gaussians(P, deg, seed=0).to(dev)
     bg = torch.zeros(3, device=dev)
+    I = _last_num_rendered(cam, g, bg)
     with torch.no_grad():
-        for i in range(warmup):
-            if i == warmup - 1:
-                _C.timing_enable(True)
+        for _ in range(warmup):
             train_step.render(cam, g, bg)
         torch.cuda.synchronize()
-        stages = _C.timing_read()
-        _C.timing_enable(["render_fwd"])
-        torch.cuda.synchronize()
+        _C.timing_enable(True)  # every stage, inside the timed region
         t0 = time.perf_counter()
         for _ in range(steps):
             train_step.render(cam, g, bg)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        live = _C.timing_read()["render_fwd"]
+        stages = _C.timing_read()
         _C.timing_enable(False)
-    I = _last_num_rendered(cam, g, bg)
-    fwd_ms = live[0] / live[1] if live[1] else 0.0
-    ab = algorithmic_bytes("render_fwd", P, I, W, H, M)
-    achieved = ab / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+    per = {k: (ms / n, n) for k, (ms, n) in stages.items() if n}
+    dom = max(per, key=lambda k: per[k][0] * per[k][1])  # the largest stage by measured time
+    dom_ms = per[dom][0]
+    ab = algorithmic_bytes(dom, P, I, W, H, M)
+    achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     fps = steps / dt
     res = {
         "metric": render_metric(cfg_name), "value": round(fps, 3), "unit": "frames/s", "ms_per_frame": round(1e3 * dt / steps, 4),
         "mpix_per_s": round(fps * W * H / 1e6, 2), "steps": steps, "warmup": warmup,
         "config": {"workload": f"{cfg_name}: {WORKLOADS[cfg_name]}", "gaussians": P, "width": W, "height": H,
-                   "sh_degree": deg, "num_rendered": I},
-        "stages_ms": {k: round(ms / n, 4) for k, (ms, n) in stages.items() if n},
-        "roofline": {"bound": "hbm", "kernel": "render_fwd", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("render_fwd_E"),
-                     "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(fwd_ms, 4)},
+                   "sh_degree": deg, "footprint": _C.get_footprint(), "num_rendered": I},
+        "stages_ms": {k: round(v[0], 4) for k, v in per.items()},
+        "stages_source": "HIP events around every rasterizer stage inside the timed region (mean per launch)",
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic(f"{dom}_{cfg_name}"),
+                     "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(dom_ms, 4)},
     }
     fwd_bytes = sum(algorithmic_bytes(k, P, I, W, H, M) for k in
                     ("preprocess", "depth_sort", "duplicate", "tile_sort", "render_fwd"))

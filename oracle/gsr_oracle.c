@@ -53,6 +53,17 @@ static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
                                0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
                                -0.5900435899266435f};
 
+/* exp for the blend's alpha: the correctly rounded float exp, taken as the
+ * double-precision exp rounded once (checked equal to the correctly rounded
+ * value for every float in [-16, 1]; glibc's expf differs on ~6e-5 of them).
+ * Upstream's CUDA expf is accurate to 2 ulp and not reproducible off the GPU,
+ * so the restatement pins the exact value: the HIP blend kernels take the same
+ * `alpha < 1/255` decisions (gsr_blend.hpp blend_g). */
+static float exp_rn(float x) {
+    volatile double d = exp((double)x); /* volatile: no narrowing to expf */
+    return (float)d;
+}
+
 typedef struct { float x, y, z; } f3;
 typedef struct { float x, y, z, w; } f4;
 
@@ -373,7 +384,7 @@ void oracle_render_forward(const uint32_t *ranges, const uint32_t *point_list, i
                         const float *co = conic_opacity + 4 * (size_t)id;
                         float power = -0.5f * (co[0] * dxp * dxp + co[2] * dyp * dyp) - co[1] * dxp * dyp;
                         if (power > 0.0f) continue;
-                        float alpha = fminf(0.99f, co[3] * expf(power));
+                        float alpha = fminf(0.99f, co[3] * exp_rn(power));
                         if (alpha < 1.0f / 255.0f) continue;
                         float test_T = T * (1 - alpha);
                         if (test_T < 0.0001f) break; /* done: this one is not blended */
@@ -428,7 +439,7 @@ void oracle_render_backward(const uint32_t *ranges, const uint32_t *point_list, 
                         const float *co = conic_opacity + 4 * (size_t)gid;
                         float power = -0.5f * (co[0] * dxp * dxp + co[2] * dyp * dyp) - co[1] * dxp * dyp;
                         if (power > 0.0f) continue;
-                        float G = expf(power);
+                        float G = exp_rn(power);
                         float alpha = fminf(0.99f, co[3] * G);
                         if (alpha < 1.0f / 255.0f) continue;
                         T = T / (1.f - alpha);

@@ -35,7 +35,7 @@ def activated(g, python_branch=False, scale_modifier=1.0):
 
 
 def run_hip(cam, g, dev, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=None, python_branch=False,
-            dL=None, debug=False, dsh_planar=False):
+            dL=None, debug=False, dsh_planar=False, footprint="rect"):
     from diff_gaussian_rasterization import _C
 
     a = activated(g, python_branch, scale_modifier)
@@ -47,11 +47,12 @@ def run_hip(cam, g, dev, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=
             float(scale_modifier), t(a.get("cov3D_precomp")), t(cam.world_view_transform),
             t(cam.full_proj_transform), math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5), cam.image_height,
             cam.image_width, shs, g.active_sh_degree, t(cam.camera_center), False, debug)
-    I, color, radii, geom, binning, img = _C.rasterize_gaussians(*args)
+    I, color, radii, geom, binning, img = _C.rasterize_gaussians(*args, footprint=footprint)
     torch.cuda.synchronize()
     P, W, H = a["means3D"].shape[0], cam.image_width, cam.image_height
-    out = dict(num_rendered=I, color=color.cpu().numpy(), radii=radii.cpu().numpy())
+    out = dict(num_rendered=I, color=color.cpu().numpy(), radii=radii.cpu().numpy(), footprint=footprint)
     out.update(read_intermediates(geom, binning, img, P, W, H, I))
+    out["keys64"] = _C.point_list_keys(P, W, H, geom, binning, I).cpu().numpy().view(np.uint64)
     if dL is not None:
         g_ = torch.as_tensor(dL, dtype=torch.float32).to(dev)
         bargs = (bg_t, args[1], radii, colors, args[4], args[5], float(scale_modifier), args[7], args[8], args[9],

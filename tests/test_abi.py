@@ -35,10 +35,11 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 4
-    # 10 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
-    assert ctypes.sizeof(_C.GsrInputs) == 40 + 11 * 8
-    assert _C.GsrInputs.bg.offset == 40
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 5
+    # 12 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
+    assert ctypes.sizeof(_C.GsrInputs) == 48 + 11 * 8
+    assert _C.GsrInputs.footprint.offset == 40
+    assert _C.GsrInputs.bg.offset == 48
 
 
 def test_scratch_layouts_are_aligned_and_disjoint(lib):
@@ -78,6 +79,7 @@ def _inputs(**kw):
     (dict(D=4, M=25), "sh_degree must be in [0, 3]"),
     (dict(P=-1), "num_points, 3"),
     (dict(W=0), "image size"),
+    (dict(footprint=2), "footprint must be"),
 ])
 def test_argument_validation_mirrors_upstream_errors(lib, kw, msg):
     s = _inputs(**kw)
@@ -145,3 +147,28 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setenv("GSR_LIBRARY", str(tmp_path / "nope.so"))
     with pytest.raises(ImportError, match="not found"):
         _C.load_library()
+
+
+def test_footprint_selector():
+    from diff_gaussian_rasterization import _C, get_footprint, set_footprint
+
+    assert get_footprint() == "rect"  # upstream's footprint unless asked
+    prev = set_footprint("tight")
+    try:
+        assert prev == "rect" and get_footprint() == "tight"
+        with pytest.raises(ValueError, match="footprint must be"):
+            set_footprint("box")
+    finally:
+        set_footprint(prev)
+    assert _C.FOOTPRINTS == {"rect": 0, "tight": 1}
+    assert lib_point_list_keys_validates()
+
+
+def lib_point_list_keys_validates():
+    from diff_gaussian_rasterization import _C
+
+    lib = _C.load_library()
+    assert lib.gsr_point_list_keys(10, 16, 16, None, None, 0, None, None) == 0  # nothing to write
+    assert lib.gsr_point_list_keys(10, 16, 16, None, None, 5, None, None) != 0
+    assert "NULL" in lib.gsr_last_error().decode()
+    return True
