@@ -59,7 +59,11 @@ EXPORTED = (
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
 FOOTPRINTS = {"rect": 0, "tight": 1}
-_footprint = os.environ.get("GSR_FOOTPRINT", "rect")
+# The package default is "tight" (DESIGN.md §2): image, radii, final_T and every
+# gradient are upstream's either way, and of upstream's outputs only the
+# num_rendered integer differs; GSR_FOOTPRINT=rect (or set_footprint("rect"))
+# gives upstream's lists bit for bit.  (The C struct's zero value is RECT.)
+_footprint = os.environ.get("GSR_FOOTPRINT", "tight")
 if _footprint not in FOOTPRINTS:
     raise ImportError(f"GSR_FOOTPRINT={_footprint!r}: expected one of {sorted(FOOTPRINTS)}")
 
@@ -67,10 +71,10 @@ if _footprint not in FOOTPRINTS:
 def set_footprint(mode: str) -> str:
     """Select the tile footprint of later forwards; returns the previous mode.
 
-    "rect" (default): upstream's getRect footprint — num_rendered, the sorted keys,
-    point_list, ranges and n_contrib are upstream's.  "tight": only the rect tiles
-    the Gaussian's alpha >= 1/255 ellipse reaches (same image and gradients,
-    ~40 % fewer list entries; num_rendered counts the shorter lists)."""
+    "rect": upstream's getRect footprint — num_rendered, the sorted keys, point_list,
+    ranges and n_contrib are upstream's.  "tight" (default): only the rect tiles the
+    Gaussian's alpha >= 1/255 ellipse reaches (same image, radii and gradients, ~40 %
+    fewer list entries at config C; num_rendered counts the shorter lists)."""
     global _footprint
     if mode not in FOOTPRINTS:
         raise ValueError(f"footprint must be one of {sorted(FOOTPRINTS)} (got {mode!r})")
@@ -230,7 +234,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     """-> (num_rendered, color [3,H,W], radii [P] int32, geomBuffer, binningBuffer, imgBuffer)
 
     ``footprint`` (keyword, not upstream): "rect" | "tight" for this call; None =
-    the module setting (``set_footprint``, env GSR_FOOTPRINT, default "rect")."""
+    the module setting (``set_footprint``, env GSR_FOOTPRINT, default "tight")."""
     lib = load_library()
     H, W = int(image_height), int(image_width)
     if footprint is not None and footprint not in FOOTPRINTS:

@@ -24,9 +24,10 @@ gets no gradient through autograd; the sink rebuilds the SH leaf gradients summe
 over all ranks' views).  ``set_sh_grad_sink(None)`` restores upstream behaviour.
 
 Tile footprint (not upstream; ``set_footprint``, env ``GSR_FOOTPRINT``): "rect"
-(default) bins every tile of upstream's getRect rect, so ``num_rendered`` and the
-binning buffer's lists are upstream's; "tight" bins only the tiles the alpha >=
-1/255 ellipse reaches — same image, radii and gradients from shorter lists.
+bins every tile of upstream's getRect rect, so ``num_rendered`` and the binning
+buffer's lists are upstream's bit for bit; "tight" (default) bins only the tiles
+the alpha >= 1/255 ellipse reaches — the same image, radii and gradients from
+shorter lists (of upstream's outputs only the ``num_rendered`` integer differs).
 
 Debug mode (``raster_settings.debug``): the native side synchronises after every
 kernel; on failure a CPU copy of the arguments is written to

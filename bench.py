@@ -85,36 +85,104 @@ def pmc_traffic(stage: str):
     return float(v) if v is not None else None
 
 
-def cpu_baseline(P: int, W: int, H: int, deg: int, budget_s: float = 30.0) -> dict:
-    """Time the C oracle (single thread) on full views of the same workload."""
+def _host_cpu() -> dict:
+    """Core count (`nproc`, which honours the box's CPU share / OMP_NUM_THREADS) and
+    the CPU model name (lscpu's "Model name", from /proc/cpuinfo)."""
+    import subprocess
+
+    try:
+        n = int(subprocess.run(["nproc"], capture_output=True, text=True, check=True).stdout.strip())
+    except (OSError, ValueError, subprocess.CalledProcessError):
+        n = len(os.sched_getaffinity(0))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": n, "model": model}
+
+
+def cpu_baseline(configs=("A", "B", "C", "E"), repeats: int = 3, cap_s: float = 1800.0) -> dict:
+    """SURVEY.md §8(d)'s CPU baseline: the reference's render() shape with
+    convert_SHs_python and compute_cov3D_python (gaussian_renderer/__init__.py:74-90:
+    SH -> RGB and the 3D covariance in torch, autograd through them), the rasterizer
+    forward / backward by the C oracle's OpenMP build (oracle/, a port of the
+    upstream algorithm; rasterize -> L1 -> backward for the training configs), on
+    all `nproc` host cores.  Median of `repeats` after one warm-up per config."""
+    ncpu = _host_cpu()
+    os.environ.setdefault("OMP_NUM_THREADS", str(ncpu["nproc"]))
+    import math
+
     import numpy as np
+    import torch
 
     import synthetic
+    import train_step
     from oracle import oracle
 
     oracle.build()
-    cam = synthetic.make_camera(W, H, 0)
-    g = synthetic.make_gaussians(P, deg, seed=0)
-    target = synthetic.make_target(W, H).numpy()
-    args = (g.get_xyz.detach().numpy(), g.get_opacity.detach().numpy(), cam.world_view_transform.numpy(),
-            cam.full_proj_transform.numpy(), cam.camera_center.numpy(), np.zeros(3, np.float32), H, W,
-            np.tan(cam.FoVx / 2), np.tan(cam.FoVy / 2), 1.0, deg)
-    kw = dict(shs=g.get_features.detach().numpy(), scales=g.get_scaling.detach().numpy(),
-              rotations=g.get_rotation.detach().numpy())
-    times = []
-    t_start = time.perf_counter()
-    while True:
-        t0 = time.perf_counter()
-        f = oracle.forward(*args, **kw)
+    torch.set_num_threads(ncpu["nproc"])
+    threads = oracle.num_threads(mt=True)
+
+    def one(cfg, cam, g, target):
+        xyz, opac = g.get_xyz, g.get_opacity
+        feats = g.get_features
+        shs_view = feats.transpose(1, 2).view(-1, 3, (g.max_sh_degree + 1) ** 2)
+        dirs = xyz - cam.camera_center.repeat(feats.shape[0], 1)
+        dirs = dirs / dirs.norm(dim=1, keepdim=True)
+        colors = torch.clamp_min(train_step.eval_sh(g.active_sh_degree, shs_view, dirs) + 0.5, 0.0)
+        cov3D = train_step.covariance(g.get_scaling, 1.0, g.rotation)
+        f = oracle.forward(xyz.detach().numpy(), opac.detach().numpy(), cam.world_view_transform.numpy(),
+                           cam.full_proj_transform.numpy(), cam.camera_center.numpy(), np.zeros(3, np.float32),
+                           cam.image_height, cam.image_width, math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5), 1.0,
+                           g.active_sh_degree, colors_precomp=colors.detach().numpy(),
+                           cov3D_precomp=cov3D.detach().numpy(), mt=True)
+        if not cfg["backward"]:
+            return
         dL = (np.sign(f["color"] - target) / f["color"].size).astype(np.float32)  # L1 backward
-        oracle.backward(f, dL)
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > budget_s / 2 or len(times) >= 3:
-            break
-    med = sorted(times)[len(times) // 2]
-    return {"value": 1.0 / med, "unit": "train-iters/s", "cores": 1, "kind": "port",
-            "sample": f"{len(times)} full view(s) of the same workload (P={P}, {W}x{H}, SH{deg}) through the C oracle "
-                      f"(forward + L1 grad + backward), single thread; median {med:.2f} s/view"}
+        b = oracle.backward(f, dL)
+        torch.autograd.backward([xyz, colors, cov3D, opac],
+                                [torch.from_numpy(b[k]) for k in ("dmeans3D", "dcolors", "dcov3D", "dopacity")])
+
+    out = {}
+    t_all = time.perf_counter()
+    for name in configs:
+        cfg = synthetic.CONFIGS[name]
+        P, W, H, deg = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
+        cam = synthetic.make_camera(W, H, 0)
+        g = synthetic.make_gaussians(P, deg, seed=0).to("cpu", requires_grad=True)
+        target = synthetic.make_target(W, H, seed=1).numpy()
+        times = []
+        t_cfg = time.perf_counter()
+        for k in range(repeats + 1):
+            if time.perf_counter() - t_cfg > cap_s:
+                break
+            for p in g.params():
+                p.grad = None
+            t0 = time.perf_counter()
+            one(cfg, cam, g, target)
+            if k:  # the first run is the warm-up
+                times.append(time.perf_counter() - t0)
+        unit = "train-iters/s" if cfg["backward"] else "frames/s"
+        if len(times) < repeats:
+            out[name] = {"status": "timeout", "cap_s": cap_s, "runs": len(times)}
+            continue
+        med = sorted(times)[len(times) // 2]
+        out[name] = {"value": round(1.0 / med, 4), "unit": unit, "s_per_iter": round(med, 3),
+                     "work": "render -> L1 -> backward" if cfg["backward"] else "render (forward)",
+                     "gaussians": P, "width": W, "height": H, "sh_degree": deg}
+        del g
+    head = out.get("C", {})
+    return {"value": head.get("value"), "unit": "train-iters/s", "cores": threads, "kind": "port",
+            "nproc": ncpu["nproc"], "cpu_model": ncpu["model"], "torch_threads": torch.get_num_threads(),
+            "sample": f"config C (the headline workload) through the reference-shaped render() with "
+                      f"convert_SHs_python / compute_cov3D_python (torch) and the C oracle's OpenMP build as the "
+                      f"rasterizer, forward + L1 + backward on {threads} threads; median of {repeats} after 1 "
+                      f"warm-up; the configs table has A, B, E the same way ({time.perf_counter() - t_all:.0f} s)",
+            "configs": out}
 
 
 def main():
@@ -275,7 +343,7 @@ def main():
             del out
             line["config_E_render"] = render_rates("E", dev, args.render_steps, 3)
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(P, W, H, deg)
+            line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -56,7 +56,7 @@ enum gsr_status {
 };
 
 /* Tile footprint of a Gaussian (which of its bounding-rect tiles get a list
- * entry).  Not an upstream argument: RECT (0, the default) is upstream's
+ * entry).  Not an upstream argument: RECT (0, the struct's zero value) is upstream's
  * getRect footprint — every tile of the 3-sigma bounding rect, so num_rendered,
  * tiles_touched, the sorted (tile << 32 | depth) keys, point_list, ranges and
  * n_contrib are upstream's (rasterizer_impl.cu duplicateWithKeys /
@@ -65,7 +65,8 @@ enum gsr_status {
  * pixel of their tile skips, so image, radii, final_T and every gradient are
  * the same, with ~40 % fewer instances to sort and stream (config C: 8.0M ->
  * 4.9M); num_rendered, the lists and n_contrib then index the shorter lists.
- * Forward and backward of one render must use the same footprint. */
+ * Forward and backward of one render must use the same footprint.  The Python
+ * package defaults to TIGHT (of upstream's outputs only num_rendered differs). */
 enum gsr_footprint { GSR_FOOTPRINT_RECT = 0, GSR_FOOTPRINT_TIGHT = 1 };
 
 /* Inputs shared by forward and backward.  Mirrors the argument list of

@@ -31,6 +31,12 @@
  * forward (tests/test_oracle_autograd.py).  The blend/sort stages are pinned by
  * the analytic known-answer tests of SURVEY.md A.10 only.
  *
+ * Threads: liboracle.so (the checker) is single-threaded.  The same source
+ * built with -fopenmp (liboracle_mt.so, bench.py's CPU baseline on all host
+ * cores) runs the per-Gaussian loops, the per-tile blend loops and the sort in
+ * parallel; its forward is bit-identical to the single-threaded one, its
+ * render backward sums per-thread partial gradients (a different float order).
+ *
  * Floating point: compile with -ffp-contract=off.  The integer outputs
  * (radii, rects, tiles_touched, keys) are derived with the same operation
  * order as the HIP preprocess kernel, which is also built without
@@ -38,6 +44,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -231,6 +238,7 @@ int oracle_preprocess(int P, int D, int M, const float *means3D, const float *sc
     const float focal_x = W / (2.0f * tan_fovx);
     const unsigned gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
     int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
     for (int idx = 0; idx < P; idx++) {
         radii[idx] = 0;
         tiles_touched[idx] = 0;
@@ -300,6 +308,7 @@ int64_t oracle_inclusive_scan(int P, const uint32_t *in, uint32_t *out) {
 void oracle_duplicate_with_keys(int P, const float *means2D, const float *depths, const uint32_t *offsets,
                                 const int *radii, int W, int H, uint64_t *keys, uint32_t *values) {
     const unsigned gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+#pragma omp parallel for schedule(dynamic, 1024)
     for (int idx = 0; idx < P; idx++) {
         if (radii[idx] <= 0) continue;
         uint32_t off = (idx == 0) ? 0 : offsets[idx - 1];
@@ -326,9 +335,74 @@ static int kv_cmp(const void *a, const void *b) {
     return x->pos < y->pos ? -1 : (x->pos > y->pos);
 }
 
+#ifdef _OPENMP
+#include <omp.h>
+/* Threaded form of the same stable sort: a stable counting sort by tile (the
+ * key's high word; per-thread histograms over contiguous chunks), then every
+ * tile's run sorted by (key, emission position) — the qsort's order exactly. */
+static void sort_pairs_mt(int64_t n, const uint64_t *keys_in, const uint32_t *vals_in, uint64_t *keys_out,
+                          uint32_t *vals_out) {
+    uint32_t ntiles = 0;
+    for (int64_t i = 0; i < n; i++) {
+        const uint32_t t = (uint32_t)(keys_in[i] >> 32) + 1;
+        ntiles = t > ntiles ? t : ntiles;
+    }
+    const int nt = omp_get_max_threads();
+    int64_t *hist = (int64_t *)calloc((size_t)nt * ntiles + 1, sizeof(int64_t));
+    int64_t *start = (int64_t *)calloc((size_t)ntiles + 1, sizeof(int64_t));
+    kv_t *tmp = (kv_t *)malloc(sizeof(kv_t) * (size_t)(n > 0 ? n : 1));
+#pragma omp parallel num_threads(nt)
+    {
+        const int t = omp_get_thread_num();
+        const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+        int64_t *h = hist + (size_t)t * ntiles;
+        for (int64_t i = lo; i < hi; i++) h[keys_in[i] >> 32]++;
+#pragma omp barrier
+#pragma omp single
+        {
+            int64_t acc = 0;
+            for (uint32_t b = 0; b < ntiles; b++) {
+                start[b] = acc;
+                for (int u = 0; u < nt; u++) {
+                    const int64_t c = hist[(size_t)u * ntiles + b];
+                    hist[(size_t)u * ntiles + b] = acc;
+                    acc += c;
+                }
+            }
+            start[ntiles] = acc;
+        }
+        for (int64_t i = lo; i < hi; i++) {
+            kv_t *e = &tmp[h[keys_in[i] >> 32]++];
+            e->key = keys_in[i];
+            e->val = vals_in[i];
+            e->pos = (uint32_t)i;
+        }
+#pragma omp barrier
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t b = 0; b < (int64_t)ntiles; b++) {
+            const int64_t s0 = start[b], s1 = start[b + 1];
+            qsort(tmp + s0, (size_t)(s1 - s0), sizeof(kv_t), kv_cmp);
+            for (int64_t i = s0; i < s1; i++) {
+                keys_out[i] = tmp[i].key;
+                vals_out[i] = tmp[i].val;
+            }
+        }
+    }
+    free(tmp);
+    free(start);
+    free(hist);
+}
+#endif
+
 /* cub::DeviceRadixSort::SortPairs is stable: equal keys keep emission order. */
 void oracle_sort_pairs(int64_t n, const uint64_t *keys_in, const uint32_t *vals_in, uint64_t *keys_out,
                        uint32_t *vals_out) {
+#ifdef _OPENMP
+    if (omp_get_max_threads() > 1) {
+        sort_pairs_mt(n, keys_in, vals_in, keys_out, vals_out);
+        return;
+    }
+#endif
     kv_t *tmp = (kv_t *)malloc(sizeof(kv_t) * (size_t)(n > 0 ? n : 1));
     for (int64_t i = 0; i < n; i++) {
         tmp[i].key = keys_in[i];
@@ -366,6 +440,7 @@ void oracle_render_forward(const uint32_t *ranges, const uint32_t *point_list, i
                            const float *colors, const float *conic_opacity, float *final_T, uint32_t *n_contrib,
                            const float *bg, float *out_color) {
     const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ty++)
         for (int tx = 0; tx < gx; tx++) {
             const uint32_t *range = ranges + 2 * (ty * gx + tx);
@@ -408,15 +483,17 @@ void oracle_render_forward(const uint32_t *ranges, const uint32_t *point_list, i
 /* backward.cu renderCUDA: back-to-front replay; accumulates (float, in pixel
  * order) into dL_dmean2D [P][3], dL_dconic [P][4] (x,y,w used), dL_dopacity
  * [P], dL_dcolors [P][3].  Output arrays must be zeroed by the caller. */
-void oracle_render_backward(const uint32_t *ranges, const uint32_t *point_list, int W, int H, const float *bg,
-                            const float *means2D, const float *conic_opacity, const float *colors,
-                            const float *final_Ts, const uint32_t *n_contrib, const float *dL_dpixels,
-                            float *dL_dmean2D, float *dL_dconic, float *dL_dopacity, float *dL_dcolors) {
+static void render_backward_tiles(const uint32_t *ranges, const uint32_t *point_list, int W, int H, const float *bg,
+                                  const float *means2D, const float *conic_opacity, const float *colors,
+                                  const float *final_Ts, const uint32_t *n_contrib, const float *dL_dpixels,
+                                  float *dL_dmean2D, float *dL_dconic, float *dL_dopacity, float *dL_dcolors,
+                                  int tile_lo, int tile_step) {
     const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
-    for (int ty = 0; ty < gy; ty++)
-        for (int tx = 0; tx < gx; tx++) {
+    for (int tile = tile_lo; tile < gx * gy; tile += tile_step) {
+        const int ty = tile / gx, tx = tile % gx;
+        {
             const uint32_t *range = ranges + 2 * (ty * gx + tx);
             for (int ly = 0; ly < BLOCK_Y; ly++)
                 for (int lx = 0; lx < BLOCK_X; lx++) {
@@ -471,12 +548,54 @@ void oracle_render_backward(const uint32_t *ranges, const uint32_t *point_list, 
                     }
                 }
         }
+    }
+}
+
+void oracle_render_backward_p(int P, const uint32_t *ranges, const uint32_t *point_list, int W, int H,
+                              const float *bg, const float *means2D, const float *conic_opacity, const float *colors,
+                              const float *final_Ts, const uint32_t *n_contrib, const float *dL_dpixels,
+                              float *dL_dmean2D, float *dL_dconic, float *dL_dopacity, float *dL_dcolors) {
+#ifdef _OPENMP
+    const int nt = omp_get_max_threads();
+    if (nt > 1) {
+        /* each thread replays the tiles it takes into its own zeroed partials;
+         * the partials are then added in thread order */
+        const size_t per = (size_t)P * 11;
+        float *part = (float *)calloc(per * (size_t)nt, sizeof(float));
+#pragma omp parallel num_threads(nt)
+        {
+            const int t = omp_get_thread_num();
+            float *q = part + per * (size_t)t;
+            const int ntile = ((W + BLOCK_X - 1) / BLOCK_X) * ((H + BLOCK_Y - 1) / BLOCK_Y);
+#pragma omp for schedule(dynamic, 2)
+            for (int tile = 0; tile < ntile; tile++)  /* one tile per call */
+                render_backward_tiles(ranges, point_list, W, H, bg, means2D, conic_opacity, colors, final_Ts,
+                                      n_contrib, dL_dpixels, q, q + 3 * (size_t)P, q + 7 * (size_t)P,
+                                      q + 8 * (size_t)P, tile, ntile);
+#pragma omp for schedule(static)
+            for (int64_t i = 0; i < (int64_t)P; i++) {
+                for (int u = 0; u < nt; u++) {
+                    const float *r = part + per * (size_t)u;
+                    for (int c = 0; c < 3; c++) dL_dmean2D[3 * i + c] += r[3 * i + c];
+                    for (int c = 0; c < 4; c++) dL_dconic[4 * i + c] += r[3 * (size_t)P + 4 * i + c];
+                    dL_dopacity[i] += r[7 * (size_t)P + i];
+                    for (int c = 0; c < 3; c++) dL_dcolors[3 * i + c] += r[8 * (size_t)P + 3 * i + c];
+                }
+            }
+        }
+        free(part);
+        return;
+    }
+#endif
+    render_backward_tiles(ranges, point_list, W, H, bg, means2D, conic_opacity, colors, final_Ts, n_contrib,
+                          dL_dpixels, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolors, 0, 1);
 }
 
 /* backward.cu computeCov2DCUDA: dL/dconic -> dL/dcov3D and (assigned) dL/dmean3D. */
 void oracle_cov2d_backward(int P, const float *means, const int *radii, const float *cov3Ds, float h_x, float h_y,
                            float tan_fovx, float tan_fovy, const float *view_matrix, const float *dL_dconics,
                            float *dL_dmeans, float *dL_dcov) {
+#pragma omp parallel for schedule(static)
     for (int idx = 0; idx < P; idx++) {
         if (!(radii[idx] > 0)) continue;
         const float *c3 = cov3Ds + 6 * (size_t)idx;
@@ -669,6 +788,7 @@ void oracle_preprocess_backward(int P, int D, int M, const float *means, const i
                                 float scale_modifier, const float *proj, const float *campos,
                                 const float *dL_dmean2D, float *dL_dmeans, const float *dL_dcolor,
                                 const float *dL_dcov3D, float *dL_dsh, float *dL_dscale, float *dL_drot) {
+#pragma omp parallel for schedule(static)
     for (int idx = 0; idx < P; idx++) {
         if (!(radii[idx] > 0)) continue;
         f3 m = {means[3 * idx], means[3 * idx + 1], means[3 * idx + 2]};
@@ -729,4 +849,13 @@ void oracle_sh_grad_sum(int P, int nviews, int M, const float *means, const floa
     free(noclamp);
     free(dmean);
     free(dsh);
+}
+
+/* threads the parallel loops use (1 in the single-threaded checker build) */
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
 }

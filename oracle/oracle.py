@@ -27,27 +27,36 @@ import numpy as np
 
 _HERE = Path(__file__).resolve().parent
 _LIB_PATH = _HERE / "liboracle.so"
-_lib = None
+_LIB_MT_PATH = _HERE / "liboracle_mt.so"  # same source with OpenMP (bench.py's CPU baseline)
+_libs = {}
 
 BLOCK_X = 16
 BLOCK_Y = 16
 
 
 def build() -> Path:
-    """Compile liboracle.so with the committed Makefile (gcc only)."""
+    """Compile liboracle.so and liboracle_mt.so with the committed Makefile (gcc only)."""
     subprocess.run(["make", "-s", "-C", str(_HERE)], check=True)
     return _LIB_PATH
 
 
-def _load():
-    global _lib
-    if _lib is None:
-        if not _LIB_PATH.exists():
+def _load(mt: bool = False):
+    """The single-threaded checker library, or (mt) its OpenMP build."""
+    if mt not in _libs:
+        path = _LIB_MT_PATH if mt else _LIB_PATH
+        if not path.exists():
             build()
-        _lib = ctypes.CDLL(str(_LIB_PATH))
-        _lib.oracle_inclusive_scan.restype = ctypes.c_int64
-        _lib.oracle_preprocess.restype = ctypes.c_int
-    return _lib
+        lib = ctypes.CDLL(str(path))
+        lib.oracle_inclusive_scan.restype = ctypes.c_int64
+        lib.oracle_preprocess.restype = ctypes.c_int
+        lib.oracle_num_threads.restype = ctypes.c_int
+        _libs[mt] = lib
+    return _libs[mt]
+
+
+def num_threads(mt: bool = True) -> int:
+    """Threads the (mt) library's parallel loops use (OMP_NUM_THREADS)."""
+    return int(_load(mt).oracle_num_threads())
 
 
 def _p(a):
@@ -69,10 +78,11 @@ def _f32(a):
 
 def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx, tanfovy,
             scale_modifier=1.0, sh_degree=0, shs=None, colors_precomp=None, scales=None, rotations=None,
-            cov3D_precomp=None, prefiltered=False):
+            cov3D_precomp=None, prefiltered=False, mt=False):
     """Full forward. All array inputs are numpy (or array-likes); matrices are the
-    16-float row-major storage of the reference's transposed matrices."""
-    lib = _load()
+    16-float row-major storage of the reference's transposed matrices.  mt: the
+    OpenMP build (same results)."""
+    lib = _load(mt)
     means3D = _f32(means3D).reshape(-1, 3)
     P = means3D.shape[0]
     H, W = int(image_height), int(image_width)
@@ -146,14 +156,14 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height
                          cov3D_precomp=cov3D_precomp, viewmatrix=viewmatrix, projmatrix=projmatrix, campos=campos,
                          bg=bg, W=W, H=H, tanfovx=float(tanfovx), tanfovy=float(tanfovy),
                          scale_modifier=float(scale_modifier), sh_degree=int(sh_degree), M=M, colors=colors,
-                         point_list_full=point_list))
+                         point_list_full=point_list, mt=mt))
 
 
 def backward(state, dL_dout_color):
     """Full backward from the forward state; returns the 8 native gradients of
     ``_C.rasterize_gaussians_backward`` plus dL/dconic."""
-    lib = _load()
     inp = state["_in"]
+    lib = _load(inp.get("mt", False))
     P = inp["means3D"].shape[0]
     W, H, M = inp["W"], inp["H"], inp["M"]
     g = np.ascontiguousarray(np.asarray(dL_dout_color, np.float32).reshape(3, H, W))
@@ -161,7 +171,8 @@ def backward(state, dL_dout_color):
     dconic = np.zeros((P, 4), np.float32)
     dopacity = np.zeros((P, 1), np.float32)
     dcolors = np.zeros((P, 3), np.float32)
-    lib.oracle_render_backward(_p(state["ranges"]), _p(inp["point_list_full"]), ctypes.c_int(W), ctypes.c_int(H),
+    lib.oracle_render_backward_p(ctypes.c_int(P), _p(state["ranges"]), _p(inp["point_list_full"]), ctypes.c_int(W),
+                               ctypes.c_int(H),
                                _p(inp["bg"]), _p(state["means2D"]), _p(state["conic_opacity"]), _p(inp["colors"]),
                                _p(state["final_T"]), _p(state["n_contrib"]), _p(g), _p(dmean2D), _p(dconic),
                                _p(dopacity), _p(dcolors))

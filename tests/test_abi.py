@@ -152,10 +152,10 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
 def test_footprint_selector():
     from diff_gaussian_rasterization import _C, get_footprint, set_footprint
 
-    assert get_footprint() == "rect"  # upstream's footprint unless asked
-    prev = set_footprint("tight")
+    assert get_footprint() == "tight"  # package default; "rect" = upstream's lists
+    prev = set_footprint("rect")
     try:
-        assert prev == "rect" and get_footprint() == "tight"
+        assert prev == "tight" and get_footprint() == "rect"
         with pytest.raises(ValueError, match="footprint must be"):
             set_footprint("box")
     finally:
