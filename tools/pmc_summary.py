@@ -45,6 +45,27 @@ for k, cs in sorted(vals.items()):
     print(k)
     for c, x in sorted(line.items()):
         print(f"    {c:28s} {x:>16,.1f}" if isinstance(x, float) else f"    {c:28s} {x}")
+# multi-kernel stages: HBM bytes of one stage launch = per-dispatch means times the
+# dispatches of each kernel per launch.  The radix kernels serve both sorts; their
+# ITEMS template argument tells them apart (gsr_common.hpp tsort_items/dsort_items:
+# tile sort <8> at config C, <16> at E; depth sort <4> at C, <8> at E).
+# radix_digit_scan_kernel is shared and tiny (256 x blocks counters): its mean is
+# counted once per pass.
+def _mean_hbm(prefix):
+    for k, line in summary["kernels"].items():
+        if k.startswith(prefix) and "hbm_bytes_per_launch" in line:
+            return line["hbm_bytes_per_launch"]
+    return None
+
+
+titems = "16" if SUFFIX == "_E" else "8"
+parts = [(f"gsr::radix_upsweep_kernel<{titems}>", 2), (f"gsr::radix_downsweep_kernel<{titems}>", 2),
+         ("gsr::radix_digit_scan_kernel", 2), ("gsr::identify_ranges_kernel", 1)]
+got = [(_mean_hbm(k), n) for k, n in parts]
+if all(v is not None for v, _ in got):
+    summary["stages"]["tile_sort" + SUFFIX] = {
+        "hbm_bytes_per_launch": sum(v * n for v, n in got),
+        "kernel": " + ".join(f"{n} x {k}" for k, n in parts)}
 for st, rec in summary["stages"].items():
     frac = summary["kernels"].get(rec["kernel"], {}).get("valu_issue_frac")
     if frac is not None:
