@@ -100,9 +100,12 @@ def read_intermediates(geom, binning, img, P, W, H, I):
     return d
 
 
-def run_oracle(oracle, cam, g, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=None, python_branch=False):
+def run_oracle(oracle, cam, g, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=None, python_branch=False,
+               mt=False):
+    """mt: the oracle's OpenMP build (forward bit-identical; the render backward
+    adds per-thread partial gradients, a different float order) for full-size cases."""
     a = activated(g, python_branch, scale_modifier)
-    kw = dict(scale_modifier=scale_modifier, sh_degree=g.active_sh_degree)
+    kw = dict(scale_modifier=scale_modifier, sh_degree=g.active_sh_degree, mt=mt)
     if colors_precomp is None:
         kw["shs"] = a["shs"].numpy()
     else:

@@ -397,7 +397,7 @@ def test_config_c_full_size_parity(dev, oracle):
     in both footprints (one oracle run)."""
     cam, g = case(1_000_000, 1920, 1080, 3, seed=0)
     dL = random_dL(1080, 1920)
-    r = run_oracle(oracle, cam, g)
+    r = run_oracle(oracle, cam, g, mt=True)
     rb = oracle.backward(r, dL)
     for footprint in ("rect", "tight"):
         h = run_hip(cam, g, dev, dL=dL, footprint=footprint)
@@ -422,7 +422,7 @@ def test_config_e_full_size_forward_parity(dev, oracle):
     point_list, ranges; tight: their subset), the image and final_T within 1e-4 on
     every pixel, n_contrib bit-exact (rect)."""
     cam, g = case(5_000_000, 3840, 2160, 3, seed=0)
-    r = run_oracle(oracle, cam, g)
+    r = run_oracle(oracle, cam, g, mt=True)
     for footprint in ("rect", "tight"):
         h = run_hip(cam, g, dev, footprint=footprint)
         check_forward(h, r)

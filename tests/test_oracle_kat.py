@@ -124,3 +124,22 @@ def test_integer_stage_invariants(oracle):
     # mark_visible agrees with the near-plane cull
     vis = oracle.mark_visible(g.get_xyz.numpy(), cam.world_view_transform)
     assert np.all(vis[f["radii"] > 0])
+
+
+def test_threaded_oracle_matches_single_threaded(oracle):
+    """liboracle_mt.so (OpenMP; bench.py's CPU baseline and the full-size GPU parity
+    cases) renders bit-identically to the single-threaded checker; its backward sums
+    per-thread partials, so the gradients agree to float reordering."""
+    import numpy as np
+
+    from helpers import case, random_dL, run_oracle
+
+    cam, g = case(20_000, 200, 150, 3, seed=3, view=2)
+    dL = random_dL(150, 200)
+    a, b = run_oracle(oracle, cam, g), run_oracle(oracle, cam, g, mt=True)
+    for k in ("color", "radii", "keys", "point_list", "ranges", "n_contrib", "final_T", "means2D", "conic_opacity"):
+        assert np.array_equal(a[k], b[k]), k
+    ga, gb = oracle.backward(a, dL), oracle.backward(b, dL)
+    for k in ga:
+        den = max(float(np.linalg.norm(ga[k])), 1e-30)
+        assert float(np.linalg.norm(ga[k] - gb[k])) / den < 1e-5, k
