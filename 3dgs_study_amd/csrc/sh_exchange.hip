@@ -49,6 +49,11 @@ __global__ void __launch_bounds__(SX_THREADS) sh_from_colors_kernel(int P, int n
         const int deg = (int)r[3];
         const float *d3 = r + 4 + 3 * (size_t)li;
         const float d[3] = {d3[0], d3[1], d3[2]};
+        // a zero colour gradient (culled or clamped in this view) adds exactly
+        // nothing: skipped, so a mean at the view's camera centre (zero-length
+        // direction, NaN basis) cannot poison the sum; upstream gives a culled
+        // Gaussian no SH gradient at all
+        if (d[0] == 0.f && d[1] == 0.f && d[2] == 0.f) continue;
         const float ox = mx - r[0], oy = my - r[1], oz = mz - r[2];
         const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
         float b[16];

@@ -25,21 +25,30 @@ It also skips the 192 MB dsh write and the SH ``cat`` backward on every rank.
 
 Two modes for the all-reduced gradients:
   * overlapped (``overlap=True``, default): a post-accumulate-grad hook on every
-    parameter starts that gradient's all-reduce (async, on RCCL's stream) the
-    moment autograd has written it — xyz straight out of the rasterizer's
+    parameter counts the backwards that accumulate into it and, on the step's last
+    one (``views_per_step`` backwards per rank and step), starts that gradient's
+    all-reduce (async, on RCCL's stream) — xyz straight out of the rasterizer's
     backward, f_dc / f_rest after the SH ``cat`` backward, opacity / scaling /
-    rotation after their activation backwards — so the exchange of the big
-    f_rest block (76 % of the bytes) runs under the remaining backward kernels,
-    and no flat copy of the gradients is made.  ``__call__`` waits for them.
-  * flat (no pending hooks, e.g. gradients assigned by hand): the six gradients
-    are packed into ONE fp32 bucket and reduced with one call.
+    rotation after their activation backwards — so the exchange runs under the
+    remaining backward kernels and no flat copy is made.  ``__call__`` waits.
+  * flat: every gradient whose all-reduce did not start from a hook (no hook on a
+    replaced tensor, gradients assigned by hand, fewer backwards than announced) is
+    packed into ONE fp32 bucket and reduced with one call in ``__call__``.
+
+Parameters may be given as a zero-argument callable returning the current tensors
+(and ``sh`` likewise): the reference's densify / prune replaces every parameter with
+a new ``nn.Parameter`` (scene/gaussian_model.py cat_tensors_to_optimizer /
+_prune_optimizer), and ``__call__`` re-binds its hooks to whatever the callable
+returns, so the exchange follows the model instead of going stale.
 """
 from __future__ import annotations
 
-from typing import Sequence
+from typing import Callable, Sequence, Union
 
 import torch
 import torch.distributed as dist
+
+ParamSource = Union[Sequence[torch.Tensor], Callable[[], Sequence[torch.Tensor]]]
 
 
 def views_for_rank(rank: int, world: int, num_views: int) -> list:
@@ -50,34 +59,64 @@ def views_for_rank(rank: int, world: int, num_views: int) -> list:
 class GradAllReduce:
     """Sum the gradients of `params` over the process group.
 
-    ``sh=(xyz, f_dc, f_rest)`` (three of `params`) exchanges the SH gradient as
-    per-view colour gradients instead (module docstring); it engages when the group
-    has more than one rank, or always with ``sh_force=True`` (tests).  ``rebuild``
-    replaces the HIP kernel that turns gathered records into the SH gradients (CPU
-    tests only)."""
+    ``sh=(xyz, f_dc, f_rest)`` (three of `params`, or a callable returning them)
+    exchanges the SH gradient as per-view colour gradients instead (module
+    docstring); it engages when the group has more than one rank, or always with
+    ``sh_force=True`` (tests).  ``views_per_step``: backwards each rank runs per step
+    (the overlapped all-reduces start on the last one).  ``rebuild`` replaces the HIP
+    kernel that turns gathered records into the SH gradients (CPU tests only)."""
 
-    def __init__(self, params: Sequence[torch.Tensor], group=None, overlap: bool = True, sh=None,
-                 sh_force: bool = False, rebuild=None):
-        self.params = list(params)
+    def __init__(self, params: ParamSource, group=None, overlap: bool = True, sh=None, sh_force: bool = False,
+                 rebuild=None, views_per_step: int = 1):
+        if views_per_step < 1:
+            raise ValueError("views_per_step must be >= 1")
+        self._params_src = params
+        self._sh_src = sh
         self.group = group
-        self.numel = sum(p.numel() for p in self.params)
-        self._works = []
+        self.overlap = overlap
+        self.views_per_step = views_per_step
+        self._rebuild = rebuild
+        self._works = []       # (param, work) of the all-reduces started from hooks
         self._hooks = []
+        self._counts = {}      # id(param) -> backwards accumulated into it this step
         self._gathers = []
         self._sh = None
         self._prev_sink = None
-        if sh is not None and (sh_force or self._active()):
-            xyz, f_dc, f_rest = sh
-            if not any(f_dc is p for p in self.params) or not any(f_rest is p for p in self.params):
-                raise ValueError("sh=(xyz, f_dc, f_rest) must be among params")
-            self._sh = (xyz, f_dc, f_rest)
-            self._rebuild = rebuild
+        self._sink_installed = False
+        self._sh_on = sh is not None and (sh_force or self._active())
+        self._bind()
+        if self._sh_on:
             from diff_gaussian_rasterization import set_sh_grad_sink
             self._prev_sink = set_sh_grad_sink(self)
+            self._sink_installed = True
+
+    # ---- binding to the current parameter tensors
+    def _resolve(self):
+        params = list(self._params_src() if callable(self._params_src) else self._params_src)
+        sh = None
+        if self._sh_on:
+            sh = tuple(self._sh_src() if callable(self._sh_src) else self._sh_src)
+            xyz, f_dc, f_rest = sh
+            if not any(f_dc is p for p in params) or not any(f_rest is p for p in params):
+                raise ValueError("sh=(xyz, f_dc, f_rest) must be among params")
+        return params, sh
+
+    def _bind(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self.params, self._sh = self._resolve()
+        self.numel = sum(p.numel() for p in self.params)
         self._reduced = [p for p in self.params if self._sh is None or not any(p is q for q in self._sh[1:])]
-        if overlap:
+        self._counts = {id(p): 0 for p in self._reduced}
+        if self.overlap:
             for p in self._reduced:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._launch))
+
+    def _stale(self) -> bool:
+        params, sh = self._resolve()
+        return (len(params) != len(self.params) or any(a is not b for a, b in zip(params, self.params))
+                or (sh is not None and any(a is not b for a, b in zip(sh, self._sh))))
 
     @property
     def nbytes(self) -> int:
@@ -86,7 +125,7 @@ class GradAllReduce:
         n = sum(p.numel() for p in self._reduced) * 4
         if self._sh is not None:
             from diff_gaussian_rasterization import _C
-            n += _C.sh_record_floats(self._sh[0].size(0)) * 4
+            n += _C.sh_record_floats(self._sh[0].size(0)) * 4 * self.views_per_step
         return n
 
     @property
@@ -98,9 +137,19 @@ class GradAllReduce:
 
     # ---- the rasterizer's SH sink (diff_gaussian_rasterization.set_sh_grad_sink)
     def accepts(self, sh: torch.Tensor, means3D: torch.Tensor) -> bool:
+        """True when this backward's SH input is the bound model's.  With more than
+        one rank a mismatch raises: a silent local dsh would leave this rank's SH
+        gradient out of the exchange and the replicas would drift apart."""
+        if self._stale():  # the model's tensors were replaced (densify / prune): follow them
+            self._bind()
         xyz, f_dc, f_rest = self._sh
-        return (means3D.data_ptr() == xyz.data_ptr() and sh.size(0) == xyz.size(0)
-                and sh.size(1) == f_dc.size(1) + f_rest.size(1))
+        ok = (means3D.data_ptr() == xyz.data_ptr() and sh.size(0) == xyz.size(0)
+              and sh.size(1) == f_dc.size(1) + f_rest.size(1))
+        if not ok and self._active():
+            raise RuntimeError("GradAllReduce: the rasterizer's SH input is not the bound model's "
+                               f"(means3D {tuple(means3D.shape)} vs xyz {tuple(xyz.shape)}); pass params/sh as "
+                               "callables that return the current tensors")
+        return ok
 
     def record(self, P: int) -> torch.Tensor:
         from diff_gaussian_rasterization import _C
@@ -124,6 +173,8 @@ class GradAllReduce:
         for _, _, w in self._gathers:
             if w is not None:
                 w.wait()
+        # gathered buffers hold [rank 0 .. world-1] per push; with several views per
+        # rank the sum runs push by push (identical order on every rank)
         recs = torch.cat([o for o, _, _ in self._gathers]) if len(self._gathers) > 1 else self._gathers[0][0]
         nviews = sum(n for _, n, _ in self._gathers)
         self._gathers = []
@@ -141,38 +192,73 @@ class GradAllReduce:
                 p.grad.add_(g)
 
     def _launch(self, p: torch.Tensor) -> None:
-        if self._active():
-            self._works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        k = id(p)
+        if k not in self._counts:
+            return
+        self._counts[k] += 1
+        if self._counts[k] > self.views_per_step:
+            raise RuntimeError(f"GradAllReduce: {self._counts[k]} backwards accumulated into a parameter in one step "
+                               f"(views_per_step={self.views_per_step}); its all-reduce already started")
+        if self._counts[k] == self.views_per_step and self._active():
+            self._works.append((p, dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
 
     def remove_hooks(self) -> None:
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        if self._sh is not None:
+        if self._sink_installed:
             from diff_gaussian_rasterization import set_sh_grad_sink
             set_sh_grad_sink(self._prev_sink)
+            self._sink_installed = False
             self._sh = None
+            self._sh_on = False
 
     def __call__(self):
-        """Finish this step's exchange: wait for the overlapped all-reduces, or (none
-        pending) reduce the current gradients as one flat bucket; then rebuild the SH
-        gradients from the gathered colour gradients (SH exchange on)."""
-        if self._works:
-            for w in self._works:
-                w.wait()
-            self._works = []
-            if self._sh is not None:
-                self._finish_sh()
-            return None
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self._reduced]
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        if self._active():
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-        off = 0
-        for p in self._reduced:
-            n = p.numel()
-            p.grad = flat[off:off + n].view_as(p)
-            off += n
+        """Finish this step's exchange: wait for the overlapped all-reduces, reduce
+        every other gradient as one flat bucket, then rebuild the SH gradients from
+        the gathered colour gradients (SH exchange on).  Returns the flat bucket (or
+        None when every gradient went through a hook)."""
+        done = set()
+        for p, w in self._works:
+            w.wait()
+            done.add(id(p))
+        self._works = []
+        rest = [p for p in self._reduced if id(p) not in done]
+        flat = None
+        if rest:
+            grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in rest]
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            if self._active():
+                dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            off = 0
+            for p in rest:
+                n = p.numel()
+                p.grad = flat[off:off + n].view_as(p)
+                off += n
         if self._sh is not None:
             self._finish_sh()
+        for k in self._counts:
+            self._counts[k] = 0
+        if self._stale():  # re-bind the hooks to the model's current tensors for the next step
+            self._bind()
         return flat
+
+
+@torch.no_grad()
+def reduce_densification_stats(xyz_gradient_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
+                               group=None) -> None:
+    """Combine the ranks' densification statistics in place before a densify step:
+    SUM of the accumulated screen-space gradient norms and of the visibility counts,
+    MAX of the largest screen radii (scene/gaussian_model.py:565-581 accumulates them
+    per view; train.py:126-127 and :130-136 use them), so every rank densifies and
+    prunes the same Gaussians and the replicas stay identical."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return
+    both = torch.cat([xyz_gradient_accum.reshape(-1), denom.reshape(-1)])
+    w1 = dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group, async_op=True)
+    w2 = dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX, group=group, async_op=True)
+    w1.wait()
+    w2.wait()
+    n = xyz_gradient_accum.numel()
+    xyz_gradient_accum.copy_(both[:n].view_as(xyz_gradient_accum))
+    denom.copy_(both[n:].view_as(denom))

@@ -79,11 +79,11 @@ class FusedAdam:
 
     @torch.no_grad()
     def step(self):
+        """Validate every segment first, then advance the step counts and launch, so a
+        rejected call leaves no parameter's state advanced."""
         lib = _C.load_library()
         segs = (_C.GsrAdamSegment * _C.ADAM_MAX_SEGS)()
-        n = 0
-        step = None
-        dev = None
+        todo = []
         for g in self.param_groups:
             for p in g["params"]:
                 if p.grad is None:
@@ -91,20 +91,24 @@ class FusedAdam:
                 _cuda(p, "FusedAdam")
                 if not (p.is_contiguous() and p.grad.is_contiguous()):
                     raise RuntimeError("FusedAdam: parameters and gradients must be contiguous")
-                st = self.state.get(p)
-                if st is None:
-                    st = self.state[p] = {"step": 0, "exp_avg": torch.zeros_like(p),
-                                          "exp_avg_sq": torch.zeros_like(p)}
-                st["step"] += 1
-                if step is not None and st["step"] != step:
-                    raise RuntimeError("FusedAdam: parameters at different step counts")
-                step, dev = st["step"], p.device
-                segs[n] = _C.GsrAdamSegment(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
-                                            st["exp_avg_sq"].data_ptr(), p.numel(), float(g["lr"]))
-                n += 1
-        if n:
-            _C._check(lib.gsr_adam_step(segs, n, step, self.betas[0], self.betas[1], self.eps, _C._stream(dev)),
-                      "gsr_adam_step")
+                todo.append((g, p))
+        if len(todo) > _C.ADAM_MAX_SEGS:
+            raise RuntimeError(f"FusedAdam: at most {_C.ADAM_MAX_SEGS} tensors per launch")
+        steps = {self.state[p]["step"] if p in self.state else 0 for _, p in todo}
+        if len(steps) > 1:
+            raise RuntimeError("FusedAdam: parameters at different step counts")
+        if not todo:
+            return
+        step = steps.pop() + 1
+        for n, (g, p) in enumerate(todo):
+            st = self.state.get(p)
+            if st is None:
+                st = self.state[p] = {"step": 0, "exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)}
+            st["step"] = step
+            segs[n] = _C.GsrAdamSegment(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
+                                        st["exp_avg_sq"].data_ptr(), p.numel(), float(g["lr"]))
+        _C._check(lib.gsr_adam_step(segs, len(todo), step, self.betas[0], self.betas[1], self.eps,
+                                    _C._stream(todo[0][1].device)), "gsr_adam_step")
 
     def zero_grad(self, set_to_none: bool = True):
         for g in self.param_groups:
@@ -125,6 +129,12 @@ def densify_stats(radii: torch.Tensor, viewspace_grad: torch.Tensor, max_radii2D
                  (xyz_gradient_accum, "xyz_gradient_accum"), (denom, "denom")):
         _cuda(t, f"densify_stats({n})")
     P = radii.shape[0]
+    for t, n, shape in ((max_radii2D, "max_radii2D", (P,)), (xyz_gradient_accum, "xyz_gradient_accum", (P, 1)),
+                        (denom, "denom", (P, 1))):
+        # updated in place through their data pointers: a strided view would be misread
+        if not t.is_contiguous() or t.dtype != torch.float32 or t.numel() != P:
+            raise RuntimeError(f"densify_stats: {n} must be a contiguous float32 tensor of {P} elements "
+                               f"(shape {shape}), got {tuple(t.shape)} {t.dtype}")
     vg = viewspace_grad.contiguous()
     _C._check(lib.gsr_densify_stats(P, radii.contiguous().data_ptr(), vg.data_ptr(), vg.shape[1],
                                     max_radii2D.data_ptr(), xyz_gradient_accum.data_ptr(), denom.data_ptr(),

@@ -215,6 +215,13 @@ class TrainState:
                 group["lr"] = self.xyz_scheduler(iteration)
                 return group["lr"]
 
+    def reduce_densification_stats(self, group=None):
+        """View-parallel: SUM / SUM / MAX the per-rank statistics over the group before a
+        densify step (multiview.reduce_densification_stats)."""
+        import multiview
+
+        multiview.reduce_densification_stats(self.xyz_gradient_accum, self.denom, self.max_radii2D, group)
+
     @torch.no_grad()
     def densification_stats(self, out: dict):
         radii, vis, vsp = out["radii"], out["visibility_filter"], out["viewspace_points"]
@@ -229,11 +236,18 @@ class TrainState:
 
 
 def full_train_step(iteration: int, camera, gaussians, state: TrainState, target: torch.Tensor,
-                    bg: torch.Tensor) -> torch.Tensor:
+                    bg: torch.Tensor, reducer=None) -> torch.Tensor:
     """One iteration of train.py:86-141 without logging, checkpoints and the periodic
     densify/prune/opacity reset: lr schedule, render, L1 + lambda (1 - SSIM), backward,
     densification statistics, Adam step, zero_grad.  ``state.fused`` selects the HIP
-    loss/Adam/statistics kernels (train_ops.py) over the reference's torch ops."""
+    loss/Adam/statistics kernels (train_ops.py) over the reference's torch ops.
+
+    View-parallel: ``reducer`` (multiview.GradAllReduce over the
+    process group) finishes the gradient exchange started inside the backward before
+    the optimizer step, so every rank steps on the sum of all ranks' views and the
+    replicas stay identical; ``camera``/``target`` are this rank's view.  The
+    densification statistics stay per rank until a densify step combines them
+    (TrainState.reduce_densification_stats)."""
     state.update_learning_rate(iteration)
     out = render(camera, gaussians, bg)
     image = out["render"]
@@ -245,6 +259,8 @@ def full_train_step(iteration: int, camera, gaussians, state: TrainState, target
     else:
         loss = (1.0 - lam) * l1_loss(image, target) + lam * (1.0 - ssim(image, target))
     loss.backward()
+    if reducer is not None:
+        reducer()
     with torch.no_grad():
         if iteration < state.opt["densify_until_iter"]:
             state.densification_stats(out)

@@ -841,8 +841,13 @@ void oracle_sh_grad_sum(int P, int nviews, int M, const float *means, const floa
     for (size_t i = 0; i < (size_t)P * M * 3; i++) dsh_sum[i] = 0.f;
     for (int v = 0; v < nviews; v++) {
         memset(dsh, 0, (size_t)P * M * 3 * sizeof(float));
-        for (int i = 0; i < P; i++)
-            sh_backward(i, degs[v], M, means, campos + 3 * v, zeros_sh, noclamp, drgb + (size_t)v * P * 3, dmean, dsh);
+        const float *d = drgb + (size_t)v * P * 3;
+        for (int i = 0; i < P; i++) {
+            /* a view whose colour gradient is zero (culled, clamped) adds nothing; upstream
+             * never evaluates the basis for a culled Gaussian (NaN at the camera centre) */
+            if (d[3 * i] == 0.f && d[3 * i + 1] == 0.f && d[3 * i + 2] == 0.f) continue;
+            sh_backward(i, degs[v], M, means, campos + 3 * v, zeros_sh, noclamp, d, dmean, dsh);
+        }
         for (size_t i = 0; i < (size_t)P * M * 3; i++) dsh_sum[i] += dsh[i];
     }
     free(zeros_sh);

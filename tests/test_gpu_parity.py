@@ -202,8 +202,17 @@ def check_forward(h, r, rgb_from_sh=True):
             assert t_flip_pixel(r, int(x), int(y), W, int(h["n_contrib"][y, x])), \
                 f"n_contrib differs at ({x},{y}): {h['n_contrib'][y, x]} vs {r['n_contrib'][y, x]}, unexplained"
     else:
-        same = (last_contributor_ids(h, W, H) == last_contributor_ids(r, W, H)).mean()
-        assert same == 1.0, f"last contributor equal on only {same:.6f} of pixels"
+        # the same Gaussian is each pixel's last contributor, up to the same rare,
+        # explained T-termination flips (n_contrib indexes each implementation's own list)
+        ids_h, ids_r = last_contributor_ids(h, W, H), last_contributor_ids(r, W, H)
+        bad = np.argwhere(ids_h != ids_r)
+        assert len(bad) <= max(2, 2e-6 * ids_h.size), f"last contributor differs at {len(bad)} pixels"
+        gx = (W + 15) // 16
+        for y, x in bad:
+            s0, e0 = r["ranges"][(y // 16) * gx + x // 16]
+            pos = np.flatnonzero(r["point_list"][s0:e0] == ids_h[y, x]) if ids_h[y, x] >= 0 else np.zeros(0)
+            n_other = int(pos[0]) + 1 if len(pos) else 0
+            assert t_flip_pixel(r, int(x), int(y), W, n_other), f"last contributor differs at ({x},{y}), unexplained"
     return err
 
 

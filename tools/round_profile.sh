@@ -1,19 +1,22 @@
 #!/bin/bash
-# Round deliverables on the box: GPU parity tests (all, incl. slow), the default
-# benchmark line (with the CPU baseline), the rocprofv3 kernel trace of config C
-# and E, and the PMC passes of config C and E.  usage: bash tools/round_profile.sh TAG [skip-tests]
+# Round deliverables on the box: the default benchmark line (with the CPU
+# baseline), the rocprofv3 kernel trace of config C and E, the PMC passes of
+# config C and E, then the GPU parity tests (all, incl. slow).
+# usage: bash tools/round_profile.sh TAG [skip-tests]
 set -o pipefail
 TAG=${1:-round}
 mkdir -p gpurun_out
-if [ "${2:-}" != "skip-tests" ]; then
-  timeout -k 10 1200 python -u -m pytest tests/ -v -m gpu -p no:cacheprovider -x --timeout 120 --timeout-method thread \
-      > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
-  tail -2 gpurun_out/${TAG}_tests.log
-fi
 timeout -k 10 600 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench.log; exit 1; }
 grep '"metric"' gpurun_out/${TAG}_bench.log | cut -c1-300
 bash tools/prof.sh ${TAG}_C || exit 1
 bash tools/prof.sh ${TAG}_E --config E || exit 1
 bash tools/pmc.sh ${TAG} > /dev/null || exit 1
 PMC_ARGS="--config E" PMC_SUFFIX="_E --merge" bash tools/pmc.sh ${TAG} > /dev/null || exit 1
-echo done
+echo profiles done
+if [ "${2:-}" != "skip-tests" ]; then
+  timeout -k 10 1000 python -u -m pytest tests/ -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread \
+      > gpurun_out/${TAG}_tests.log 2>&1
+  rc=$?
+  tail -4 gpurun_out/${TAG}_tests.log
+  exit $rc
+fi
