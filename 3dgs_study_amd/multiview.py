@@ -193,7 +193,7 @@ class GradAllReduce:
 
     def _launch(self, p: torch.Tensor) -> None:
         k = id(p)
-        if k not in self._counts:
+        if k not in self._counts or not self._active():  # one rank: nothing to exchange
             return
         self._counts[k] += 1
         if self._counts[k] > self.views_per_step:
@@ -223,6 +223,11 @@ class GradAllReduce:
             w.wait()
             done.add(id(p))
         self._works = []
+        if self._stale():
+            # the model's tensors were replaced since the hooks were bound (densify /
+            # prune): their gradients go through the flat bucket this step, and the
+            # hooks move to them for the next
+            self._bind()
         rest = [p for p in self._reduced if id(p) not in done]
         flat = None
         if rest:
@@ -239,8 +244,6 @@ class GradAllReduce:
             self._finish_sh()
         for k in self._counts:
             self._counts[k] = 0
-        if self._stale():  # re-bind the hooks to the model's current tensors for the next step
-            self._bind()
         return flat
 
 

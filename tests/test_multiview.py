@@ -334,3 +334,333 @@ def test_sh_grad_from_colors_kernel_vs_oracle(dev, oracle):
         got = dc.cpu().numpy() if rest is None else np.concatenate([dc.cpu().numpy(), rest.cpu().numpy()], axis=1)
         err = np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30)
         assert err <= 1e-6, (M, err)
+
+
+# ---------------------------------------------------------------- several views per rank, re-binding, training
+def _loss(params, view):
+    """A stand-in for one view's render -> loss: view-dependent weights per parameter."""
+    g = torch.Generator().manual_seed(1000 + view)
+    return sum((torch.randn(p.shape, generator=g) * p * p).sum() for p in params)
+
+
+def _shapes(P=6):
+    return [(P, 3), (P, 1, 3), (P, 15, 3), (P, 1), (P, 3), (P, 4)]
+
+
+def _views_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce, views_for_rank
+
+    torch.manual_seed(0)
+    params = [torch.randn(s, requires_grad=True) for s in _shapes()]
+    views = views_for_rank(rank, world, 4)
+    ar = GradAllReduce(params, views_per_step=len(views))
+    for v in views:  # two backwards per rank: the all-reduces start on the second
+        _loss(params, v).backward()
+    pending = len(ar._works)
+    ar()
+    out[rank] = ([p.grad.clone() for p in params], pending)
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+def test_two_views_per_rank_overlapped_gloo_world2():
+    """with several backwards per step the hooks start each all-reduce on the
+    step's last backward only; every rank ends with the sum over all 4 views."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_views_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    torch.manual_seed(0)
+    params = [torch.randn(s, requires_grad=True) for s in _shapes()]
+    for v in range(4):
+        _loss(params, v).backward()
+    (g0, n0), (g1, n1) = res[0], res[1]
+    assert n0 == n1 == 6
+    for a, b, p in zip(g0, g1, params):
+        assert torch.equal(a, b)
+        torch.testing.assert_close(a, p.grad, rtol=1e-6, atol=1e-6)
+
+
+def _rebind_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    model = {"params": [torch.randn(s, requires_grad=True) for s in _shapes()]}
+    ar = GradAllReduce(lambda: model["params"])
+    res = []
+    for step in range(3):
+        if step == 1:  # densify: every parameter replaced by a longer one (cat_tensors_to_optimizer)
+            model["params"] = [torch.cat([p.detach(), p.detach()[:2] * 0.5]).requires_grad_(True)
+                               for p in model["params"]]
+        _loss(model["params"], 10 * step + rank).backward()
+        hooked = len(ar._works)
+        ar()
+        res.append(([p.grad.clone() for p in model["params"]], hooked))
+        for p in model["params"]:
+            p.grad = None
+    out[rank] = res
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+def test_exchange_follows_replaced_parameters_gloo_world2():
+    """after a densify step replaces every parameter, the exchange keeps
+    summing over the ranks (flat bucket on the step of the swap, hooks re-bound for
+    the next) instead of reducing the stale tensors."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_rebind_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    torch.manual_seed(0)
+    params = [torch.randn(s, requires_grad=True) for s in _shapes()]
+    for step in range(3):
+        if step == 1:
+            params = [torch.cat([p.detach(), p.detach()[:2] * 0.5]).requires_grad_(True) for p in params]
+        for r in (0, 1):
+            _loss(params, 10 * step + r).backward()
+        (g0, h0), (g1, h1) = res[0][step], res[1][step]
+        assert h0 == h1 == (0 if step == 1 else 6), (step, h0)  # no hooks on the fresh tensors yet
+        for a, b, p in zip(g0, g1, params):
+            assert torch.equal(a, b) and a.shape == p.shape
+            torch.testing.assert_close(a, p.grad, rtol=1e-6, atol=1e-6)
+        for p in params:
+            p.grad = None
+
+
+def _train_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    params = [torch.randn(s, requires_grad=True) for s in _shapes()]
+    opt = torch.optim.Adam([{"params": [p], "lr": 0.01 * (i + 1)} for i, p in enumerate(params)], eps=1e-15)
+    ar = GradAllReduce(params)
+    for step in range(4):
+        _loss(params, 2 * step + rank).backward()
+        ar()  # exchange before the optimizer step (train_step.full_train_step's order)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    out[rank] = [p.detach().clone() for p in params]
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+def test_view_parallel_training_keeps_replicas_identical_gloo_world2():
+    """N > 1 training: exchange then Adam on every rank; after 4 steps the replicas are
+    bit-identical and equal a single process stepping on the summed gradients."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_train_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    torch.manual_seed(0)
+    params = [torch.randn(s, requires_grad=True) for s in _shapes()]
+    opt = torch.optim.Adam([{"params": [p], "lr": 0.01 * (i + 1)} for i, p in enumerate(params)], eps=1e-15)
+    for step in range(4):
+        grads = []
+        for r in (0, 1):
+            _loss(params, 2 * step + r).backward()
+            grads.append([p.grad.clone() for p in params])
+            for p in params:
+                p.grad = None
+        for p, a, b in zip(params, *grads):
+            p.grad = a + b
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    for a, b, p in zip(res[0], res[1], params):
+        assert torch.equal(a, b)
+        assert torch.equal(a, p.detach())
+
+
+def _stats_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import reduce_densification_stats
+
+    P = 7
+    g = torch.Generator().manual_seed(rank)
+    acc = torch.rand(P, 1, generator=g)
+    den = torch.randint(0, 3, (P, 1), generator=g).float()
+    mx = torch.rand(P, generator=g) * 10
+    reduce_densification_stats(acc, den, mx)
+    out[rank] = (acc, den, mx)
+    dist.destroy_process_group()
+
+
+def test_densification_stats_reduce_sum_sum_max_gloo_world2():
+    """scene/gaussian_model.py:565-581 statistics combined over the ranks before a
+    densify step: SUM, SUM, MAX — identical on every rank."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_stats_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    loc = []
+    for r in (0, 1):
+        g = torch.Generator().manual_seed(r)
+        loc.append((torch.rand(7, 1, generator=g), torch.randint(0, 3, (7, 1), generator=g).float(),
+                    torch.rand(7, generator=g) * 10))
+    for r in (0, 1):
+        acc, den, mx = res[r]
+        assert torch.equal(acc, loc[0][0] + loc[1][0])
+        assert torch.equal(den, loc[0][1] + loc[1][1])
+        assert torch.equal(mx, torch.maximum(loc[0][2], loc[1][2]))
+
+
+def _foreign_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    P, M = 9, 16
+    params = [torch.randn(s, requires_grad=True) for s in _shapes(P)]
+    ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), rebuild=lambda *a: None)
+    try:
+        ar.accepts(torch.empty(P + 1, M, 3), torch.empty(P + 1, 3))
+        out[rank] = "accepted"
+    except RuntimeError as e:
+        out[rank] = str(e)
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+def test_sh_sink_refuses_a_foreign_model_with_several_ranks():
+    """with more than one rank, a backward whose SH input is not the bound
+    model raises instead of silently keeping a local dsh."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_foreign_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    for r in (0, 1):
+        assert "not the bound model" in res[r], res[r]
+
+
+# ---------------------------------------------------------------- on the GPU: training steps, config D
+def _gpu_train_worker(rank, world, port, out, sh_exchange):
+    _init(rank, world, port)
+    import synthetic
+    import train_step
+    from multiview import GradAllReduce
+
+    dev = torch.device("cuda:0")
+    cam = synthetic.make_camera(160, 120, view=rank).to(dev)
+    g = synthetic.make_gaussians(20_000, 3, seed=0).to(dev, requires_grad=True)
+    target = synthetic.make_target(160, 120).to(dev)
+    st = train_step.TrainState(g, spatial_lr_scale=6.6, fused=True)
+    reducer = GradAllReduce(g.params, sh=(lambda: g.params()[:3]) if sh_exchange else None)
+    for it in range(1, 4):
+        train_step.full_train_step(it, cam, g, st, target, torch.zeros(3, device=dev), reducer=reducer)
+    torch.cuda.synchronize()
+    out[rank] = [p.detach().cpu() for p in g.params()]
+    reducer.remove_hooks()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sh_exchange", [False, True], ids=["allreduce", "sh_colour_exchange"])
+def test_view_parallel_full_train_step_keeps_replicas_identical(dev, sh_exchange):
+    """Two ranks (gloo, sharing cuda:0) run three reference training iterations
+    (train.py:86-141: render, L1 + D-SSIM, backward, exchange, fused Adam) on views 0
+    and 1: the replicas stay bit-identical and match one process that steps on the sum
+    of the two views' gradients."""
+    import synthetic
+    import train_step
+
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_gpu_train_worker, args=(2, port, out, sh_exchange), nprocs=2, join=True)
+        res = dict(out)
+    g = synthetic.make_gaussians(20_000, 3, seed=0).to(dev, requires_grad=True)
+    p0 = [p.detach().cpu().clone() for p in g.params()]
+    target = synthetic.make_target(160, 120).to(dev)
+    st = train_step.TrainState(g, spatial_lr_scale=6.6, fused=True)
+    cams = [synthetic.make_camera(160, 120, view=v).to(dev) for v in (0, 1)]
+    for it in range(1, 4):
+        st.update_learning_rate(it)
+        grads = []
+        for cam in cams:
+            for p in g.params():
+                p.grad = None
+            out_ = train_step.render(cam, g, torch.zeros(3, device=dev))
+            import train_ops
+            train_ops.l1_ssim_loss(out_["render"], target, 0.2).backward()
+            grads.append([p.grad.clone() for p in g.params()])
+        with torch.no_grad():
+            for p, a, b in zip(g.params(), *grads):
+                p.grad = a + b
+            st.optimizer.step()
+            st.optimizer.zero_grad(set_to_none=True)
+    ref = [p.detach().cpu() for p in g.params()]
+    for a, b, r, q in zip(res[0], res[1], ref, p0):
+        assert torch.equal(a, b)  # replicas identical
+        rel = ((a - q) - (r - q)).norm() / (r - q).norm().clamp_min(1e-30)
+        assert rel < 1e-4, float(rel)
+
+
+def _config_d_worker(rank, world, port, out, sh_exchange, path):
+    _init(rank, world, port)
+    import hashlib
+
+    import synthetic
+    import train_step
+    from multiview import GradAllReduce
+
+    dev = torch.device("cuda:0")
+    cfg = synthetic.CONFIGS["C"]
+    cam = synthetic.make_camera(cfg["W"], cfg["H"], view=rank).to(dev)
+    g = synthetic.make_gaussians(cfg["P"], cfg["sh_degree"], seed=0).to(dev, requires_grad=True)
+    target = synthetic.make_target(cfg["W"], cfg["H"], seed=1).to(dev)
+    params = g.params()
+    reducer = GradAllReduce(params, sh=(params[0], params[1], params[2]) if sh_exchange else None)
+    train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
+    reducer()
+    grads = [p.grad.detach().cpu().contiguous() for p in params]
+    h = hashlib.sha256()
+    for x in grads:
+        h.update(x.numpy().tobytes())
+    out[rank] = h.hexdigest()
+    if rank == 0:
+        torch.save(grads, path)
+    reducer.remove_hooks()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("sh_exchange", [False, True], ids=["allreduce", "sh_colour_exchange"])
+def test_config_d_eight_ranks_on_one_gpu(dev, sh_exchange, tmp_path):
+    """Config D's workload (1M Gaussians, 1920x1080, views 0-7, one per rank) with 8
+    ranks over gloo sharing cuda:0 — the exchange code path of the RCCL run, which the
+    1-GPU box cannot measure: every rank ends with bit-identical leaf gradients, and
+    they match the sequential sum of the 8 single-view gradients (rel-L2 1e-5)."""
+    import synthetic
+    import train_step
+
+    port = _free_port()
+    path = tmp_path / "rank0_grads.pt"
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_config_d_worker, args=(8, port, out, sh_exchange, str(path)), nprocs=8, join=True)
+        res = dict(out)
+    assert len(set(res.values())) == 1, "ranks disagree"
+    got = torch.load(path, weights_only=True)
+    cfg = synthetic.CONFIGS["C"]
+    g = synthetic.make_gaussians(cfg["P"], cfg["sh_degree"], seed=0).to(dev, requires_grad=True)
+    target = synthetic.make_target(cfg["W"], cfg["H"], seed=1).to(dev)
+    total = None
+    for view in range(8):
+        for p in g.params():
+            p.grad = None
+        cam = synthetic.make_camera(cfg["W"], cfg["H"], view=view).to(dev)
+        train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
+        grads = [p.grad.detach().clone() for p in g.params()]
+        total = grads if total is None else [a + b for a, b in zip(total, grads)]
+    for a, ref in zip(got, total):
+        ref = ref.cpu()
+        rel = (a - ref).norm() / ref.norm().clamp_min(1e-30)
+        assert rel < 1e-5, float(rel)
