@@ -66,23 +66,29 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
 // `alpha < 1/255` skip.  The blend loops evaluate power as d^T conic' d
 // (conic' = -conic/2, contracted) and exp in hardware (v_exp_f32 of
 // power * log2 e): both within a few ulp of upstream's float expression and
-// libm's expf.  Where that could move a skip decision — alpha within 2^-12
-// relative of 1/255 (the combined error is below 2^-16), or a positive power
-// (the conic is positive definite, so only rounding makes one) — the pair is
-// redone exactly as the CPU restatement does it: upstream's expression in
-// upstream's operation order without contraction, and exp in double rounded
-// once (the correctly rounded expf, which libm's expf returns except within
-// 0.002 ulp of a rounding tie).  So every skip decision, and with it
-// n_contrib, matches the oracle's.  The branch is lane-masked and taken for
-// ~1e-4 of the pairs; the forward and backward share it (same decisions).
-struct BlendG {
-    float power, G;
-};
+// the correctly rounded expf.  Where that could move a skip decision — alpha
+// within 2^-12 relative of 1/255 (the combined error is below 2^-16), or a
+// positive power (the conic is positive definite, so only rounding makes one)
+// — the pair is redone exactly as the CPU restatement does it (blend_fix):
+// upstream's expression in upstream's operation order without contraction,
+// and exp in double rounded once (the correctly rounded expf).  So every skip
+// decision, and with it n_contrib, matches the oracle's.  The loops test the
+// flags of both Gaussians of an iteration with ONE wave-uniform branch
+// (ballot), taken for ~1e-4 of the pairs: a per-lane branch around each
+// Gaussian cost render_fwd 20 % and render_bwd 7 % (exec-mask juggling that
+// broke the two Gaussians' interleaving); this form costs 15 % / 6 % (config C:
+// 132 -> 152 us, 247 -> 261 us; of that the positive-power test is 8 / 3 us and
+// the double-precision call ~0 / 3 us).  The forward and backward share the
+// decisions bit for bit.
+__device__ __forceinline__ bool blend_near(float power, float opacity_times_G) {
+    return power > 0.0f || fabsf(opacity_times_G * 255.0f - 1.0f) < 0x1p-12f;
+}
 // exp(x) for |x| <= 16 in double, Taylor to degree 13 on |r| <= ln2/2
-// (truncation < 2^-55 relative), rounded once to float.  Not inlined: the
-// rarely taken re-check then adds a call instead of its double-precision
-// registers to every iteration of the blend loops (inlined, the library exp
-// cost render_fwd 54 -> 73 VGPRs, render_bwd 68 -> 92).
+// (truncation < 2^-55 relative), rounded once to float (equal to the correctly
+// rounded exp for every float in [-16, 1]).  Not inlined: the rarely taken
+// re-check then adds a call instead of its double-precision registers to
+// every iteration of the blend loops (inlined, the library exp cost
+// render_fwd 54 -> 73 VGPRs, render_bwd 68 -> 92).
 __device__ __attribute__((noinline)) float exp_rn_f32(float x) {
     const double xd = (double)x;
     const double n = __builtin_rint(xd * 1.4426950408889634);
@@ -103,16 +109,12 @@ __device__ __attribute__((noinline)) float exp_rn_f32(float x) {
     p = __builtin_fma(p, r, 1.0);
     return (float)__builtin_ldexp(p, (int)n);
 }
-__device__ __forceinline__ BlendG blend_g(float pw, float dx, float dy, float ca, float cb, float cc, float opacity) {
-    BlendG r{pw, __expf(pw)};
-    const float a = opacity * r.G;
-    if (__builtin_expect(pw > 0.0f || fabsf(a * 255.0f - 1.0f) < 0x1p-12f, 0)) {
+// the exact power and G of a flagged pair (conic' = -conic/2 from the splat record)
+__device__ __forceinline__ void blend_fix(float &power, float &G, float dx, float dy, float ca, float cb, float cc) {
 #pragma clang fp contract(off)
-        const float cx = -2.0f * ca, cy = -2.0f * cb, cz = -2.0f * cc;  // exact
-        r.power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-        r.G = exp_rn_f32(r.power);
-    }
-    return r;
+    const float cx = -2.0f * ca, cy = -2.0f * cb, cz = -2.0f * cc;  // exact
+    power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
+    G = exp_rn_f32(power);
 }
 
 // s_waitcnt vmcnt(4) expcnt(7) lgkmcnt(15): everything but the 4 youngest

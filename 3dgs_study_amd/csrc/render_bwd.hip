@@ -131,22 +131,25 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     const bool h16 = (lane & 16) != 0;
 
     struct Pre {
-        float dx, dy, G, alpha;
+        float dx, dy, G, alpha, power;
         bool valid;
     };
-    auto prepare = [&](float4 p0, float4 p1, int k, int lim, bool live) {  // valid needs lo + k < last_contrib
+    // power and G as render_fwd.hip computes them, bit for bit (same expression,
+    // same exact re-check near the skip thresholds, done by finish_pair)
+    auto prepare = [&](float4 p0, float4 p1) {
         Pre q;
         q.dx = p0.x - fx;
         q.dy = p0.y - fy;
         const float ux = p0.z * q.dx + p0.w * q.dy;  // conic' * d with conic' = -conic/2 (splat record)
         const float uy = p0.w * q.dx + p1.x * q.dy;
-        // power and G bit for bit as render_fwd.hip computes them (same expression,
-        // same exact re-check near the skip thresholds)
-        const BlendG e = blend_g(q.dx * ux + q.dy * uy, q.dx, q.dy, p0.z, p0.w, p1.x, p1.y);
-        q.G = e.G;
-        q.alpha = fminf(0.99f, p1.y * q.G);
-        q.valid = live && k < lim && !(e.power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
+        q.power = q.dx * ux + q.dy * uy;
+        q.G = __expf(q.power);
         return q;
+    };
+    // valid needs lo + k < last_contributor, power <= 0 and alpha >= 1/255
+    auto finish = [&](Pre &q, float4 p1, int k, int lim, bool live) {
+        q.alpha = fminf(0.99f, p1.y * q.G);
+        q.valid = live && k < lim && !(q.power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
     };
     // The per-pixel quantities the nine sums of one Gaussian are made of.
     struct Part {
@@ -250,8 +253,14 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
             const float4 a0 = ld4(rb + 3), a1 = ld4(rb + 4), a2 = ld4(rb + 5);
             boff -= 2 * (uint32_t)sizeof(st.rec[0]);
             const int la = __float_as_int(a2.w), lb = __float_as_int(b2.w);
-            const Pre qa = prepare(a0, a1, la, lim, true);  // entry lo + l = upstream `contributor`
-            const Pre qb = prepare(b0, b1, lb, lim, two);
+            Pre qa = prepare(a0, a1), qb = prepare(b0, b1);
+            const bool na = blend_near(qa.power, a1.y * qa.G), nb = blend_near(qb.power, b1.y * qb.G);
+            if (__builtin_expect(__ballot(na || nb) != 0, 0)) {  // rare: exact skip decisions (gsr_blend.hpp)
+                if (na) blend_fix(qa.power, qa.G, qa.dx, qa.dy, a0.z, a0.w, a1.x);
+                if (nb) blend_fix(qb.power, qb.G, qb.dx, qb.dy, b0.z, b0.w, b1.x);
+            }
+            finish(qa, a1, la, lim, true);  // entry lo + l = upstream `contributor`
+            finish(qb, b1, lb, lim, two);
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
             const Part pa = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: a before b

@@ -70,23 +70,37 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
             // to cover LDS and transcendental latency; only the T recurrence is serial.
             for (int k = 0; k < ns; k += FWD_GROUP) {
                 float pw[FWD_GROUP], al[FWD_GROUP], cr[FWD_GROUP], cg[FWD_GROUP], cb[FWD_GROUP];
+                float G[FWD_GROUP], op[FWD_GROUP];
                 int li[FWD_GROUP];
+                bool near = false;
 #pragma unroll
                 for (int g = 0; g < FWD_GROUP; g++) {
                     const int kg = min(k + g, ns - 1);
                     const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1];
                     cb[g] = st.rec[kg][2].x;
                     li[g] = __float_as_int(st.rec[kg][2].w);
+                    // conic' = -conic/2 (splat record): pw is upstream's power up to
+                    // rounding; render_bwd.hip recomputes it bit for bit
                     const float dx = r0.x - fx, dy = r0.y - fy;
-                    // conic' = -conic/2 (splat record): pw is upstream's power; render_bwd.hip
-                    // recomputes it bit for bit
                     const float ux = r0.z * dx + r0.w * dy, uy = r0.w * dx + r1.x * dy;
-                    const BlendG e = blend_g(dx * ux + dy * uy, dx, dy, r0.z, r0.w, r1.x, r1.y);
-                    pw[g] = e.power;
-                    al[g] = fminf(0.99f, r1.y * e.G);
+                    pw[g] = dx * ux + dy * uy;
+                    G[g] = __expf(pw[g]);
+                    op[g] = r1.y;
+                    near = near || blend_near(pw[g], op[g] * G[g]);
                     cr[g] = r1.z;
                     cg[g] = r1.w;
                 }
+                if (__builtin_expect(__ballot(near) != 0, 0)) {  // rare: exact skip decisions (gsr_blend.hpp)
+#pragma unroll
+                    for (int g = 0; g < FWD_GROUP; g++) {
+                        const int kg = min(k + g, ns - 1);
+                        const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1];
+                        if (blend_near(pw[g], op[g] * G[g]))
+                            blend_fix(pw[g], G[g], r0.x - fx, r0.y - fy, r0.z, r0.w, r1.x);
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < FWD_GROUP; g++) al[g] = fminf(0.99f, op[g] * G[g]);
                 // upstream's front-to-back step without branches or lane-mask logic
                 // (selects on VGPRs only: the per-Gaussian SALU work of bool masks
                 // and exec juggling, one scalar unit per CU, bounded this loop).
