@@ -38,7 +38,23 @@ struct RenderFwdArgs {
 #endif
 constexpr int FWD_GROUP = GSR_FWD_GROUP;  // Gaussians per blend iteration
 
-__global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs a) {
+// Per-wave LDS image of a chunk's surviving Gaussians for the forward.  Each
+// record carries the power as a quadratic in the pixel's offset (x, y) in 0..7
+// from the quadrant's first pixel:
+//   p(x, y) = K6 + K4 x + K5 y + K1 x^2 + K2 x y + K3 y^2
+// (conic' = -conic/2, centre offset (u, v) = mean - quadrant origin: K1 = c'a,
+// K2 = 2 c'b, K3 = c'c, K4 = -2 (c'a u + c'b v), K5 = -2 (c'b u + c'c v),
+// K6 = p(0, 0)), five FMAs per pixel instead of the eight of d^T conic' d.
+// It is within a few ulp of upstream's expression like that one (the expansion
+// keeps the terms at the magnitude of the form itself); the rare pairs near a
+// skip threshold are redone exactly from (u, v) (blend_fix).
+//   rec[k][0] = {K6, K4, K5, K1}, rec[k][1] = {K2, K3, opacity, r},
+//   rec[k][2] = {g, b, -, lane},  rec[k][3] = {u, v, -, -}
+struct FwdChunk {
+    float4 rec[64][4];
+};
+
+__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(8))) render_fwd_kernel(RenderFwdArgs a) {
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
     if (tile < 0) return;
@@ -46,7 +62,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
-    const float fx = (float)px, fy = (float)py;
+    const float lx = (float)(lane & 7), ly = (float)(lane >> 3);  // offset in the quadrant
     const uint2 r = a.ranges[tile];
     const int n = (int)(r.y - r.x);
 
@@ -54,8 +70,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
     uint32_t last = 0;
     uint32_t work = 0;  // wave-uniform: surviving Gaussians walked (~ the backward's replay work)
     float live = inside ? 1.0f : 0.0f;  // 0 once the pixel has stopped (or lies outside the image)
-    __shared__ ChunkStage stage[BLEND_WAVES];
-    ChunkStage &st = stage[BLEND_WAVES == 1 ? 0 : w];
+    __shared__ FwdChunk stage[BLEND_WAVES];
+    FwdChunk &st = stage[BLEND_WAVES == 1 ? 0 : w];
     if (__any(inside) && n > 0) {
         const uint32_t *list = a.point_list + r.x;
         const int nm1 = n - 1;
@@ -63,7 +79,19 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
         // pos + l); returns true once every pixel of the quadrant is saturated.
         auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
-            const int ns = stage_survivors(st, lane, rel, __ballot(rel), A, B, C);
+            const uint64_t mask = __ballot(rel);
+            if (rel) {  // compacted: slot = survivors in lower lanes
+                const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                const float u = A.x - (float)qx0, v = A.y - (float)qy0;  // exact (see blend_fix)
+                const float ca = A.z, cb = A.w, cc = B.x;
+                const float hu = ca * u + cb * v, hv = cb * u + cc * v;
+                st.rec[slot][0] = make_float4(u * hu + v * hv, -2.0f * hu, -2.0f * hv, ca);
+                st.rec[slot][1] = make_float4(2.0f * cb, cc, B.y, B.z);
+                st.rec[slot][2] = make_float4(B.w, C.x, 0.0f, __int_as_float(lane));
+                st.rec[slot][3] = make_float4(u, v, 0.0f, 0.0f);
+            }
+            const int ns = __builtin_popcountll(mask);
             work += ns;
             // FWD_GROUP Gaussians per iteration: their LDS reads, powers and exps are
             // independent, so each wave has that much instruction-level parallelism
@@ -76,27 +104,25 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_fwd_kernel(RenderFwdArgs
 #pragma unroll
                 for (int g = 0; g < FWD_GROUP; g++) {
                     const int kg = min(k + g, ns - 1);
-                    const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1];
-                    cb[g] = st.rec[kg][2].x;
-                    li[g] = __float_as_int(st.rec[kg][2].w);
-                    // conic' = -conic/2 (splat record): pw is upstream's power up to
-                    // rounding; render_bwd.hip recomputes it bit for bit
-                    const float dx = r0.x - fx, dy = r0.y - fy;
-                    const float ux = r0.z * dx + r0.w * dy, uy = r0.w * dx + r1.x * dy;
-                    pw[g] = dx * ux + dy * uy;
+                    const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r2 = st.rec[kg][2];
+                    li[g] = __float_as_int(r2.w);
+                    const float t1 = fmaf(r1.x, ly, fmaf(r0.w, lx, r0.y)), t2 = fmaf(r1.y, ly, r0.z);
+                    pw[g] = fmaf(t2, ly, fmaf(t1, lx, r0.x));
                     G[g] = __expf(pw[g]);
-                    op[g] = r1.y;
+                    op[g] = r1.z;
                     near = near || blend_near(pw[g], op[g] * G[g]);
-                    cr[g] = r1.z;
-                    cg[g] = r1.w;
+                    cr[g] = r1.w;
+                    cg[g] = r2.x;
+                    cb[g] = r2.y;
                 }
                 if (__builtin_expect(__ballot(near) != 0, 0)) {  // rare: exact skip decisions (gsr_blend.hpp)
 #pragma unroll
                     for (int g = 0; g < FWD_GROUP; g++) {
                         const int kg = min(k + g, ns - 1);
-                        const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1];
+                        const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r3 = st.rec[kg][3];
+                        // d = mean - pixel = (u - x, v - y), exact like upstream's subtraction
                         if (blend_near(pw[g], op[g] * G[g]))
-                            blend_fix(pw[g], G[g], r0.x - fx, r0.y - fy, r0.z, r0.w, r1.x);
+                            blend_fix(pw[g], G[g], r3.x - lx, r3.y - ly, r0.w, 0.5f * r1.x, r1.y);
                     }
                 }
 #pragma unroll
