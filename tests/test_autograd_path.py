@@ -3,7 +3,8 @@
 GaussianRasterizer -> _RasterizeGaussians.backward -> the activations (exp, sigmoid,
 normalize, the SH cat; or the Python SH / cov3D branch) -> the six leaf gradients
 and viewspace_points.grad, against the CPU oracle's native gradients pushed through
-torch autograd of the same activations on the CPU."""
+torch autograd of the same activations on the CPU.  Both sides run the caller's activations on the GPU, so
+the rasterizer sees bit-identical inputs and its integer decisions agree exactly."""
 import math
 
 import numpy as np
@@ -17,40 +18,43 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-def _reference_grads(oracle, cam, g, dL, python_branch, mt=False):
-    """Leaf gradients of sum(image * dL): the reference's activations in torch on the
-    CPU, the rasterizer forward/backward by the oracle (the native autograd Function's
-    role), torch autograd for the rest."""
+def _reference_grads(oracle, cam, g, dev, dL, python_branch, mt=False):
+    """Leaf gradients of sum(image * dL): the reference's activations (the caller's
+    torch ops, on the GPU as in the HIP run, so the rasterizer sees bit-identical
+    inputs), the rasterizer forward/backward by the oracle in place of the native
+    autograd Function, torch autograd through the activations for the rest."""
     import train_step
 
-    leaves = [p.detach().clone().requires_grad_(True) for p in g.params()]
+    leaves = [p.detach().to(dev).clone().requires_grad_(True) for p in g.params()]
     xyz, f_dc, f_rest, opac_l, scal_l, rot_l = leaves
+    camd = cam.to(dev)
     opacity = torch.sigmoid(opac_l)
     feats = torch.cat((f_dc, f_rest), dim=1)
     kw = dict(scale_modifier=1.0, sh_degree=g.active_sh_degree, mt=mt)
     inputs, names = [xyz, opacity], ["dmeans3D", "dopacity"]
     if python_branch:
         shs_view = feats.transpose(1, 2).view(-1, 3, (g.max_sh_degree + 1) ** 2)
-        dirs = xyz - cam.camera_center.repeat(feats.shape[0], 1)
+        dirs = xyz - camd.camera_center.repeat(feats.shape[0], 1)
         dirs = dirs / dirs.norm(dim=1, keepdim=True)
         colors = torch.clamp_min(train_step.eval_sh(g.active_sh_degree, shs_view, dirs) + 0.5, 0.0)
         cov3D = train_step.covariance(torch.exp(scal_l), 1.0, rot_l)
-        kw.update(colors_precomp=colors.detach().numpy(), cov3D_precomp=cov3D.detach().numpy())
+        kw.update(colors_precomp=colors.detach().cpu().numpy(), cov3D_precomp=cov3D.detach().cpu().numpy())
         inputs += [colors, cov3D]
         names += ["dcolors", "dcov3D"]
     else:
         scales = torch.exp(scal_l)
         rotations = torch.nn.functional.normalize(rot_l)
-        kw.update(shs=feats.detach().numpy(), scales=scales.detach().numpy(), rotations=rotations.detach().numpy())
+        kw.update(shs=feats.detach().cpu().numpy(), scales=scales.detach().cpu().numpy(),
+                  rotations=rotations.detach().cpu().numpy())
         inputs += [feats, scales, rotations]
         names += ["dsh", "dscales", "drot"]
-    f = oracle.forward(xyz.detach().numpy(), opacity.detach().numpy(), cam.world_view_transform.numpy(),
+    f = oracle.forward(xyz.detach().cpu().numpy(), opacity.detach().cpu().numpy(), cam.world_view_transform.numpy(),
                        cam.full_proj_transform.numpy(), cam.camera_center.numpy(), np.zeros(3, np.float32),
                        cam.image_height, cam.image_width, math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5), **kw)
     b = oracle.backward(f, dL)
-    torch.autograd.backward(inputs, [torch.from_numpy(np.ascontiguousarray(b[n])).reshape(x.shape)
+    torch.autograd.backward(inputs, [torch.from_numpy(np.ascontiguousarray(b[n])).to(dev).reshape(x.shape)
                                      for n, x in zip(names, inputs)])
-    return f, [p.grad for p in leaves], b["dmeans2D"]
+    return f, [p.grad.cpu() for p in leaves], b["dmeans2D"]
 
 
 def _hip_grads(cam, g, dev, dL, python_branch):
@@ -68,7 +72,7 @@ def _check(oracle, cam, g, dev, python_branch, mt=False):
     from helpers import random_dL
 
     dL = random_dL(cam.image_height, cam.image_width)
-    f, ref, ref_vs = _reference_grads(oracle, cam, g, dL, python_branch, mt)
+    f, ref, ref_vs = _reference_grads(oracle, cam, g, dev, dL, python_branch, mt)
     out, got, got_vs = _hip_grads(cam, g, dev, dL, python_branch)
     assert np.abs(out["render"].detach().cpu().numpy() - f["color"]).max() <= 1e-4
     np.testing.assert_array_equal(out["radii"].cpu().numpy(), f["radii"])

@@ -173,10 +173,15 @@ def test_full_train_step_fused_matches_torch(dev):
         losses = [train_step.full_train_step(it, cam, g, st, target, bg).item() for it in (1, 2)]
         out[fused] = (losses, [p.detach().clone() for p in g.params()], st)
     np.testing.assert_allclose(out[True][0], out[False][0], rtol=1e-5)
-    # Adam divides by sqrt(v): an entry whose gradient is ~0 moves by up to ~lr on a
-    # last-ulp difference of that gradient, so compare parameters to 2e-5 absolute
-    for a, b in zip(out[True][1], out[False][1]):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=2e-5)
+    # Adam divides by sqrt(v) (eps 1e-15): an entry whose gradient is ~0 moves by up to
+    # ~lr per step on a last-ulp difference of that gradient (here the fused loss's
+    # dL/dpix vs torch's, and the atomics' summation order), even flipping sign.  So:
+    # nearly every entry within 2e-5, the rare rest within the 2 steps' 2 lr bound.
+    lrs = [g["lr"] for g in out[False][2].optimizer.param_groups]
+    for a, b, lr in zip(out[True][1], out[False][1], lrs):
+        d = (a - b).abs()
+        assert float((d > 2e-5 + 1e-4 * b.abs()).float().mean()) < 1e-3, float((d > 2e-5).float().mean())
+        assert float(d.max()) <= 2 * 2 * lr + 1e-6, (float(d.max()), lr)
     for n in ("max_radii2D", "denom"):
         torch.testing.assert_close(getattr(out[True][2], n), getattr(out[False][2], n), rtol=0, atol=0)
     torch.testing.assert_close(out[True][2].xyz_gradient_accum, out[False][2].xyz_gradient_accum, rtol=1e-4,
