@@ -44,27 +44,43 @@ __global__ void __launch_bounds__(SX_THREADS) sh_from_colors_kernel(int P, int n
     float acc[3 * MC];
 #pragma unroll
     for (int k = 0; k < 3 * MC; k++) acc[k] = 0.f;
-    for (int v = 0; v < nviews; v++) {
-        const float *r = rec + (size_t)v * (size_t)stride;
-        const int deg = (int)r[3];
-        const float *d3 = r + 4 + 3 * (size_t)li;
-        const float d[3] = {d3[0], d3[1], d3[2]};
-        // a zero colour gradient (culled or clamped in this view) adds exactly
-        // nothing: skipped, so a mean at the view's camera centre (zero-length
-        // direction, NaN basis) cannot poison the sum; upstream gives a culled
-        // Gaussian no SH gradient at all
-        if (d[0] == 0.f && d[1] == 0.f && d[2] == 0.f) continue;
-        const float ox = mx - r[0], oy = my - r[1], oz = mz - r[2];
-        const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
-        float b[16];
-        sh_basis(deg, ox / len, oy / len, oz / len, b);
-        const int ncoef = min((deg + 1) * (deg + 1), MC);
+    // Views in groups of VB: the group's colour rows are loaded before any of its
+    // products, so the loads of VB views are in flight together (one view at a
+    // time left the kernel waiting on each view's load: 97 us for 8 views at
+    // 1M Gaussians, vs 34 us for one).  Sums stay in view order.
+    constexpr int VB = 4;
+    for (int v0 = 0; v0 < nviews; v0 += VB) {
+        float dv[VB][3];
 #pragma unroll
-        for (int k = 0; k < MC; k++)
-            if (k < ncoef) {
+        for (int j = 0; j < VB; j++) {
+            const int v = min(v0 + j, nviews - 1);
+            const float *d3 = rec + (size_t)v * (size_t)stride + 4 + 3 * (size_t)li;
 #pragma unroll
-                for (int c = 0; c < 3; c++) acc[3 * k + c] += b[k] * d[c];
-            }
+            for (int c = 0; c < 3; c++) dv[j][c] = d3[c];
+        }
+#pragma unroll
+        for (int j = 0; j < VB; j++) {
+            if (v0 + j >= nviews) break;
+            const float *r = rec + (size_t)(v0 + j) * (size_t)stride;
+            const float *d = dv[j];
+            // a zero colour gradient (culled or clamped in this view) adds exactly
+            // nothing: skipped, so a mean at the view's camera centre (zero-length
+            // direction, NaN basis) cannot poison the sum; upstream gives a culled
+            // Gaussian no SH gradient at all
+            if (d[0] == 0.f && d[1] == 0.f && d[2] == 0.f) continue;
+            const int deg = (int)r[3];
+            const float ox = mx - r[0], oy = my - r[1], oz = mz - r[2];
+            const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
+            float b[16];
+            sh_basis(deg, ox / len, oy / len, oz / len, b);
+            const int ncoef = min((deg + 1) * (deg + 1), MC);
+#pragma unroll
+            for (int k = 0; k < MC; k++)
+                if (k < ncoef) {
+#pragma unroll
+                    for (int c = 0; c < 3; c++) acc[3 * k + c] += b[k] * d[c];
+                }
+        }
     }
     if (live) {
 #pragma unroll

@@ -201,8 +201,11 @@ def main():
                          "the rest (multiview.py); 'allreduce' all-reduces all 59 floats/Gaussian")
     ap.add_argument("--footprint-steps", type=int, default=100,
                     help="timed steps of the same unit with the other tile footprint (gsr.h gsr_footprint); 0 = skip")
-    ap.add_argument("--stage-events", default="all", choices=["all", "none"],
-                    help="HIP events around every rasterizer stage in the timed region (stages_ms, roofline)")
+    ap.add_argument("--stage-events", default="split", choices=["split", "all", "none"],
+                    help="split: the per-stage split (stages_ms, dominant stage) from its own steady-state block of "
+                         "the same K steps right before the timed region, whose steps carry events only around the "
+                         "dominant stage (its live launch time = the roofline); all: events on every stage inside "
+                         "the timed region (they cost ~5%% of the step); none: no events")
     ap.add_argument("--render-steps", type=int, default=20,
                     help="timed forward-only renders of config E (5M, 4K) reported beside the C line; 0 = skip")
     args = ap.parse_args()
@@ -260,11 +263,19 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    # Timed region.  Every rasterizer stage carries HIP events on the launch stream
-    # (gsr_timing_*): stages_ms and the dominant stage's live average launch time
-    # (the roofline) come from these K steps.
-    _C.timing_enable(args.stage_events == "all")
+    # Stage split (HIP events on the launch stream around every rasterizer stage,
+    # gsr_timing_*): a steady-state block of K steps after the warm-up.  Recording
+    # 14 events per step costs ~5 % of the step, so the timed region below carries
+    # events only around the dominant stage.
+    per_stage, dom = {}, "render_bwd"
+    if args.stage_events == "split":
+        per_stage, dom = stage_split(one_step, args.steps)
+    # Timed region: K steps; events around the dominant stage give its live
+    # average launch time (the roofline).
+    _C.timing_enable({"split": [dom], "all": True, "none": False}[args.stage_events])
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = one_step()
@@ -279,8 +290,9 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    per_stage = {k: (ms / n if n else 0.0, n) for k, (ms, n) in stages.items() if n}
-    dom = max(per_stage, key=lambda k: per_stage[k][0] * per_stage[k][1]) if per_stage else "render_bwd"
+    if args.stage_events == "all":
+        per_stage = {k: (ms / n if n else 0.0, n) for k, (ms, n) in stages.items() if n}
+        dom = max(per_stage, key=lambda k: per_stage[k][0] * per_stage[k][1]) if per_stage else "render_bwd"
     dom_live = stages.get(dom, (0.0, 0))
 
     if rank == 0:
@@ -318,7 +330,7 @@ def main():
             },
             "mpix_per_s": round(value * W * H / 1e6, 2),
             "stages_ms": {k: round(v[0], 4) for k, v in per_stage.items()},
-            "stages_source": "HIP events around every rasterizer stage inside the timed region (mean per launch)",
+            "stages_source": STAGES_SOURCE[args.stage_events],
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -349,6 +361,32 @@ def main():
         dist.destroy_process_group()
 
 
+STAGES_SOURCE = {
+    "split": "HIP events around every rasterizer stage over a steady-state block of the same K steps right before "
+             "the timed region (mean per launch); inside the timed region only the dominant stage carries events",
+    "all": "HIP events around every rasterizer stage inside the timed region (mean per launch)",
+    "none": "not measured (--stage-events none)",
+}
+
+
+def stage_split(step_fn, steps: int):
+    """Per-stage mean launch time over `steps` steady-state calls of step_fn, and the
+    stage with the largest total: ({stage: (ms_per_launch, launches)}, dominant)."""
+    import torch
+    from diff_gaussian_rasterization import _C
+
+    torch.cuda.synchronize()
+    _C.timing_enable(True)
+    for _ in range(steps):
+        step_fn()
+    torch.cuda.synchronize()
+    stages = _C.timing_read()
+    _C.timing_enable(False)
+    per = {k: (ms / n, n) for k, (ms, n) in stages.items() if n}
+    dom = max(per, key=lambda k: per[k][0] * per[k][1]) if per else "render_bwd"
+    return per, dom
+
+
 def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
     """The headline unit again with the other tile footprint (rect <-> tight):
     same image and gradients from lists of a different length."""
@@ -361,20 +399,18 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
         I = _last_num_rendered(cam, g, bg)
         for _ in range(warmup):
             one_step()
+        per, _ = stage_split(one_step, steps)
         torch.cuda.synchronize()
-        _C.timing_enable(True)
         t0 = time.perf_counter()
         for _ in range(steps):
             one_step()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        stages = _C.timing_read()
-        _C.timing_enable(False)
     finally:
         set_footprint(prev)
     return {"footprint": mode, "value": round(steps / dt, 3), "unit": "train-iters/s",
             "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps, "num_rendered": I,
-            "stages_ms": {k: round(ms / n, 4) for k, (ms, n) in stages.items() if n}}
+            "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "stages_source": STAGES_SOURCE["split"]}
 
 
 def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0) -> dict:
@@ -397,18 +433,18 @@ def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0) -> 
     with torch.no_grad():
         for _ in range(warmup):
             train_step.render(cam, g, bg)
+        # the largest stage by measured time, from a steady-state block of its own
+        per, dom = stage_split(lambda: train_step.render(cam, g, bg), steps)
+        _C.timing_enable([dom])  # only the dominant stage inside the timed region
         torch.cuda.synchronize()
-        _C.timing_enable(True)  # every stage, inside the timed region
         t0 = time.perf_counter()
         for _ in range(steps):
             train_step.render(cam, g, bg)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        stages = _C.timing_read()
+        live = _C.timing_read()[dom]
         _C.timing_enable(False)
-    per = {k: (ms / n, n) for k, (ms, n) in stages.items() if n}
-    dom = max(per, key=lambda k: per[k][0] * per[k][1])  # the largest stage by measured time
-    dom_ms = per[dom][0]
+    dom_ms = live[0] / live[1]
     ab = algorithmic_bytes(dom, P, I, W, H, M)
     achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     fps = steps / dt
@@ -418,7 +454,7 @@ def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0) -> 
         "config": {"workload": f"{cfg_name}: {WORKLOADS[cfg_name]}", "gaussians": P, "width": W, "height": H,
                    "sh_degree": deg, "footprint": _C.get_footprint(), "num_rendered": I},
         "stages_ms": {k: round(v[0], 4) for k, v in per.items()},
-        "stages_source": "HIP events around every rasterizer stage inside the timed region (mean per launch)",
+        "stages_source": STAGES_SOURCE["split"],
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": pmc_traffic(f"{dom}_{cfg_name}"),
