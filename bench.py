@@ -304,7 +304,9 @@ def main():
         traffic = pmc_traffic(dom)
         coll = "RCCL" if backend == "nccl" else backend
         line = {
-            "metric": "train iters/sec (fwd+bwd) + Mpix/sec, 1080p, 1M Gaussians @1/2/4/8 GPU",
+            # BASELINE.json's headline metric at C; the other backward configs name their own shape
+            "metric": ("train iters/sec (fwd+bwd) + Mpix/sec, 1080p, 1M Gaussians @1/2/4/8 GPU" if args.config == "C"
+                       else f"train iters/sec (fwd+bwd) + Mpix/sec, {W}x{H}, {P} Gaussians, SH{deg}"),
             "value": round(value, 3),
             "unit": "train-iters/s",
             "n_gpus": world,

@@ -18,5 +18,5 @@ for SET in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_
   if [ $rc -ne 0 ]; then echo "pass $i failed rc=$rc"; tail -5 $OUT/p$i.log; exit $rc; fi
 done
 mkdir -p gpurun_out
-python3 tools/pmc_summary.py $OUT gpurun_out/${TAG}_pmc_summary.json ${PMC_SUFFIX:-} > gpurun_out/${TAG}_pmc.txt
-cat gpurun_out/${TAG}_pmc.txt
+python3 tools/pmc_summary.py $OUT gpurun_out/${TAG}_pmc_summary.json ${PMC_SUFFIX:-} > gpurun_out/${TAG}_pmc${PMC_TXT:-}.txt
+cat gpurun_out/${TAG}_pmc${PMC_TXT:-}.txt

@@ -11,7 +11,7 @@ grep '"metric"' gpurun_out/${TAG}_bench.log | cut -c1-300
 bash tools/prof.sh ${TAG}_C || exit 1
 bash tools/prof.sh ${TAG}_E --config E || exit 1
 bash tools/pmc.sh ${TAG} > /dev/null || exit 1
-PMC_ARGS="--config E" PMC_SUFFIX="_E --merge" bash tools/pmc.sh ${TAG} > /dev/null || exit 1
+PMC_ARGS="--config E" PMC_SUFFIX="_E --merge" PMC_TXT=_E bash tools/pmc.sh ${TAG} > /dev/null || exit 1
 echo profiles done
 if [ "${2:-}" != "skip-tests" ]; then
   timeout -k 10 1000 python -u -m pytest tests/ -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread \
