@@ -70,40 +70,6 @@ __device__ inline void rows_to_lds(const float *__restrict__ src, int g0, int n,
     }
 }
 
-// Split form of rows_to_lds for a workgroup slice of THREADS rows of RWC floats
-// (RWC a multiple of 4: RWC / 4 float4 per thread): issue the loads into
-// registers first, do unrelated work while they fly, then store them.  A
-// partial slice (the grid's last workgroup) loads clamped indices and stores
-// only its valid part.
-template <int THREADS, int RWC>
-struct RowPrefetch {
-    static constexpr int NB4 = RWC / 4;
-    float4 v[NB4];
-    // n = 0: every lane loads element 0 of src (any valid 16-B-aligned buffer), so
-    // the number of loads in flight never depends on a run-time branch (the
-    // compiler's vmcnt bookkeeping would otherwise wait for all of them early)
-    __device__ __forceinline__ void load(const float *__restrict__ src, int g0, int n) {
-        const float4 *b4 = reinterpret_cast<const float4 *>(src + (size_t)g0 * RWC);
-        const int last = max(n * NB4 - 1, 0);
-#pragma unroll
-        for (int b = 0; b < NB4; b++) v[b] = b4[min((int)threadIdx.x + b * THREADS, last)];
-    }
-    __device__ __forceinline__ void store(int n, float *lds) const {
-        const int n4 = n * NB4;
-#pragma unroll
-        for (int b = 0; b < NB4; b++) {
-            const int i = (int)threadIdx.x + b * THREADS;
-            if (i < n4) {
-                const int e = i << 2;
-                lds[lds_row_index<RWC>(e, RWC, 0.f)] = v[b].x;
-                lds[lds_row_index<RWC>(e + 1, RWC, 0.f)] = v[b].y;
-                lds[lds_row_index<RWC>(e + 2, RWC, 0.f)] = v[b].z;
-                lds[lds_row_index<RWC>(e + 3, RWC, 0.f)] = v[b].w;
-            }
-        }
-    }
-};
-
 // The reverse: LDS rows (stride RW + 1) -> global rows [g0, g0 + n).
 template <int THREADS, int RWC = 0>
 __device__ inline void lds_to_rows(const float *lds, int g0, int n, int RW_, float *__restrict__ dst) {

@@ -72,11 +72,15 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
     const bool use_sh = in.sh != nullptr && in.colors_precomp == nullptr;
     const int n = min(PRE_THREADS, in.P - g0);
-    // This Gaussian's own inputs are loaded first and the workgroup's SH rows after
-    // them: the row loads (12 x 16 B per lane at degree 3) stay in flight behind
-    // the geometry below (vmcnt counts in issue order) and go to LDS only before
-    // the colour evaluation.
-    constexpr bool PREFETCH = RWC > 0 && RWC % 4 == 0;
+    // This Gaussian's own inputs are loaded first and its SH row after them: at
+    // degree 3 each thread loads its own 192-B row as 12 x 16 B straight into
+    // registers, in flight behind the geometry below (vmcnt counts in issue
+    // order).  Per instruction the lanes touch 64 different 128-B lines (stride
+    // 192 B) but the 12 loads cover the wave's 12 KB exactly, so L2 serves the
+    // re-touches; without an LDS stage the kernel is no longer LDS-limited to 3
+    // waves per SIMD (preprocess 68 -> 66 us at C, 334 -> 317 us at E).  Other
+    // degrees stage the workgroup's rows through LDS (coalesced, odd row stride).
+    constexpr bool DIRECT = RWC == 48;  // each thread's own row in registers, no LDS
     const bool live = idx < in.P;
     const int li = live ? idx : in.P - 1;
     const f3 p = {in.means3D[3 * li], in.means3D[3 * li + 1], in.means3D[3 * li + 2]};
@@ -94,11 +98,14 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         for (int k = 0; k < 4; k++) gin[3 + k] = in.rotations[4 * (size_t)li + k];
     }
     const float opac = in.opacities[li];
-    RowPrefetch<PRE_THREADS, PREFETCH ? RWC : 4> pf;
-    if (PREFETCH)  // unconditional (a dummy load of element 0 without SH rows)
-        pf.load(use_sh ? in.sh : in.means3D, use_sh ? g0 : 0, use_sh ? n : 0);
-    else if (use_sh)
+    float4 rowv[DIRECT ? 12 : 1];
+    if constexpr (DIRECT) {  // launched only with SH rows (16-B aligned)
+        const float4 *r4 = reinterpret_cast<const float4 *>(in.sh + (size_t)li * 48);
+#pragma unroll
+        for (int b = 0; b < 12; b++) rowv[b] = r4[b];
+    } else if (use_sh) {
         rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
+    }
     uint32_t touched = 0, key = 0;
     bool perr = false, key_vis = false;
     // what the colour stage (after the barrier) needs
@@ -215,8 +222,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
     if (idx < 8 * ORDER_NBUCKET) a.order_cnt[idx] = 0u;  // the backward wave-order buckets (render_fwd.hip)
     // colour stage: the SH rows land in LDS now, after the geometry
-    if (PREFETCH && use_sh) pf.store(n, sh_lds);
-    if (use_sh) __syncthreads();
+    if (use_sh && !DIRECT) __syncthreads();
     if (emit) {
         float rgb[3];
         uint8_t clampbits = 0;
@@ -228,7 +234,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
             const float dx = p.x - in.campos[0], dy = p.y - in.campos[1], dz = p.z - in.campos[2];
             const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
             const float x = dx / len, y = dy / len, z = dz / len;
-            const float *sh = sh_lds + threadIdx.x * (RW + 1);
+            const float *sh = DIRECT ? reinterpret_cast<const float *>(rowv) : sh_lds + threadIdx.x * (RW + 1);
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 const float v = sh_channel(sh, c, in.D, x, y, z);
@@ -356,7 +362,8 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
     a.radii = radii;
     a.order_cnt = at<uint32_t>(geom, L.order_cnt);
     const int nb = pre_blocks(in.P);
-    const size_t lds = (in.sh && !in.colors_precomp) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
+    const bool direct = in.sh && !in.colors_precomp && 3 * in.M == 48 && ((uintptr_t)in.sh & 15u) == 0;
+    const size_t lds = (in.sh && !in.colors_precomp && !direct) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     // SH row width as a compile-time constant for the common degrees (cheap LDS
     // row indexing); any other width takes the run-time path
     switch (in.sh && !in.colors_precomp ? 3 * in.M : 0) {

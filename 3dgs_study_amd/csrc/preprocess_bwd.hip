@@ -26,7 +26,7 @@ struct PreBwdArgs {
 
 // backward.cu computeColorFromSH (backward).  `sh` and `dsh` may alias (the
 // same LDS row): every SH coefficient is read before any gradient is written.
-__device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, float ox, float oy, float oz,
+__device__ __forceinline__ void sh_backward(const float *sh, float *dsh, int deg, int M, float ox, float oy, float oz,
                                    const float dRGB[3], f3 &dmean) {
     const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
     const float x = ox / len, y = oy / len, z = oz / len;
@@ -72,11 +72,10 @@ __device__ inline void sh_backward(const float *sh, float *dsh, int deg, int M, 
         for (int k = 0; k < 16; k++)
             if (k < ncoef) dsh[3 * k + c] = b[k] * d;
     }
-    for (int k = ncoef; k < M; k++) {
-        dsh[3 * k + 0] = 0.f;
-        dsh[3 * k + 1] = 0.f;
-        dsh[3 * k + 2] = 0.f;
-    }
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        if (k >= ncoef && k < M) dsh[3 * k + 0] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
+    for (int k = max(ncoef, 16); k < M; k++) dsh[3 * k + 0] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
     const float ddx = (dRGBdx[0] * dRGB[0] + dRGBdx[1] * dRGB[1]) + dRGBdx[2] * dRGB[2];
     const float ddy = (dRGBdy[0] * dRGB[0] + dRGBdy[1] * dRGB[1]) + dRGBdy[2] * dRGB[2];
     const float ddz = (dRGBdz[0] * dRGB[0] + dRGBdz[1] * dRGB[1]) + dRGBdz[2] * dRGB[2];
@@ -101,10 +100,12 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
                                        const Mat4 &V, const Mat4 &Pm);
 
 // One workgroup = PB_THREADS consecutive Gaussians.  Each thread loads its own
-// inputs first and the workgroup's SH rows after them, into registers: the rows
-// stay in flight while the geometry backward (cov2D, projection, cov3D) runs,
-// then go to LDS, where each thread turns its row into dL/dSH in place before
-// the rows stream back out coalesced.
+// inputs first and, at SH degree 3, its own 192-B SH row after them (12 x 16 B
+// into registers, in flight while the geometry backward — cov2D, projection,
+// cov3D — runs), turns the row into dL/dSH in place in registers and stores it
+// (row or coefficient-plane layout).  With no LDS stage the kernel runs 4 waves
+// per SIMD instead of 3 (112 -> 102 us at config C).  Other degrees stage the
+// workgroup's rows through LDS and stream them back out coalesced.
 template <int RWC>
 __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PB_THREADS][3M + 1]
@@ -115,7 +116,7 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     // the rows are needed for dL/dmean3D's view-direction term even when the
     // exchange takes the colour gradient instead of dsh
     const bool stage = in.sh != nullptr && (a.o.dsh != nullptr || a.o.drgb != nullptr || a.o.sh_dir) && in.M > 0;
-    constexpr bool PREFETCH = RWC > 0 && RWC % 4 == 0;
+    constexpr bool DIRECT = RWC == 48;  // each thread's own row in registers, no LDS
     const int idx = g0 + (int)threadIdx.x;
     const bool live = idx < in.P;
     const int li = live ? idx : in.P - 1;
@@ -140,25 +141,33 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const float accb = acc[8];                                       // color b
     const int32_t rad = a.radii[li];
     const uint32_t cl = a.clamped[li];
-    RowPrefetch<PB_THREADS, PREFETCH ? RWC : 4> pf;
-    if (PREFETCH)  // unconditional (a dummy load of element 0 without SH rows)
-        pf.load(stage ? in.sh : in.means3D, stage ? g0 : 0, stage ? n : 0);
-    else if (stage)
+    float rowv[DIRECT ? 48 : 1];
+    if constexpr (DIRECT) {  // launched only with staged (stage == true), 16-B aligned SH rows
+        const float4 *r4 = reinterpret_cast<const float4 *>(in.sh + (size_t)li * 48);
+#pragma unroll
+        for (int b = 0; b < 12; b++) {
+            const float4 v = r4[b];
+            rowv[4 * b] = v.x;
+            rowv[4 * b + 1] = v.y;
+            rowv[4 * b + 2] = v.z;
+            rowv[4 * b + 3] = v.w;
+        }
+    } else if (stage) {
         rows_to_lds<PB_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
+    }
     // pin the per-Gaussian loads ahead of the rows (the compiler would otherwise
     // sink them into the branch below, behind the rows, and wait for all of them)
     asm volatile("" ::"v"(acc0.x), "v"(acc0.y), "v"(acc0.z), "v"(acc0.w), "v"(acc1.x), "v"(acc1.y), "v"(acc1.z),
                  "v"(acc1.w), "v"(accb), "v"(rad), "v"(cl));
     ShStage st{};
     if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, rad, cl, V, Pm);
-    if (PREFETCH && stage) pf.store(n, sh_lds);
-    if (stage) __syncthreads();
+    if (stage && !DIRECT) __syncthreads();
     if (live) {
         f3 dmean = st.dmean;
         if (stage) {
-            float *row = sh_lds + threadIdx.x * (RW + 1);
+            float *row = DIRECT ? rowv : sh_lds + threadIdx.x * (RW + 1);
             if (st.vis)
-                sh_backward(row, row, in.D, in.M, mean.x - in.campos[0], mean.y - in.campos[1],
+                sh_backward(row, row, in.D, DIRECT ? 16 : in.M, mean.x - in.campos[0], mean.y - in.campos[1],
                             mean.z - in.campos[2], st.dRGB, dmean);
             else
                 for (int k = 0; k < RW; k++) row[k] = 0.f;
@@ -166,6 +175,23 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
         a.o.dmeans3D[3 * (size_t)idx + 0] = dmean.x;
         a.o.dmeans3D[3 * (size_t)idx + 1] = dmean.y;
         a.o.dmeans3D[3 * (size_t)idx + 2] = dmean.z;
+    }
+    if constexpr (DIRECT) {
+        if (live && a.o.dsh) {
+            if (a.o.dsh_planar) {
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (k < in.M)
+#pragma unroll
+                        for (int c = 0; c < 3; c++) a.o.dsh[(size_t)k * 3 * in.P + 3 * (size_t)idx + c] = rowv[3 * k + c];
+            } else {
+                float4 *d4 = reinterpret_cast<float4 *>(a.o.dsh + (size_t)idx * 48);
+#pragma unroll
+                for (int b = 0; b < 12; b++)
+                    d4[b] = make_float4(rowv[4 * b], rowv[4 * b + 1], rowv[4 * b + 2], rowv[4 * b + 3]);
+            }
+        }
+        return;
     }
     if (stage && a.o.dsh) {
         __syncthreads();
@@ -366,10 +392,17 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     a.accum = accum;
     a.o = o;
     const bool stage = in.sh && (o.dsh || o.drgb || o.sh_dir) && in.M > 0;
-    const size_t lds = stage ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
+    const bool direct = stage && 3 * in.M == 48 && ((uintptr_t)in.sh & 15u) == 0 &&
+                        (!a.o.dsh || a.o.dsh_planar || ((uintptr_t)a.o.dsh & 15u) == 0);
+    const size_t lds = stage && !direct ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     const dim3 grid((in.P + PB_THREADS - 1) / PB_THREADS);
     switch (3 * in.M) {  // see launch_preprocess
-        case 48: hipLaunchKernelGGL(preprocess_bwd_kernel<48>, grid, dim3(PB_THREADS), lds, s, a); break;
+        case 48:  // the direct-row kernel needs staged, 16-B aligned rows
+            if (direct) {
+                hipLaunchKernelGGL(preprocess_bwd_kernel<48>, grid, dim3(PB_THREADS), lds, s, a);
+                break;
+            }
+            [[fallthrough]];
         case 3: hipLaunchKernelGGL(preprocess_bwd_kernel<3>, grid, dim3(PB_THREADS), lds, s, a); break;
         default: hipLaunchKernelGGL(preprocess_bwd_kernel<0>, grid, dim3(PB_THREADS), lds, s, a); break;
     }
