@@ -47,8 +47,9 @@ __global__ void __launch_bounds__(SX_THREADS) sh_from_colors_kernel(int P, int n
     // Views in groups of VB: the group's colour rows are loaded before any of its
     // products, so the loads of VB views are in flight together (one view at a
     // time left the kernel waiting on each view's load: 97 us for 8 views at
-    // 1M Gaussians, vs 34 us for one).  Sums stay in view order.
-    constexpr int VB = 4;
+    // 1M Gaussians, vs 34 us for one; groups of 4: 83 us, of 8: 79 us).  Sums
+    // stay in view order.
+    constexpr int VB = 8;
     for (int v0 = 0; v0 < nviews; v0 += VB) {
         float dv[VB][3];
 #pragma unroll
@@ -86,6 +87,8 @@ __global__ void __launch_bounds__(SX_THREADS) sh_from_colors_kernel(int P, int n
 #pragma unroll
         for (int c = 0; c < 3; c++) dsh_dc[3 * (size_t)idx + c] = acc[c];
     }
+    // (per-thread dword stores of the 180-B rows instead of the LDS stage: 71 vs
+    // 34 us for one view)
     if constexpr (RW > 0) {
         float *row = lds + threadIdx.x * (RW + 1);
 #pragma unroll
