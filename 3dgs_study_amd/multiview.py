@@ -64,10 +64,12 @@ class GradAllReduce:
     docstring); it engages when the group has more than one rank, or always with
     ``sh_force=True`` (tests).  ``views_per_step``: backwards each rank runs per step
     (the overlapped all-reduces start on the last one).  ``rebuild`` replaces the HIP
-    kernel that turns gathered records into the SH gradients (CPU tests only)."""
+    kernel that turns gathered records into the SH gradients (CPU tests only).
+    ``comm_force=True`` runs every collective even in a one-rank group (tests: the
+    RCCL calls on a one-GPU box)."""
 
     def __init__(self, params: ParamSource, group=None, overlap: bool = True, sh=None, sh_force: bool = False,
-                 rebuild=None, views_per_step: int = 1):
+                 rebuild=None, views_per_step: int = 1, comm_force: bool = False):
         if views_per_step < 1:
             raise ValueError("views_per_step must be >= 1")
         self._params_src = params
@@ -75,6 +77,7 @@ class GradAllReduce:
         self.group = group
         self.overlap = overlap
         self.views_per_step = views_per_step
+        self._comm_force = comm_force  # run the collectives even in a one-rank group (RCCL smoke tests)
         self._rebuild = rebuild
         self._works = []       # (param, work) of the all-reduces started from hooks
         self._hooks = []
@@ -133,7 +136,7 @@ class GradAllReduce:
         return self._sh is not None
 
     def _active(self) -> bool:
-        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+        return dist.is_initialized() and (dist.get_world_size(self.group) > 1 or self._comm_force)
 
     # ---- the rasterizer's SH sink (diff_gaussian_rasterization.set_sh_grad_sink)
     def accepts(self, sh: torch.Tensor, means3D: torch.Tensor) -> bool:
@@ -249,13 +252,13 @@ class GradAllReduce:
 
 @torch.no_grad()
 def reduce_densification_stats(xyz_gradient_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
-                               group=None) -> None:
+                               group=None, force: bool = False) -> None:
     """Combine the ranks' densification statistics in place before a densify step:
     SUM of the accumulated screen-space gradient norms and of the visibility counts,
     MAX of the largest screen radii (scene/gaussian_model.py:565-581 accumulates them
     per view; train.py:126-127 and :130-136 use them), so every rank densifies and
     prunes the same Gaussians and the replicas stay identical."""
-    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+    if not (dist.is_initialized() and (dist.get_world_size(group) > 1 or force)):
         return
     both = torch.cat([xyz_gradient_accum.reshape(-1), denom.reshape(-1)])
     w1 = dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group, async_op=True)

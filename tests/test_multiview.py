@@ -664,3 +664,62 @@ def test_config_d_eight_ranks_on_one_gpu(dev, sh_exchange, tmp_path):
         ref = ref.cpu()
         rel = (a - ref).norm() / ref.norm().clamp_min(1e-30)
         assert rel < 1e-5, float(rel)
+
+
+def _rccl_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    for p in (str(PKG), str(ROOT), str(ROOT / "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    import synthetic
+    import train_step
+    from multiview import GradAllReduce, reduce_densification_stats
+
+    cam = synthetic.make_camera(200, 150, view=2).to(dev)
+    target = synthetic.make_target(200, 150).to(dev)
+    res = {}
+    for mode in ("plain", "allreduce", "sh_colour"):
+        g = synthetic.make_gaussians(30_000, 3, seed=4).to(dev, requires_grad=True)
+        params = g.params()
+        ar = None
+        if mode != "plain":
+            ar = GradAllReduce(params, sh=(params[0], params[1], params[2]) if mode == "sh_colour" else None,
+                               comm_force=True)
+        train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
+        if ar is not None:
+            ar()
+            ar.remove_hooks()
+        stats = [torch.rand(30_000, 1, device=dev), torch.rand(30_000, 1, device=dev), torch.rand(30_000, device=dev)]
+        ref = [t.clone() for t in stats]
+        reduce_densification_stats(*stats, force=True)
+        torch.cuda.synchronize()
+        res[mode] = ([p.grad.detach().cpu().clone() for p in params],
+                     all(torch.equal(a, b) for a, b in zip(stats, ref)))
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_one_rank(dev):
+    """The exchange's RCCL calls on the real backend ("nccl" = RCCL), which the
+    one-GPU box can only run as a one-rank group: the overlapped all-reduces from the
+    post-accumulate-grad hooks, the all-gather of the SH colour records, and the
+    densification statistics' SUM / MAX all-reduces, forced on.  With one rank every
+    collective is the identity, so the gradients must equal the plain step's and the
+    statistics must come back unchanged."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_rccl_worker, args=(1, port, out), nprocs=1, join=True)
+        res = dict(out)[0]
+    plain = res["plain"][0]
+    for mode in ("allreduce", "sh_colour"):
+        grads, stats_same = res[mode]
+        assert stats_same, mode
+        for i, (a, b) in enumerate(zip(grads, plain)):
+            rel = (a - b).norm() / b.norm().clamp_min(1e-30)
+            assert rel < 1e-5, (mode, i, float(rel))
