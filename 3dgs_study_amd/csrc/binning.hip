@@ -307,9 +307,16 @@ __global__ void __launch_bounds__(TOPSCAN_THREADS) exclusive_scan_one_block_kern
 }
 
 // duplicateWithKeys in rank order: (tile, id) for every tile of the rect.
-// The workgroup's 256 Gaussians own one contiguous run of instances; threads
-// take consecutive instances (coalesced stores) and find their Gaussian by a
-// binary search over the LDS offsets.
+// The workgroup's 256 Gaussians own one contiguous run of instances.  Each thread
+// takes EMIT_IPT consecutive instances: one binary search over the LDS offsets
+// finds the Gaussian of the first, then the thread walks on, moving to the next
+// Gaussian at each offset it passes and to the next tile incrementally (the next
+// column of the rect, or the next set bit of its tile mask); the round's
+// instances leave through LDS, coalesced.  Config E: 189 -> 175 us (one search
+// per instance: 8 dependent LDS reads and a k-th-set-bit search each); 16
+// instances per thread left too few threads busy per workgroup at config C
+// (28 -> 50 us), and stores straight from the walk were uncoalesced (58 us).
+constexpr int EMIT_IPT = 4;
 struct EmitArgs {
     int P, gx;
     const uint32_t *order;
@@ -318,6 +325,12 @@ struct EmitArgs {
     uint32_t *tile_keys;
     uint32_t *ids;
 };
+__device__ __forceinline__ uint32_t div_small(uint32_t pos, uint32_t w) {  // pos / w for pos < 2^24
+    uint32_t y = (uint32_t)((float)pos * __builtin_amdgcn_rcpf((float)w));
+    if (y * w > pos) y--;
+    if ((y + 1) * w <= pos) y++;
+    return y;
+}
 __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
     __shared__ uint32_t wsum[EMIT_BLOCK / 64];
     __shared__ uint32_t loff[EMIT_BLOCK + 1];
@@ -337,24 +350,68 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
     }
     __syncthreads();
     const uint32_t base = a.block_prefix[blockIdx.x];
-    for (uint32_t j = threadIdx.x; j < tot; j += EMIT_BLOCK) {
-        int lo = 0, hi = EMIT_BLOCK;  // largest k with loff[k] <= j (it has v > 0)
+    // a round's EMIT_BLOCK x EMIT_IPT instances go through LDS (thread t's run at
+    // stride EMIT_IPT + 1 words: conflict-free) and leave coalesced
+    constexpr int RS = EMIT_IPT + 1;
+    __shared__ uint32_t kbuf[EMIT_BLOCK * RS], ibuf[EMIT_BLOCK * RS];
+    for (uint32_t r0 = 0; r0 < tot; r0 += EMIT_BLOCK * EMIT_IPT) {
+        const uint32_t j0 = r0 + threadIdx.x * EMIT_IPT;
+        if (j0 < tot) {
+            int g = 0, hi = EMIT_BLOCK;  // largest g with loff[g] <= j0 (it has v > 0)
 #pragma unroll
-        for (int step = 0; step < 8; step++) {
-            const int mid = (lo + hi) >> 1;
-            if (loff[mid] <= j) lo = mid; else hi = mid;
+            for (int step = 0; step < 8; step++) {
+                const int mid = (g + hi) >> 1;
+                if (loff[mid] <= j0) g = mid; else hi = mid;
+            }
+            uint32_t end_g = loff[g + 1];
+            uint4 rc = rect[g];
+            uint2 mk = mask[g];
+            bool full = (mk.x & mk.y) == ~0u;
+            // current tile: row y, column x of the rect; for a mask, rem = its set
+            // bits above the current one
+            uint32_t pos = full ? j0 - loff[g] : kth_set_bit(mk.x, mk.y, j0 - loff[g]);
+            uint64_t rem = full ? 0ull : ((((uint64_t)mk.y << 32) | mk.x) & ~((2ull << pos) - 1ull));
+            uint32_t y = div_small(pos, rc.y), x = pos - y * rc.y;
+            const uint32_t n = min((uint32_t)EMIT_IPT, tot - j0);
+            for (uint32_t t = 0; t < n; t++) {
+                const uint32_t j = j0 + t;
+                if (j >= end_g) {  // the next Gaussian with instances
+                    do {
+                        g++;
+                        end_g = loff[g + 1];
+                    } while (j >= end_g);
+                    rc = rect[g];
+                    mk = mask[g];
+                    full = (mk.x & mk.y) == ~0u;
+                    const uint64_t m = ((uint64_t)mk.y << 32) | mk.x;
+                    pos = full ? 0u : (uint32_t)__builtin_ctzll(m);
+                    rem = full ? 0ull : m & (m - 1ull);
+                    y = full ? 0u : div_small(pos, rc.y);
+                    x = pos - y * rc.y;
+                }
+                kbuf[threadIdx.x * RS + t] = (rc.z + y) * (uint32_t)a.gx + rc.x + x;
+                ibuf[threadIdx.x * RS + t] = rc.w;
+                if (full) {
+                    if (++x == rc.y) {
+                        x = 0;
+                        y++;
+                    }
+                } else if (rem) {
+                    pos = (uint32_t)__builtin_ctzll(rem);
+                    rem &= rem - 1ull;
+                    y = div_small(pos, rc.y);
+                    x = pos - y * rc.y;
+                }
+            }
         }
-        const uint4 rc = rect[lo];
-        const uint2 mk = mask[lo];
-        const uint32_t k = j - loff[lo];
-        // position in the rect (row-major): the k-th kept tile
-        const uint32_t pos = (mk.x & mk.y) == ~0u ? k : kth_set_bit(mk.x, mk.y, k);
-        uint32_t y = (uint32_t)((float)pos * __builtin_amdgcn_rcpf((float)rc.y));
-        if (y * rc.y > pos) y--;
-        if ((y + 1) * rc.y <= pos) y++;
-        const uint32_t x = pos - y * rc.y;
-        a.tile_keys[base + j] = (rc.z + y) * (uint32_t)a.gx + rc.x + x;
-        a.ids[base + j] = rc.w;
+        __syncthreads();
+        const uint32_t nr = min((uint32_t)(EMIT_BLOCK * EMIT_IPT), tot - r0);
+        for (uint32_t i = threadIdx.x; i < nr; i += EMIT_BLOCK) {
+            const uint32_t li = (i / EMIT_IPT) * RS + i % EMIT_IPT;
+            a.tile_keys[base + r0 + i] = kbuf[li];
+            a.ids[base + r0 + i] = ibuf[li];
+        }
+        __syncthreads();
     }
 }
 
