@@ -1,12 +1,12 @@
 // gsr_rows.hpp — coalesced staging of per-Gaussian rows through LDS.
 //
-// The SH block of a Gaussian is a 12·M-byte row (192 B at SH degree 3).  A
-// thread-per-Gaussian kernel that reads its own row directly issues 48 dword
-// loads per lane whose 64 addresses sit 192 B apart: every wave-instruction
-// touches 64 cache lines.  Instead the workgroup streams its contiguous slice
-// of rows with 16-byte-per-lane loads into LDS rows padded to an odd number
-// of dwords (bank-conflict-free per-lane row reads), and writes gradients back
-// the same way.
+// The SH block of a Gaussian is a 12·M-byte row (192 B at SH degree 3).  The
+// preprocess kernels load a degree-3 row per thread straight into registers
+// (12 x 16 B; preprocess.hip).  For the other widths, and for the SH rebuild of
+// the view exchange (sh_exchange.hip, 180-B rows whose per-thread stores were
+// 2x slower), the workgroup streams its contiguous slice of rows with
+// 16-byte-per-lane accesses through LDS rows padded to an odd number of dwords
+// (bank-conflict-free per-lane row access).
 #pragma once
 
 #include <hip/hip_runtime.h>
