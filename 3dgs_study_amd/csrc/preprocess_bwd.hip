@@ -397,13 +397,13 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     const size_t lds = stage && !direct ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     const dim3 grid((in.P + PB_THREADS - 1) / PB_THREADS);
     switch (3 * in.M) {  // see launch_preprocess
-        case 48:  // the direct-row kernel needs staged, 16-B aligned rows
+        case 3: hipLaunchKernelGGL(preprocess_bwd_kernel<3>, grid, dim3(PB_THREADS), lds, s, a); break;
+        case 48:  // the direct-row kernel needs staged, 16-B aligned rows; else the run-time width
             if (direct) {
                 hipLaunchKernelGGL(preprocess_bwd_kernel<48>, grid, dim3(PB_THREADS), lds, s, a);
                 break;
             }
             [[fallthrough]];
-        case 3: hipLaunchKernelGGL(preprocess_bwd_kernel<3>, grid, dim3(PB_THREADS), lds, s, a); break;
         default: hipLaunchKernelGGL(preprocess_bwd_kernel<0>, grid, dim3(PB_THREADS), lds, s, a); break;
     }
     return hipGetLastError();

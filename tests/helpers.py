@@ -35,13 +35,16 @@ def activated(g, python_branch=False, scale_modifier=1.0):
 
 
 def run_hip(cam, g, dev, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=None, python_branch=False,
-            dL=None, debug=False, dsh_planar=False, footprint="rect"):
+            dL=None, debug=False, dsh_planar=False, footprint="rect", misalign_sh=False):
     from diff_gaussian_rasterization import _C
 
     a = activated(g, python_branch, scale_modifier)
     t = lambda x: x.to(dev) if x is not None else torch.empty(0, device=dev)  # noqa: E731
     bg_t = torch.tensor(bg, dtype=torch.float32, device=dev)
     shs = t(a["shs"]) if colors_precomp is None else t(None)
+    if misalign_sh and shs.numel():  # contiguous, 4 B past a 16-B boundary: the LDS-staged row path
+        buf = torch.empty(shs.numel() + 1, dtype=shs.dtype, device=dev)
+        shs = buf[1:].view_as(shs).copy_(shs)
     colors = t(torch.as_tensor(colors_precomp, dtype=torch.float32)) if colors_precomp is not None else t(None)
     args = (bg_t, t(a["means3D"]), colors, t(a["opacities"]), t(a.get("scales")), t(a.get("rotations")),
             float(scale_modifier), t(a.get("cov3D_precomp")), t(cam.world_view_transform),

@@ -232,6 +232,7 @@ def check_backward(h, rb, tol=GRAD_TOL, names=("dmeans2D", "dcolors", "dopacity"
     dict(P=10_000, W=256, H=256, deg=0, view=0),                  # config A
     dict(P=20_000, W=333, H=201, deg=3, view=3, active=2),        # ragged image, D < max degree
     dict(P=20_003, W=160, H=120, deg=3, view=5),                  # P % 4 != 0: unaligned coefficient planes
+    dict(P=8_000, W=200, H=150, deg=2, view=1),                   # M = 9: the run-time row width (LDS-staged)
     dict(P=100_000, W=800, H=800, deg=3, view=0),                 # config B
 ])
 @pytest.mark.parametrize("mode", ["rect", "tight", "rect-planar"])
@@ -458,3 +459,21 @@ def test_depth_sort_pass_count(dev, oracle, radius, passes, footprint):
     r = run_oracle(oracle, cam, g)
     check_forward(h, r)
     check_backward(h, oracle.backward(r, dL))
+
+
+def test_sh_rows_unaligned_take_the_staged_path(dev):
+    """Degree-3 SH rows load per thread as 16-B vectors when 16-B aligned
+    (preprocess.hip / preprocess_bwd.hip); a misaligned SH tensor takes the
+    LDS-staged path instead.  Both give the same image and radii bit for bit and the
+    same gradients (up to the float atomics' order in render_bwd)."""
+    import synthetic
+
+    cam = synthetic.make_camera(333, 201, view=2)
+    g = synthetic.make_gaussians(20_000, 3, seed=11)
+    dL = random_dL(201, 333, seed=5)
+    a = run_hip(cam, g, dev, dL=dL)
+    b = run_hip(cam, g, dev, dL=dL, misalign_sh=True)
+    np.testing.assert_array_equal(a["radii"], b["radii"])
+    np.testing.assert_array_equal(a["color"], b["color"])
+    for n in a["grads"]:
+        assert rel_l2(b["grads"][n], a["grads"][n]) <= 1e-6, n
