@@ -27,13 +27,24 @@ namespace gsr {
 //   dS/de12 = 2 S/A2,
 // and dL/dx(p) = (1-l)/N sign(x-y) + G*(dL/dS dS/dm1) + 2 x G*(dL/dS dS/de11)
 //              + y G*(dL/dS dS/de12)   (G symmetric: correlation == convolution).
-// A workgroup owns a 32x16 output tile of one channel and everything it needs
-// in LDS: the inputs over tile +- 10 px, the five blurred maps over tile +- 5 px,
-// the three derivative maps, and their blur back onto the tile.
-constexpr int SS_TX = 32, SS_TY = 16, SS_R = 5;                 // tile, window radius
-constexpr int SS_IX = SS_TX + 4 * SS_R, SS_IY = SS_TY + 4 * SS_R;  // input region 52 x 36
-constexpr int SS_MX = SS_TX + 2 * SS_R, SS_MY = SS_TY + 2 * SS_R;  // map region 42 x 26
-constexpr int SS_THREADS = 256;
+// A workgroup owns a 32x32 output tile of one channel and runs four separable
+// passes through LDS, each register-blocked so that a thread reuses the values it
+// reads: (1) the horizontal 11-tap sums of the five products (x, y, x^2, y^2, xy)
+// over the input rows, 3 map columns per thread; (2) the vertical sums, 7 map rows
+// per thread, then the SSIM terms and the three derivative maps; (3) and (4) the
+// derivative maps blurred back onto the tile the same way, 4 and 2 outputs per thread,
+// with the L1 term and the gradient.  512-thread workgroups: the LDS (65 KB)
+// allows two per CU, i.e. 4 waves per SIMD.  3x1080x1920: 134 us (round 1 read
+// one LDS operand per tap: 295 us, LDS-bound).
+constexpr int SS_T = 32, SS_R = 5;           // tile (square), window radius
+constexpr int SS_I = SS_T + 4 * SS_R;        // input region 52 x 52
+constexpr int SS_M = SS_T + 2 * SS_R;        // map region 42 x 42
+constexpr int SS_TX = SS_T, SS_TY = SS_T;
+constexpr int SS_THREADS = 512;  // 8 waves: 2 workgroups (16 waves) per CU within the LDS
+// outputs per thread in passes 1-4 (swept at 3x1080x1920: pass 1/2 blocking of
+// (6, 6) 158 us, (3, 3) 140, (3, 7) 134, (7, 3) 142, (2, 2) 155)
+constexpr int SS_B1 = 3, SS_B2 = 7, SS_B3 = 4, SS_B4 = 2;
+static_assert(SS_M % SS_B1 == 0 && SS_M % SS_B2 == 0 && SS_T % SS_B3 == 0 && SS_T % SS_B4 == 0, "blocking");
 
 struct SsimArgs {
     const float *x, *y;
@@ -45,110 +56,159 @@ struct SsimArgs {
 };
 
 __global__ void __launch_bounds__(SS_THREADS) l1_ssim_kernel(SsimArgs a) {
-    __shared__ float xs[SS_IY][SS_IX], ys[SS_IY][SS_IX];
-    __shared__ float hb[5][SS_IY][SS_MX];  // horizontal pass of x, y, xx, yy, xy
-    __shared__ float mp[5][SS_MY][SS_MX];  // m1, m2, e11, e22, e12 -> then dS terms a, b, c
+    // xy: the inputs (passes 1), then the derivative maps (passes 2-3);
+    // hb: the horizontal sums (passes 1-2), then the blurred-back rows (3-4)
+    __shared__ float xy[2 * SS_I * SS_I > 3 * SS_M * SS_M ? 2 * SS_I * SS_I : 3 * SS_M * SS_M];
+    __shared__ float hb[5][SS_I][SS_M];
     __shared__ float red[2][SS_THREADS / 64];
+    float(*xs)[SS_I] = reinterpret_cast<float(*)[SS_I]>(xy);
+    float(*ys)[SS_I] = reinterpret_cast<float(*)[SS_I]>(xy + SS_I * SS_I);
+    float(*dm)[SS_M][SS_M] = reinterpret_cast<float(*)[SS_M][SS_M]>(xy);
     const int c = blockIdx.z;
-    const int ox = blockIdx.x * SS_TX, oy = blockIdx.y * SS_TY;
+    const int ox = blockIdx.x * SS_T, oy = blockIdx.y * SS_T;
     const size_t plane = (size_t)a.H * a.W;
     const float *X = a.x + c * plane, *Y = a.y + c * plane;
     const int t = threadIdx.x;
+    float gw[11];
+#pragma unroll
+    for (int k = 0; k < 11; k++) gw[k] = a.g[k];
     // inputs over the tile +- 2R, zero outside the image (conv2d zero padding)
-    for (int i = t; i < SS_IX * SS_IY; i += SS_THREADS) {
-        const int ry = i / SS_IX, rx = i - ry * SS_IX;
+    for (int i = t; i < SS_I * SS_I; i += SS_THREADS) {
+        const int ry = i / SS_I, rx = i - ry * SS_I;
         const int gy = oy - 2 * SS_R + ry, gx = ox - 2 * SS_R + rx;
         const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
         xs[ry][rx] = in ? X[(size_t)gy * a.W + gx] : 0.f;
         ys[ry][rx] = in ? Y[(size_t)gy * a.W + gx] : 0.f;
     }
     __syncthreads();
-    // horizontal pass of the five products onto columns [ox - R, ox + TX + R)
-    for (int i = t; i < SS_IY * SS_MX; i += SS_THREADS) {
-        const int ry = i / SS_MX, mx = i - ry * SS_MX;
-        float s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+    // (1) horizontal sums over every input row, map columns [c0, c0 + B1)
+    for (int item = t; item < SS_I * (SS_M / SS_B1); item += SS_THREADS) {
+        const int row = item / (SS_M / SS_B1), c0 = (item - row * (SS_M / SS_B1)) * SS_B1;
+        float xv[SS_B1 + 10], yv[SS_B1 + 10];
 #pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float xv = xs[ry][mx + k], yv = ys[ry][mx + k], w = a.g[k];
-            s0 += w * xv;
-            s1 += w * yv;
-            s2 += w * (xv * xv);
-            s3 += w * (yv * yv);
-            s4 += w * (xv * yv);
+        for (int k = 0; k < SS_B1 + 10; k++) {
+            xv[k] = xs[row][c0 + k];
+            yv[k] = ys[row][c0 + k];
         }
-        hb[0][ry][mx] = s0;
-        hb[1][ry][mx] = s1;
-        hb[2][ry][mx] = s2;
-        hb[3][ry][mx] = s3;
-        hb[4][ry][mx] = s4;
+#pragma unroll
+        for (int o = 0; o < SS_B1; o++) {
+            float s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+#pragma unroll
+            for (int k = 0; k < 11; k++) {
+                const float u = xv[o + k], v = yv[o + k], w = gw[k];
+                s0 += w * u;
+                s1 += w * v;
+                s2 += w * (u * u);
+                s3 += w * (v * v);
+                s4 += w * (u * v);
+            }
+            hb[0][row][c0 + o] = s0;
+            hb[1][row][c0 + o] = s1;
+            hb[2][row][c0 + o] = s2;
+            hb[3][row][c0 + o] = s3;
+            hb[4][row][c0 + o] = s4;
+        }
     }
     __syncthreads();
-    // vertical pass -> maps over the tile +- R; then the per-pixel SSIM terms
+    // (2) vertical sums -> maps over the tile +- R, map rows [r0, r0 + B2) of a
+    // column; then the per-pixel SSIM terms and the derivative maps (over xs/ys)
     const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
     const float dLdS = -a.lambda * a.invN;
     float ssum = 0.f;
-    for (int i = t; i < SS_MY * SS_MX; i += SS_THREADS) {
-        const int my = i / SS_MX, mx = i - my * SS_MX;
-        float m[5] = {0, 0, 0, 0, 0};
+    for (int item = t; item < SS_M * (SS_M / SS_B2); item += SS_THREADS) {
+        const int col = item % SS_M, r0 = (item / SS_M) * SS_B2;
+        float m[SS_B2][5];
 #pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float w = a.g[k];
+        for (int o = 0; o < SS_B2; o++)
 #pragma unroll
-            for (int q = 0; q < 5; q++) m[q] += w * hb[q][my + k][mx];
+            for (int q = 0; q < 5; q++) m[o][q] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            float hv[SS_B2 + 10];
+#pragma unroll
+            for (int k = 0; k < SS_B2 + 10; k++) hv[k] = hb[q][r0 + k][col];
+#pragma unroll
+            for (int o = 0; o < SS_B2; o++)
+#pragma unroll
+                for (int k = 0; k < 11; k++) m[o][q] += gw[k] * hv[o + k];
         }
-        const int gy = oy - SS_R + my, gx = ox - SS_R + mx;
-        const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-        const float m1 = m[0], m2 = m[1];
-        const float m1m2 = m1 * m2, m1s = m1 * m1, m2s = m2 * m2;
-        const float s1 = m[2] - m1s, s2 = m[3] - m2s, s12 = m[4] - m1m2;
-        const float A1 = 2 * m1m2 + C1, A2 = 2 * s12 + C2, B1 = m1s + m2s + C1, B2 = s1 + s2 + C2;
-        const float S = (A1 * A2) / (B1 * B2);
-        const bool own = in && my >= SS_R && my < SS_R + SS_TY && mx >= SS_R && mx < SS_R + SS_TX;
-        ssum += own ? S : 0.f;
-        // derivative maps (zero outside the image: those S do not exist)
-        const float k1 = in ? dLdS * S : 0.f;
-        mp[0][my][mx] = k1 * (2 * m2 / A1 - 2 * m2 / A2 - 2 * m1 / B1 + 2 * m1 / B2);
-        mp[1][my][mx] = -k1 / B2;
-        mp[2][my][mx] = 2 * k1 / A2;
+#pragma unroll
+        for (int o = 0; o < SS_B2; o++) {
+            const int my = r0 + o;
+            const int gy = oy - SS_R + my, gx = ox - SS_R + col;
+            const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+            const float m1 = m[o][0], m2 = m[o][1];
+            const float m1m2 = m1 * m2, m1s = m1 * m1, m2s = m2 * m2;
+            const float s1 = m[o][2] - m1s, s2 = m[o][3] - m2s, s12 = m[o][4] - m1m2;
+            const float A1 = 2 * m1m2 + C1, A2 = 2 * s12 + C2, B1 = m1s + m2s + C1, B2 = s1 + s2 + C2;
+            // four hardware reciprocals (1 ulp) instead of seven IEEE divisions
+            const float iA1 = __builtin_amdgcn_rcpf(A1), iA2 = __builtin_amdgcn_rcpf(A2);
+            const float iB1 = __builtin_amdgcn_rcpf(B1), iB2 = __builtin_amdgcn_rcpf(B2);
+            const float S = (A1 * A2) * (iB1 * iB2);
+            const bool own = in && my >= SS_R && my < SS_R + SS_T && col >= SS_R && col < SS_R + SS_T;
+            ssum += own ? S : 0.f;
+            // derivative maps (zero outside the image: those S do not exist); written
+            // after every thread's pass-1 use of xs / ys (the barrier above)
+            const float k1 = in ? dLdS * S : 0.f;
+            dm[0][my][col] = k1 * (2 * m2 * (iA1 - iA2) + 2 * m1 * (iB2 - iB1));
+            dm[1][my][col] = -k1 * iB2;
+            dm[2][my][col] = 2 * k1 * iA2;
+        }
     }
     __syncthreads();
-    // blur the derivative maps back: horizontal onto the tile's columns (reuse hb)
-    for (int i = t; i < SS_MY * SS_TX; i += SS_THREADS) {
-        const int my = i / SS_TX, tx = i - my * SS_TX;
-        float s0 = 0, s1 = 0, s2 = 0;
+    // (3) horizontal blur of the derivative maps onto the tile columns [c0, c0 + B3)
+    for (int item = t; item < SS_M * (SS_T / SS_B3); item += SS_THREADS) {
+        const int row = item / (SS_T / SS_B3), c0 = (item - row * (SS_T / SS_B3)) * SS_B3;
 #pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float w = a.g[k];
-            s0 += w * mp[0][my][tx + k];
-            s1 += w * mp[1][my][tx + k];
-            s2 += w * mp[2][my][tx + k];
+        for (int q = 0; q < 3; q++) {
+            float dv[SS_B3 + 10];
+#pragma unroll
+            for (int k = 0; k < SS_B3 + 10; k++) dv[k] = dm[q][row][c0 + k];
+#pragma unroll
+            for (int o = 0; o < SS_B3; o++) {
+                float sacc = 0.f;
+#pragma unroll
+                for (int k = 0; k < 11; k++) sacc += gw[k] * dv[o + k];
+                hb[q][row][c0 + o] = sacc;
+            }
         }
-        hb[0][my][tx] = s0;
-        hb[1][my][tx] = s1;
-        hb[2][my][tx] = s2;
     }
     __syncthreads();
+    // (4) vertical blur onto the tile rows [r0, r0 + B4) of a column; L1 term; gradient
     float l1sum = 0.f;
-    const float kl1 = (1.f - a.lambda) * a.invN;
-    float *G = a.grad + c * plane;
-    for (int i = t; i < SS_TX * SS_TY; i += SS_THREADS) {
-        const int ty = i / SS_TX, tx = i - ty * SS_TX;
-        const int gy = oy + ty, gx = ox + tx;
-        if (gy >= a.H || gx >= a.W) continue;
-        float b0 = 0, b1 = 0, b2 = 0;
+    {
+        const int col = t % SS_T, r0 = (t / SS_T) * SS_B4;
+        float b[SS_B4][3];
 #pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float w = a.g[k];
-            b0 += w * hb[0][ty + k][tx];
-            b1 += w * hb[1][ty + k][tx];
-            b2 += w * hb[2][ty + k][tx];
+        for (int q = 0; q < 3; q++) {
+            float hv[SS_B4 + 10];
+#pragma unroll
+            for (int k = 0; k < SS_B4 + 10; k++) hv[k] = hb[q][r0 + k][col];
+#pragma unroll
+            for (int o = 0; o < SS_B4; o++) {
+                float sacc = 0.f;
+#pragma unroll
+                for (int k = 0; k < 11; k++) sacc += gw[k] * hv[o + k];
+                b[o][q] = sacc;
+            }
         }
-        const float xv = xs[ty + 2 * SS_R][tx + 2 * SS_R], yv = ys[ty + 2 * SS_R][tx + 2 * SS_R];
-        const float d = xv - yv;
-        l1sum += fabsf(d);
-        const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // torch.sign
-        G[(size_t)gy * a.W + gx] = kl1 * sg + b0 + 2.f * xv * b1 + yv * b2;
+        const float kl1 = (1.f - a.lambda) * a.invN;
+        float *G = a.grad + c * plane;
+        const int gx = ox + col;
+#pragma unroll
+        for (int o = 0; o < SS_B4; o++) {
+            const int gy = oy + r0 + o;
+            if (gy < a.H && gx < a.W) {
+                const size_t pix = (size_t)gy * a.W + gx;
+                const float xv = X[pix], yv = Y[pix];
+                const float d = xv - yv;
+                l1sum += fabsf(d);
+                const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // torch.sign
+                G[pix] = kl1 * sg + b[o][0] + 2.f * xv * b[o][1] + yv * b[o][2];
+            }
+        }
     }
+    static_assert(SS_T * (SS_T / SS_B4) == SS_THREADS, "pass 4: one item per thread");
     // workgroup partial sums (the loss value itself is finished by l1_ssim_finish)
     const float l1w = wave_sum(l1sum), ssw = wave_sum(ssum);
     if ((t & 63) == 0) {
@@ -162,9 +222,9 @@ __global__ void __launch_bounds__(SS_THREADS) l1_ssim_kernel(SsimArgs a) {
             s0 += red[0][k];
             s1 += red[1][k];
         }
-        const size_t b = ((size_t)c * a.tiles_y + blockIdx.y) * a.tiles_x + blockIdx.x;
-        a.partials[2 * b] = s0;
-        a.partials[2 * b + 1] = s1;
+        const size_t blk = ((size_t)c * a.tiles_y + blockIdx.y) * a.tiles_x + blockIdx.x;
+        a.partials[2 * blk] = s0;
+        a.partials[2 * blk + 1] = s1;
     }
 }
 
