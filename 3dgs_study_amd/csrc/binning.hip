@@ -16,8 +16,14 @@
 //                   tile of its rect (row-major, as upstream) at its offset.
 //  4. tile sort   — stable LSD radix sort of the I instances by tile index
 //                   (ceil(log2 T / 8) passes: 2 at 1080p and 4K).  Stability
-//                   keeps rank order inside a tile, i.e. (depth_bits, id).
-//  5. ranges      — identifyTileRanges on the sorted tile keys.
+//                   keeps rank order inside a tile, i.e. (depth_bits, id).  In
+//                   the two-pass case the first pass writes one word per
+//                   instance, (high tile digit << id bits) | id, and the second
+//                   sorts those words by the high digit in blocks that never
+//                   straddle a low digit, writing only the ids: 28 B per
+//                   instance over both passes instead of 40 + 4.
+//  5. ranges      — from the second pass's per-block digit counts (two-pass
+//                   case), else identifyTileRanges on the sorted tile keys.
 //
 // Steps 1-2 run in gsr_forward_preprocess while the host reads num_rendered;
 // 3-5 run in gsr_forward_render once the caller has sized the binning buffer.
@@ -77,8 +83,20 @@ struct RadixPass {
     const uint32_t *ctrl;
     int role;              // RX_PLAIN, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH
     uint32_t *vout_final;  // RX_DEPTH_THIRD in three-pass mode: the order lands here
+    // packed two-pass tile sort (tile_sort_packed): the first pass (RXM_PACK)
+    // writes vout = (key >> pack_shift) << id_bits | value; the second
+    // (RXM_UNPACK) reads those words (digit = word >> shift, value = the id bits)
+    // in blocks aligned to the first pass's digit runs (seg_totals: 2^seg_bits
+    // segments, one low tile digit each) and fills the T tile ranges
+    const uint32_t *seg_totals;
+    int seg_bits;
+    int pack_shift;
+    int id_bits;
+    uint2 *ranges;
+    int T;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
+enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
 
 // First depth pass: key = depth bits - base, clamped to 24 bits in three-pass
 // mode (only invisible Gaussians, +inf keys, reach the clamp).
@@ -104,28 +122,65 @@ __device__ __forceinline__ uint32_t radix_block(int NB) {
     return x * q + min(x, r) + j;
 }
 
+// Items [x, y) of radix block blk.  Plain: TILE_N items per block.  RXM_UNPACK:
+// each segment (one digit run of the previous pass) starts a new block, so a
+// block's instances share their low tile digit and the digit counts per block
+// give the tile ranges; sfb / sst [RADIX + 1] (LDS) receive each segment's first
+// block and first item.  The grid has radix_blocks(n) + 2^seg_bits blocks, the
+// unused tail ones are empty.
+template <int TILE_N, int MODE>
+__device__ __forceinline__ uint2 block_span(const RadixPass &a, uint32_t blk, uint32_t *sfb, uint32_t *sst,
+                                            uint32_t *wsum) {
+    if constexpr (MODE != RXM_UNPACK) {
+        const uint32_t b0 = blk * (uint32_t)TILE_N;
+        return make_uint2(b0, min(b0 + (uint32_t)TILE_N, a.n));
+    } else {
+        const uint32_t c = (int)threadIdx.x < (1 << a.seg_bits) ? a.seg_totals[threadIdx.x] : 0u;
+        const uint32_t nb = (c + (uint32_t)TILE_N - 1u) / (uint32_t)TILE_N;
+        uint32_t totb, totc;
+        const uint32_t ib = block_inclusive_scan<RX_THREADS>(nb, wsum, &totb);
+        const uint32_t ic = block_inclusive_scan<RX_THREADS>(c, wsum, &totc);
+        sfb[threadIdx.x] = ib - nb;
+        sst[threadIdx.x] = ic - c;
+        if (threadIdx.x == 0) {
+            sfb[RADIX] = totb;
+            sst[RADIX] = totc;
+        }
+        __syncthreads();
+        int sg = 0;  // the last segment whose first block is <= blk (sfb is non-decreasing, sfb[0] = 0)
+#pragma unroll
+        for (int step = RADIX / 2; step >= 1; step >>= 1)
+            if (sfb[sg + step] <= blk) sg += step;
+        const uint32_t b0 = sst[sg] + (blk - sfb[sg]) * (uint32_t)TILE_N, send = sst[sg + 1];
+        return b0 < send ? make_uint2(b0, min(b0 + (uint32_t)TILE_N, send)) : make_uint2(0u, 0u);
+    }
+}
+
 // ITEMS per thread: fewer for short inputs (more workgroups, shorter serial
 // rank chains), more for long ones (fewer blocks in the digit scan).
-template <int ITEMS>
+template <int ITEMS, int MODE>
 __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) {
     constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
+    constexpr int SEG = MODE == RXM_UNPACK ? RADIX + 1 : 1;
     __shared__ uint32_t h[RX_WAVES][RADIX];
+    __shared__ uint32_t sfb[SEG], sst[SEG], wsum[RX_WAVES];
     if (pass_skipped(a)) return;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
-    __syncthreads();
     const uint32_t blk = radix_block(a.NB);
-    const uint32_t base = blk * (uint32_t)TILE_N + w * (uint32_t)WAVE_N + lane;
+    const uint2 span = block_span<TILE_N, MODE>(a, blk, sfb, sst, wsum);
+    __syncthreads();
+    const uint32_t base = span.x + w * (uint32_t)WAVE_N + lane;
     uint32_t kk[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
         const uint32_t idx = base + 64u * r;
-        kk[r] = idx < a.n ? load_key(a, idx) : 0u;
+        kk[r] = idx < span.y ? load_key(a, idx) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < ITEMS; r++)
-        if (base + 64u * r < a.n) atomicAdd(&h[w][(kk[r] >> a.shift) & a.dmask], 1u);  // order-free count
+        if (base + 64u * r < span.y) atomicAdd(&h[w][(kk[r] >> a.shift) & a.dmask], 1u);  // order-free count
     __syncthreads();
     uint32_t c = 0;
 #pragma unroll
@@ -150,14 +205,18 @@ __global__ void __launch_bounds__(256) radix_digit_scan_kernel(RadixPass a) {
     if (threadIdx.x == 0) a.totals[blockIdx.x] = carry;
 }
 
-template <int ITEMS>
+template <int ITEMS, int MODE>
 __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a) {
     constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
+    constexpr int SEG = MODE == RXM_UNPACK ? RADIX + 1 : 1;
     __shared__ uint32_t cnt[RX_WAVES][RADIX];
     __shared__ uint32_t lstart[RADIX];   // block-local start of each digit's run
     __shared__ uint32_t gstart[RADIX];   // global start of this block's run of each digit
+    __shared__ uint32_t dstart[SEG];     // RXM_UNPACK: global start of each digit
     __shared__ uint32_t wsum[RX_WAVES];
-    __shared__ uint32_t stage_k[TILE_N], stage_v[TILE_N];
+    __shared__ uint32_t sfb[SEG], sst[SEG];
+    // RXM_UNPACK stages the packed words alone (the value is in the word)
+    __shared__ uint32_t stage_k[TILE_N], stage_v[MODE == RXM_UNPACK ? 1 : TILE_N];
     if (pass_skipped(a)) return;
     // three-pass depth sort: the third pass is the last one
     const bool final3 = a.role == RX_DEPTH_THIRD && a.ctrl[CTRL_DSORT_PASSES] == 3;
@@ -166,21 +225,23 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     const bool gather = a.gdst && (a.role != RX_DEPTH_THIRD || final3);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t blk = radix_block(a.NB);
-    const uint32_t b0 = blk * (uint32_t)TILE_N;
+    const uint2 span = block_span<TILE_N, MODE>(a, blk, sfb, sst, wsum);
+    const uint32_t b0 = span.x;
     const uint32_t base = b0 + w * (uint32_t)WAVE_N + lane;
-    uint32_t kk[ITEMS], vv[ITEMS], rk[ITEMS];
+    uint32_t kk[ITEMS], vv[MODE == RXM_UNPACK ? 1 : ITEMS], rk[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
         const uint32_t idx = base + 64u * r;
-        const bool ok = idx < a.n;
+        const bool ok = idx < span.y;
         kk[r] = ok ? load_key(a, idx) : 0u;
-        vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
+        if constexpr (MODE != RXM_UNPACK) vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
     }
     {  // where this block's items of digit d go: all smaller digits + earlier blocks
         const uint32_t t = a.totals[threadIdx.x];
         uint32_t tot;
         const uint32_t inc = block_inclusive_scan<RX_THREADS>(t, wsum, &tot);
         gstart[threadIdx.x] = inc - t + a.hist[(size_t)threadIdx.x * a.NB + blk];
+        if constexpr (MODE == RXM_UNPACK) dstart[threadIdx.x] = inc - t;
     }
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) cnt[k][threadIdx.x] = 0;
@@ -188,7 +249,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     // stable ranks inside each wave's quarter
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
-        const bool ok = base + 64u * r < a.n;
+        const bool ok = base + 64u * r < span.y;
         const uint64_t live = __ballot(ok);
         if (!live) break;
         const uint32_t d = (kk[r] >> a.shift) & a.dmask;
@@ -221,33 +282,57 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     // block-sorted image in LDS ...
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
-        if (base + 64u * r < a.n) {
+        if (base + 64u * r < span.y) {
             const uint32_t d = (kk[r] >> a.shift) & a.dmask;
             const uint32_t p = cnt[w][d] + rk[r];
             stage_k[p] = kk[r];
-            stage_v[p] = vv[r];
+            if constexpr (MODE != RXM_UNPACK) stage_v[p] = vv[r];
         }
     }
     __syncthreads();
     // ... written out in order: each digit's run is contiguous in the output too
-    const uint32_t nb = min((uint32_t)TILE_N, a.n - b0);
+    const uint32_t nb = span.y - b0;
     for (uint32_t i = threadIdx.x; i < nb; i += RX_THREADS) {
         const uint32_t k = stage_k[i];
         const uint32_t d = (k >> a.shift) & a.dmask;
         const uint32_t pos = gstart[d] + (i - lstart[d]);
-        const uint32_t v = stage_v[i];
-        if (kout) kout[pos] = k;
-        vout[pos] = v;
-        if (gather) a.gdst[pos] = a.gsrc[v];
+        if constexpr (MODE == RXM_UNPACK) {
+            vout[pos] = k & ((1u << a.id_bits) - 1u);
+        } else if constexpr (MODE == RXM_PACK) {
+            vout[pos] = ((k >> a.pack_shift) << a.id_bits) | stage_v[i];
+        } else {
+            const uint32_t v = stage_v[i];
+            if (kout) kout[pos] = k;
+            vout[pos] = v;
+            if (gather) a.gdst[pos] = a.gsrc[v];
+        }
+    }
+    if constexpr (MODE == RXM_UNPACK) {
+        // identifyTileRanges from the counts: tile (d, s) = digit d's items of
+        // segment s, which start at segment s's first block.  After the digit scan
+        // hist[d][b] = digit d's items before block b, so tile (d, s) covers
+        // dstart[d] + [hist[d][sfb[s]], hist[d][sfb[s + 1]]) (totals[d] past the
+        // last block).  One digit per workgroup; empty tiles get (0, 0).
+        const int nseg = 1 << a.seg_bits;
+        for (uint32_t d = blockIdx.x; d < (1u << a.nbits); d += gridDim.x) {
+            if ((int)threadIdx.x < nseg) {
+                const uint32_t sg = threadIdx.x, fb = sfb[sg], fe = sfb[sg + 1];
+                const uint32_t *row = a.hist + (size_t)d * a.NB;
+                const uint32_t x = fb < (uint32_t)a.NB ? row[fb] : a.totals[d];
+                const uint32_t y = fe < (uint32_t)a.NB ? row[fe] : a.totals[d];
+                const uint32_t tile = (d << a.seg_bits) | sg;
+                if (tile < (uint32_t)a.T) a.ranges[tile] = y > x ? make_uint2(dstart[d] + x, dstart[d] + y) : make_uint2(0u, 0u);
+            }
+        }
     }
 }
 
-template <int ITEMS>
+template <int ITEMS, int MODE = RXM_KV>
 static hipError_t radix_pass(const RadixPass &a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(radix_upsweep_kernel<ITEMS>, dim3(a.NB), dim3(RX_THREADS), 0, s, a);
+    hipLaunchKernelGGL((radix_upsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(RADIX), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(radix_downsweep_kernel<ITEMS>, dim3(a.NB), dim3(RX_THREADS), 0, s, a);
+    hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     return hipGetLastError();
 }
 
@@ -449,11 +534,14 @@ __global__ void __launch_bounds__(RANGE_THREADS) identify_ranges_kernel(const ui
 }
 
 // upstream's sorted 64-bit keys (binningState.point_list_keys of
-// rasterizer_impl.cu): (tile << 32) | depth bits of the entry's Gaussian
-__global__ void point_list_keys_kernel(const uint32_t *tile_keys, const uint32_t *point_list, const uint32_t *depths,
+// rasterizer_impl.cu): (tile << 32) | depth bits of the entry's Gaussian, one
+// workgroup per tile over its range (the packed tile sort keeps no sorted tile
+// array)
+__global__ void point_list_keys_kernel(const uint2 *ranges, const uint32_t *point_list, const uint32_t *depths,
                                        uint32_t n, uint64_t *keys) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) keys[i] = ((uint64_t)tile_keys[i] << 32) | depths[point_list[i]];
+    const uint2 r = ranges[blockIdx.x];
+    for (uint32_t i = r.x + threadIdx.x; i < min(r.y, n); i += blockDim.x)
+        keys[i] = ((uint64_t)blockIdx.x << 32) | depths[point_list[i]];
 }
 
 hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const void *binning, int64_t I,
@@ -461,8 +549,8 @@ hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const v
     if (I <= 0) return hipSuccess;
     const GeomLayout L = geom_layout(P, W, H);
     const BinningLayout B = binning_layout(I, W, H);
-    hipLaunchKernelGGL(point_list_keys_kernel, dim3((unsigned)((I + 255) / 256)), dim3(256), 0, s,
-                       at<const uint32_t>(binning, B.off[GSR_BIN_KEYS]),
+    hipLaunchKernelGGL(point_list_keys_kernel, dim3((unsigned)grid_dims(W, H).tiles), dim3(256), 0, s,
+                       at<const uint2>(geom, L.off[GSR_GEOM_RANGES]),
                        at<const uint32_t>(binning, B.off[GSR_BIN_POINT_LIST]),
                        at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTHS]), (uint32_t)I, keys);
     return hipGetLastError();
@@ -477,7 +565,7 @@ hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const v
 // then the rank-order block offsets of the emission.
 static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     const GeomLayout L = geom_layout(P, W, H);
-    RadixPass a;
+    RadixPass a = {};
     a.n = (uint32_t)P;
     a.NB = radix_blocks(P, dsort_items(P));
     a.hist = at<uint32_t>(geom, L.dsort_hist);
@@ -554,7 +642,8 @@ hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, vo
     a.rects = at<const uint4>(geom, L.rects_ranked);
     a.block_prefix = at<const uint32_t>(geom, L.emit_sums);
     // emit into the buffer pair that the tile passes will end in KEYS/POINT_LIST
-    const bool odd = tile_sort_passes(g.tiles) & 1;
+    // (the packed form: emit -> b, first pass -> KEYS, second -> POINT_LIST)
+    const bool odd = tile_sort_packed(g.tiles, P) || (tile_sort_passes(g.tiles) & 1);
     a.tile_keys = at<uint32_t>(binning, odd ? B.keys_b : B.off[GSR_BIN_KEYS]);
     a.ids = at<uint32_t>(binning, odd ? B.vals_b : B.off[GSR_BIN_POINT_LIST]);
     hipLaunchKernelGGL(emit_kernel, dim3(emit_blocks(P)), dim3(EMIT_BLOCK), 0, s, a);
@@ -568,20 +657,49 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
     const int npass = tile_sort_passes(g.tiles);
     uint32_t *keys[2] = {at<uint32_t>(binning, B.off[GSR_BIN_KEYS]), at<uint32_t>(binning, B.keys_b)};
     uint32_t *vals[2] = {at<uint32_t>(binning, B.off[GSR_BIN_POINT_LIST]), at<uint32_t>(binning, B.vals_b)};
-    int bits = 0;
-    while (bits < 32 && ((uint32_t)(g.tiles - 1) >> bits) != 0u) bits++;
+    const int bits = tile_bits(g.tiles);
     int cur = npass & 1;
-    RadixPass a;
+    RadixPass a = {};
     a.n = (uint32_t)I;
     const int items = tsort_items(I);
     a.NB = radix_blocks(I, items);
-    a.gsrc = nullptr;
-    a.gdst = nullptr;
-    a.ctrl = nullptr;
     a.role = RX_PLAIN;
-    a.vout_final = nullptr;
     a.hist = at<uint32_t>(binning, B.hist);
     a.totals = at<uint32_t>(binning, B.totals);
+    uint2 *ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
+    if (tile_sort_packed(g.tiles, P)) {
+        // pass 1: the low tile bits; (tile, id) in b -> packed words in KEYS
+        const int lo = bits / 2, hi = bits - lo;
+        a.kin = keys[1];
+        a.vin = vals[1];
+        a.kout = nullptr;
+        a.vout = keys[0];
+        a.shift = 0;
+        a.nbits = lo;
+        a.dmask = (1u << lo) - 1u;
+        a.pack_shift = lo;
+        a.id_bits = 32 - hi;
+        a.totals = at<uint32_t>(binning, B.totals1);
+        hipError_t e = items == TSORT_ITEMS_BIG ? radix_pass<TSORT_ITEMS_BIG, RXM_PACK>(a, s)
+                                                : radix_pass<TSORT_ITEMS, RXM_PACK>(a, s);
+        if (e != hipSuccess) return e;
+        // pass 2: the high tile bits of the packed words, segment-aligned blocks;
+        // ids -> POINT_LIST, ranges from the digit counts
+        a.kin = keys[0];
+        a.vin = nullptr;
+        a.vout = vals[0];
+        a.shift = 32 - hi;
+        a.nbits = hi;
+        a.dmask = (1u << hi) - 1u;
+        a.totals = at<uint32_t>(binning, B.totals);
+        a.seg_totals = at<const uint32_t>(binning, B.totals1);
+        a.seg_bits = lo;
+        a.NB = radix_blocks(I, items) + (1 << lo);
+        a.ranges = ranges;
+        a.T = g.tiles;
+        return items == TSORT_ITEMS_BIG ? radix_pass<TSORT_ITEMS_BIG, RXM_UNPACK>(a, s)
+                                        : radix_pass<TSORT_ITEMS, RXM_UNPACK>(a, s);
+    }
     for (int p = 0; p < npass; p++) {
         a.kin = keys[cur];
         a.vin = vals[cur];
@@ -597,7 +715,6 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
         if (e != hipSuccess) return e;
         cur ^= 1;
     }
-    uint2 *ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
     const int64_t per_block = 4 * RANGE_THREADS;
     hipLaunchKernelGGL(identify_ranges_kernel, dim3((unsigned)((I + per_block - 1) / per_block)), dim3(RANGE_THREADS),
                        0, s, (const uint32_t *)keys[0], (uint32_t)I, ranges);

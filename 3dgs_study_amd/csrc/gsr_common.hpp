@@ -67,10 +67,21 @@ __host__ __device__ inline int radix_blocks(int64_t n, int items) {
 }
 __host__ __device__ inline int emit_blocks(int P) { return (P + EMIT_BLOCK - 1) / EMIT_BLOCK; }
 // LSD passes of the tile sort: enough 8-bit digits to cover tile indices [0, T)
-__host__ __device__ inline int tile_sort_passes(int T) {
+__host__ __device__ inline int tile_bits(int T) {
     int bits = 0;
     while (bits < 32 && ((uint32_t)(T - 1) >> bits) != 0u) bits++;
-    return (bits + RADIX_BITS - 1) / RADIX_BITS;
+    return bits;
+}
+__host__ __device__ inline int tile_sort_passes(int T) { return (tile_bits(T) + RADIX_BITS - 1) / RADIX_BITS; }
+// The two-pass tile sort (9-16 tile bits: 1080p, 4K) packs its first pass's
+// output as (high tile digit << id bits) | Gaussian id, one word per instance,
+// when the ids fit beside the digit (P <= 2^(32 - high bits): 16.7M Gaussians
+// at 4K); the second pass then moves one word in and one out, and the tile
+// ranges come from its digit counts (binning.hip).
+__host__ __device__ inline bool tile_sort_packed(int T, int P) {
+    if (tile_sort_passes(T) != 2) return false;
+    const int bits = tile_bits(T), hi = bits - bits / 2;
+    return (uint64_t)P <= (1ull << (32 - hi));
 }
 __host__ __device__ inline int pre_blocks(int P) { return (P + PRE_THREADS - 1) / PRE_THREADS; }
 
@@ -132,8 +143,9 @@ struct BinningLayout {
     size_t off[GSR_BIN_NFIELDS];
     size_t keys_b;  // uint32 [I] tile-sort ping-pong
     size_t vals_b;  // uint32 [I]
-    size_t hist;    // uint32 [RADIX][radix_blocks(I, tsort_items(I))]
+    size_t hist;    // uint32 [RADIX][radix_blocks(I, tsort_items(I)) + RADIX] (+ RADIX: segment-aligned blocks)
     size_t totals;  // uint32 [RADIX]
+    size_t totals1; // uint32 [RADIX] the first tile pass's digit totals (the second pass's segments)
     size_t bytes;
 };
 __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H) {
@@ -145,8 +157,9 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H)
     L.off[GSR_BIN_POINT_LIST] = take(n * 4);
     L.keys_b = take(n * 4);
     L.vals_b = take(n * 4);
-    L.hist = take((size_t)RADIX * radix_blocks((int64_t)n, tsort_items((int64_t)n)) * 4);
+    L.hist = take((size_t)RADIX * (radix_blocks((int64_t)n, tsort_items((int64_t)n)) + RADIX) * 4);
     L.totals = take((size_t)RADIX * 4);
+    L.totals1 = take((size_t)RADIX * 4);
     L.bytes = o;
     return L;
 }

@@ -391,7 +391,8 @@ def point_list_keys(P, W, H, geomBuffer, binningBuffer, num_rendered):
     """upstream's sorted 64-bit keys (tile << 32 | depth bits) of a forward's lists,
     as an int64 tensor holding the uint64 bit patterns (gsr_point_list_keys)."""
     lib = load_library()
-    keys = torch.empty((max(int(num_rendered), 0),), dtype=torch.int64, device=geomBuffer.device)
+    # all ones where no tile range covers an entry (never, for a consistent binning)
+    keys = torch.full((max(int(num_rendered), 0),), -1, dtype=torch.int64, device=geomBuffer.device)
     if keys.numel():
         _check(lib.gsr_point_list_keys(int(P), int(W), int(H), geomBuffer.data_ptr(), binningBuffer.data_ptr(),
                                        int(num_rendered), keys.data_ptr(), _stream(geomBuffer.device)),

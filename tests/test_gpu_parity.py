@@ -111,9 +111,10 @@ def check_binning_tight(h, r, W, H):
     np.testing.assert_array_equal(tt_h[big], tt_r[big])
     assert h["num_rendered"] == int(tt_h.sum()) <= r["num_rendered"]
     I = h["num_rendered"]
-    keys_h = h["keys"][:I].astype(np.int64)
+    # the tile of each entry, from the ranges (gsr_point_list_keys): all ones if a
+    # position is in no range
+    keys_h = (h["keys64"] >> np.uint64(32)).astype(np.int64)
     keys_r = (r["keys"] >> 32).astype(np.int64)
-    np.testing.assert_array_equal(h["keys64"] >> np.uint64(32), keys_h.astype(np.uint64))
     pair_h = keys_h * P + h["point_list"][:I]
     pair_r = keys_r * P + r["point_list"]
     keep = np.isin(pair_r, pair_h)
@@ -284,6 +285,24 @@ def test_long_tiles(dev, oracle, footprint):
     r = run_oracle(oracle, cam, g)
     lens = r["ranges"][:, 1] - r["ranges"][:, 0]
     assert lens.max() > 8192
+    check_forward(h, r)
+
+
+@pytest.mark.parametrize("P,W,H", [
+    (40, 333, 201),      # 273 tiles, 9 bits: packed two-pass sort, most segments (low digits) empty
+    (2_000, 1000, 600),  # 2,394 tiles, 12 bits
+    (3_000, 4000, 2200), # 34,500 tiles, 16 bits: 8 + 8, ids in 24 bits
+    (1_000, 4112, 4100), # 66,049 tiles, 17 bits: three passes, ranges from the sorted keys
+])
+def test_tile_sort_widths(dev, oracle, P, W, H):
+    """The tile sort at every pass layout: one pass (<= 8 tile bits: configs A, the small
+    cases above), the packed two-pass form (segment-aligned second pass, ranges from its
+    digit counts) from 9 to 16 bits, and three plain passes above 16 bits; keys,
+    point_list and ranges equal upstream's (rect footprint)."""
+    cam, g = case(P, W, H, 0, seed=11, view=0)
+    h = run_hip(cam, g, dev, footprint="rect")
+    r = run_oracle(oracle, cam, g)
+    assert h["num_rendered"] > 0
     check_forward(h, r)
 
 
