@@ -100,12 +100,12 @@ enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
 
 // First depth pass: key = depth bits - base, clamped to 24 bits in three-pass
 // mode (only invisible Gaussians, +inf keys, reach the clamp).
-__device__ __forceinline__ uint32_t load_key(const RadixPass &a, uint32_t idx) {
-    const uint32_t k = a.kin[idx];
+__device__ __forceinline__ uint32_t key_of(const RadixPass &a, uint32_t k) {
     if (a.role != RX_DEPTH_FIRST) return k;
     const uint32_t d = k - a.ctrl[CTRL_KEY_BASE];
     return a.ctrl[CTRL_DSORT_PASSES] == 3 ? min(d, 0xffffffu) : d;
 }
+__device__ __forceinline__ uint32_t load_key(const RadixPass &a, uint32_t idx) { return key_of(a, a.kin[idx]); }
 __device__ __forceinline__ bool pass_skipped(const RadixPass &a) {
     return a.role == RX_DEPTH_FOURTH && a.ctrl[CTRL_DSORT_PASSES] == 3;
 }
@@ -160,27 +160,40 @@ __device__ __forceinline__ uint2 block_span(const RadixPass &a, uint32_t blk, ui
 // rank chains), more for long ones (fewer blocks in the digit scan).
 template <int ITEMS, int MODE>
 __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) {
-    constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
+    constexpr int TILE_N = RX_THREADS * ITEMS;
     constexpr int SEG = MODE == RXM_UNPACK ? RADIX + 1 : 1;
     __shared__ uint32_t h[RX_WAVES][RADIX];
     __shared__ uint32_t sfb[SEG], sst[SEG], wsum[RX_WAVES];
     if (pass_skipped(a)) return;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
     const uint32_t blk = radix_block(a.NB);
     const uint2 span = block_span<TILE_N, MODE>(a, blk, sfb, sst, wsum);
     __syncthreads();
-    const uint32_t base = span.x + w * (uint32_t)WAVE_N + lane;
-    uint32_t kk[ITEMS];
+    // order-free count: 16-B loads over the block's 16-B aligned body (ITEMS / 4
+    // per thread), single keys for its ragged head and tail (< 4 each)
+    static_assert(ITEMS % 4 == 0, "quads");
+    const uint32_t v0 = min((span.x + 3u) & ~3u, span.y), v1 = max(span.y & ~3u, v0);
+    const uint4 *k4 = reinterpret_cast<const uint4 *>(a.kin);
+    uint4 q[ITEMS / 4];
 #pragma unroll
-    for (int r = 0; r < ITEMS; r++) {
-        const uint32_t idx = base + 64u * r;
-        kk[r] = idx < span.y ? load_key(a, idx) : 0u;
+    for (int r = 0; r < ITEMS / 4; r++) {
+        const uint32_t qi = (v0 >> 2) + threadIdx.x + (uint32_t)(r * RX_THREADS);
+        q[r] = qi < (v1 >> 2) ? k4[qi] : make_uint4(0u, 0u, 0u, 0u);
     }
+    auto count = [&](uint32_t k) { atomicAdd(&h[w][(key_of(a, k) >> a.shift) & a.dmask], 1u); };
 #pragma unroll
-    for (int r = 0; r < ITEMS; r++)
-        if (base + 64u * r < span.y) atomicAdd(&h[w][(kk[r] >> a.shift) & a.dmask], 1u);  // order-free count
+    for (int r = 0; r < ITEMS / 4; r++) {
+        if ((v0 >> 2) + threadIdx.x + (uint32_t)(r * RX_THREADS) < (v1 >> 2)) {
+            count(q[r].x);
+            count(q[r].y);
+            count(q[r].z);
+            count(q[r].w);
+        }
+    }
+    if (threadIdx.x < v0 - span.x) count(a.kin[span.x + threadIdx.x]);
+    if (threadIdx.x < span.y - v1) count(a.kin[v1 + threadIdx.x]);
     __syncthreads();
     uint32_t c = 0;
 #pragma unroll
