@@ -205,17 +205,8 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
 __global__ void __launch_bounds__(256) radix_digit_scan_kernel(RadixPass a) {
     __shared__ uint32_t wsum[4];
     if (pass_skipped(a)) return;
-    uint32_t *row = a.hist + (size_t)blockIdx.x * a.NB;
-    uint32_t carry = 0;
-    for (int base = 0; base < a.NB; base += 256) {
-        const int i = base + threadIdx.x;
-        const uint32_t v = i < a.NB ? row[i] : 0u;
-        uint32_t tot;
-        const uint32_t inc = block_inclusive_scan<256>(v, wsum, &tot);
-        if (i < a.NB) row[i] = carry + inc - v;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) a.totals[blockIdx.x] = carry;
+    const uint32_t tot = block_exclusive_scan_inplace<256, 16>(a.hist + (size_t)blockIdx.x * a.NB, a.NB, wsum);
+    if (threadIdx.x == 0) a.totals[blockIdx.x] = tot;
 }
 
 template <int ITEMS, int MODE>
@@ -393,15 +384,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK)
 constexpr int TOPSCAN_THREADS = 1024;
 __global__ void __launch_bounds__(TOPSCAN_THREADS) exclusive_scan_one_block_kernel(uint32_t *v, int n) {
     __shared__ uint32_t wsum[TOPSCAN_THREADS / 64];
-    uint32_t carry = 0;
-    for (int base = 0; base < n; base += TOPSCAN_THREADS) {
-        const int i = base + threadIdx.x;
-        const uint32_t x = i < n ? v[i] : 0u;
-        uint32_t tot;
-        const uint32_t inc = block_inclusive_scan<TOPSCAN_THREADS>(x, wsum, &tot);
-        if (i < n) v[i] = carry + inc - x;
-        carry += tot;
-    }
+    block_exclusive_scan_inplace<TOPSCAN_THREADS, 8>(v, n, wsum);
 }
 
 // duplicateWithKeys in rank order: (tile, id) for every tile of the rect.
