@@ -95,28 +95,41 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *wsum) {
     return tot;
 }
 
-// Exclusive scan of v[0, n) in place by one workgroup; returns the total.  Each
-// thread takes PER consecutive entries per round (all its loads in flight at
-// once, one block scan per THREADS * PER entries): a block scan per THREADS
-// entries left the 256 digit scans of the config-E tile sort at ~30 us each.
+// Exclusive scan of v[0, n) in place by one workgroup; returns the total.  Per
+// round each wave takes 64 * PER consecutive entries with coalesced loads (all
+// in flight at once), scans them as PER wave scans chained by the running wave
+// total, and one exchange of the wave totals places the waves: a block scan
+// (two barriers) per THREADS entries left the 256 digit scans of the config-E
+// tile sort at ~28 us each.
 template <int THREADS, int PER>
 __device__ __forceinline__ uint32_t block_exclusive_scan_inplace(uint32_t *v, int n, uint32_t *wsum) {
+    constexpr int NW = THREADS / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t carry = 0;
     for (int base = 0; base < n; base += THREADS * PER) {
-        const int i0 = base + (int)threadIdx.x * PER;
-        uint32_t x[PER], s = 0;
+        const int wb = base + w * 64 * PER + lane;
+        uint32_t x[PER], ex[PER], run = 0;
+#pragma unroll
+        for (int j = 0; j < PER; j++) x[j] = wb + 64 * j < n ? v[wb + 64 * j] : 0u;
 #pragma unroll
         for (int j = 0; j < PER; j++) {
-            x[j] = i0 + j < n ? v[i0 + j] : 0u;
-            s += x[j];
+            const uint32_t s = wave_inclusive_scan(x[j]);
+            ex[j] = run + s - x[j];
+            run += (uint32_t)__builtin_amdgcn_readlane((int)s, 63);
         }
-        uint32_t tot;
-        uint32_t run = carry + block_inclusive_scan<THREADS>(s, wsum, &tot) - s;
+        if (lane == 0) wsum[w] = run;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
 #pragma unroll
-        for (int j = 0; j < PER; j++) {
-            if (i0 + j < n) v[i0 + j] = run;
-            run += x[j];
+        for (int k = 0; k < NW; k++) {
+            const uint32_t t = wsum[k];
+            pre += k < w ? t : 0u;
+            tot += t;
         }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; j++)
+            if (wb + 64 * j < n) v[wb + 64 * j] = carry + pre + ex[j];
         carry += tot;
     }
     return carry;
