@@ -47,25 +47,36 @@ for k, cs in sorted(vals.items()):
         print(f"    {c:28s} {x:>16,.1f}" if isinstance(x, float) else f"    {c:28s} {x}")
 # multi-kernel stages: HBM bytes of one stage launch = per-dispatch means times the
 # dispatches of each kernel per launch.  The radix kernels serve both sorts; their
-# ITEMS template argument tells them apart (gsr_common.hpp tsort_items/dsort_items:
-# tile sort <8> at config C, <16> at E; depth sort <4> at C, <8> at E).
-# radix_digit_scan_kernel is shared and tiny (256 x blocks counters): its mean is
+# template arguments tell them apart (gsr_common.hpp tsort_items/dsort_items: tile
+# sort <8, mode> at config C, <16, mode> at E; depth sort <4, 0> at C, <8, 0> at
+# E; mode 1 / 2 = the packed two-pass tile sort, 0 = plain key/value passes).
+# radix_digit_scan_kernel is shared and small (256 x blocks counters): its mean is
 # counted once per pass.
-def _mean_hbm(prefix):
-    for k, line in summary["kernels"].items():
-        if k.startswith(prefix) and "hbm_bytes_per_launch" in line:
-            return line["hbm_bytes_per_launch"]
+def tile_sort_stage(kernels, titems, suffix=""):
+    """One tile-sort launch: the packed two passes (binning.hip) when their
+    kernels were traced, else the plain passes + identify_ranges."""
+    def mean(prefix):
+        for k, line in kernels.items():
+            if k.startswith(prefix) and k.endswith(suffix) and (suffix or not k.endswith("_E")) \
+                    and "hbm_bytes_per_launch" in line:
+                return line["hbm_bytes_per_launch"]
+        return None
+    up, down = "gsr::radix_upsweep_kernel", "gsr::radix_downsweep_kernel"
+    packed = [(f"{up}<{titems}, 1>", 1), (f"{down}<{titems}, 1>", 1), (f"{up}<{titems}, 2>", 1),
+              (f"{down}<{titems}, 2>", 1), ("gsr::radix_digit_scan_kernel", 2)]
+    plain = [(f"{up}<{titems}, 0>", 2), (f"{down}<{titems}, 0>", 2), ("gsr::radix_digit_scan_kernel", 2),
+             ("gsr::identify_ranges_kernel", 1)]
+    for parts in (packed, plain):
+        got = [(mean(k), n) for k, n in parts]
+        if all(v is not None for v, _ in got):
+            return {"hbm_bytes_per_launch": sum(v * n for v, n in got),
+                    "kernel": " + ".join(f"{n} x {k}" for k, n in parts)}
     return None
 
 
-titems = "16" if SUFFIX == "_E" else "8"
-parts = [(f"gsr::radix_upsweep_kernel<{titems}>", 2), (f"gsr::radix_downsweep_kernel<{titems}>", 2),
-         ("gsr::radix_digit_scan_kernel", 2), ("gsr::identify_ranges_kernel", 1)]
-got = [(_mean_hbm(k), n) for k, n in parts]
-if all(v is not None for v, _ in got):
-    summary["stages"]["tile_sort" + SUFFIX] = {
-        "hbm_bytes_per_launch": sum(v * n for v, n in got),
-        "kernel": " + ".join(f"{n} x {k}" for k, n in parts)}
+rec = tile_sort_stage(summary["kernels"], "16" if SUFFIX == "_E" else "8")
+if rec:
+    summary["stages"]["tile_sort" + SUFFIX] = rec
 for st, rec in summary["stages"].items():
     frac = summary["kernels"].get(rec["kernel"], {}).get("valu_issue_frac")
     if frac is not None:
