@@ -306,6 +306,28 @@ def test_tile_sort_widths(dev, oracle, P, W, H):
     check_forward(h, r)
 
 
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("P", [1 << 24, (1 << 24) + 1])
+def test_tile_sort_id_width_boundary(dev, oracle, P):
+    """16 tile bits (8 + 8): ids below 2^24 fit beside the high digit (the packed
+    two-pass sort, P = 2^24); one Gaussian more and the sort takes the plain key /
+    value passes and identify_ranges (gsr_common.hpp tile_sort_packed).  20k
+    Gaussians spread over the whole index range, the last two included, face the
+    camera; the rest sit behind it."""
+    cam, g = case(P, 4000, 2200, 0, seed=12)
+    rng = np.random.default_rng(0)
+    vis = np.unique(np.concatenate([rng.choice(P, 20_000, replace=False), [P - 2, P - 1]]))
+    with torch.no_grad():
+        behind = torch.ones(P, dtype=torch.bool)
+        behind[torch.as_tensor(vis)] = False
+        g.xyz[behind] = g.xyz[behind] * 0.1 + torch.tensor([0.0, 0.0, -7.0])
+    h = run_hip(cam, g, dev, footprint="rect")
+    r = run_oracle(oracle, cam, g, mt=True)
+    assert h["num_rendered"] > 0 and int(h["point_list"].max()) >= (1 << 24) - 2
+    check_forward(h, r)
+
+
 def test_empty_and_culled(dev, oracle):
     from diff_gaussian_rasterization import _C
 
