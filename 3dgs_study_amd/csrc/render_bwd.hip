@@ -70,7 +70,7 @@ __device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
-__global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs a) {
+__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(6))) render_bwd_kernel(RenderBwdArgs a) {
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
     // workgroup 8 r + x: XCD x's r-th quadrant in bucket order (gsr_blend.hpp)
     const int lane = threadIdx.x & 63;
@@ -129,6 +129,10 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
     const bool act_a = slot_a >= 0, act_b = slot_b >= 0;
     // lanes 16-31 (and 48-63) keep Gaussian b's sums in the first exchange stage
     const bool h16 = (lane & 16) != 0;
+    // dL/dpix of the first exchange stage's partner pixel (lane ^ 16)
+    const float qdpx0 = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, dpx0), 0x401F));
+    const float qdpx1 = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, dpx1), 0x401F));
+    const float qdpx2 = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, dpx2), 0x401F));
 
     struct Pre {
         float dx, dy, G, alpha, power;
@@ -197,21 +201,25 @@ __global__ void __launch_bounds__(BLEND_THREADS) render_bwd_kernel(RenderBwdArgs
         const float ky = h16 ? pb.dy : pa.dy, sy = h16 ? pa.dy : pb.dy;
         const float k5 = h16 ? pb.g5 : pa.g5, s5 = h16 ? pa.g5 : pb.g5;
         const float kt = h16 ? pb.t : pa.t, st_ = h16 ? pa.t : pb.t;
-        const float k0 = kW * kx, s0 = sW * sx;
-        const float k1 = kW * ky, s1 = sW * sy;
-        auto x16 = [&](float keep, float send) {
-            return keep + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send),
-                                                                                0x1F | (16 << 10)));
+        // the partner (lane ^ 16) sends its five base quantities of the Gaussian
+        // this lane keeps, and this lane forms both pixels' nine products (five
+        // exchanges instead of nine, the partner's terms fused into FMAs)
+        auto x16 = [&](float send) {
+            return __builtin_bit_cast(float,
+                                      __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send), 0x1F | (16 << 10)));
         };
-        const float o0 = x16(k0, s0);
-        const float o1 = x16(k1, s1);
-        const float o2 = x16(k0 * kx, s0 * sx);
-        const float o3 = x16(k0 * ky, s0 * sy);
-        const float o4 = x16(k1 * ky, s1 * sy);
-        const float o5 = x16(k5, s5);
-        const float o6 = x16(kt * dpx0, st_ * dpx0);
-        const float o7 = x16(kt * dpx1, st_ * dpx1);
-        const float o8 = x16(kt * dpx2, st_ * dpx2);
+        const float rW = x16(sW), rx = x16(sx), ry = x16(sy), r5 = x16(s5), rt = x16(st_);
+        const float k0 = kW * kx, k1 = kW * ky;
+        const float r0 = rW * rx, r1 = rW * ry;
+        const float o0 = k0 + r0;
+        const float o1 = k1 + r1;
+        const float o2 = fmaf(k0, kx, r0 * rx);
+        const float o3 = fmaf(k0, ky, r0 * ry);
+        const float o4 = fmaf(k1, ky, r1 * ry);
+        const float o5 = k5 + r5;
+        const float o6 = fmaf(kt, dpx0, rt * qdpx0);
+        const float o7 = fmaf(kt, dpx1, rt * qdpx1);
+        const float o8 = fmaf(kt, dpx2, rt * qdpx2);
         const float t0 = swz_stage<8>(o0, o1, lane);
         const float t1 = swz_stage<8>(o2, o3, lane);
         const float t2 = swz_stage<8>(o4, o5, lane);
