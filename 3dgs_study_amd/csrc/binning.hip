@@ -17,11 +17,13 @@
 //  4. tile sort   — stable LSD radix sort of the I instances by tile index
 //                   (ceil(log2 T / 8) passes: 2 at 1080p and 4K).  Stability
 //                   keeps rank order inside a tile, i.e. (depth_bits, id).  In
-//                   the two-pass case the first pass writes one word per
-//                   instance, (high tile digit << id bits) | id, and the second
-//                   sorts those words by the high digit in blocks that never
-//                   straddle a low digit, writing only the ids: 28 B per
-//                   instance over both passes instead of 40 + 4.
+//                   the two-pass case emit already writes each instance as
+//                   one byte (its low tile digit) and one word, (high tile
+//                   digit << id bits) | id; the first pass sorts the words by
+//                   the byte, the second sorts them by the high digit in blocks
+//                   that never straddle a low digit, writing only the ids:
+//                   22 B per instance over emit and both passes, instead of
+//                   28 + 8 (a word each for tile and id from emit).
 //  5. ranges      — from the second pass's per-block digit counts (two-pass
 //                   case), else identifyTileRanges on the sorted tile keys.
 //
@@ -84,13 +86,13 @@ struct RadixPass {
     int role;              // RX_PLAIN, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH
     uint32_t *vout_final;  // RX_DEPTH_THIRD in three-pass mode: the order lands here
     // packed two-pass tile sort (tile_sort_packed): the first pass (RXM_PACK)
-    // writes vout = (key >> pack_shift) << id_bits | value; the second
+    // takes byte keys (kin as uint8: the low tile digit) and moves the packed
+    // words (high tile digit << id_bits | id) emit wrote as values; the second
     // (RXM_UNPACK) reads those words (digit = word >> shift, value = the id bits)
     // in blocks aligned to the first pass's digit runs (seg_totals: 2^seg_bits
     // segments, one low tile digit each) and fills the T tile ranges
     const uint32_t *seg_totals;
     int seg_bits;
-    int pack_shift;
     int id_bits;
     uint2 *ranges;
     int T;
@@ -171,6 +173,31 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
     const uint32_t blk = radix_block(a.NB);
     const uint2 span = block_span<TILE_N, MODE>(a, blk, sfb, sst, wsum);
     __syncthreads();
+    if constexpr (MODE == RXM_PACK) {
+        // byte keys: 16 per 16-B load over the block's 16-B aligned body, single
+        // bytes for its ragged tail (blocks start at multiples of TILE_N)
+        const uint8_t *k8 = reinterpret_cast<const uint8_t *>(a.kin);
+        const uint32_t v1 = span.y & ~15u;
+        const uint4 *k4 = reinterpret_cast<const uint4 *>(k8);
+        auto count4 = [&](uint32_t word) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) atomicAdd(&h[w][(word >> (8 * b)) & a.dmask], 1u);
+        };
+        for (uint32_t qi = (span.x >> 4) + threadIdx.x; qi < (v1 >> 4); qi += RX_THREADS) {
+            const uint4 q = k4[qi];
+            count4(q.x);
+            count4(q.y);
+            count4(q.z);
+            count4(q.w);
+        }
+        if (threadIdx.x < span.y - v1) atomicAdd(&h[w][k8[v1 + threadIdx.x] & a.dmask], 1u);
+        __syncthreads();
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < RX_WAVES; k++) c += h[k][threadIdx.x];
+        a.hist[(size_t)threadIdx.x * a.NB + blk] = c;
+        return;
+    }
     // order-free count: 16-B loads over the block's 16-B aligned body (ITEMS / 4
     // per thread), single keys for its ragged head and tail (< 4 each)
     static_assert(ITEMS % 4 == 0, "quads");
@@ -243,7 +270,10 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     for (int r = 0; r < ITEMS; r++) {
         const uint32_t idx = base + 64u * r;
         const bool ok = idx < span.y;
-        kk[r] = ok ? load_key(a, idx) : 0u;
+        if constexpr (MODE == RXM_PACK)
+            kk[r] = ok ? (uint32_t)reinterpret_cast<const uint8_t *>(a.kin)[idx] : 0u;
+        else
+            kk[r] = ok ? load_key(a, idx) : 0u;
         if constexpr (MODE != RXM_UNPACK) vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
     }
     {  // where this block's items of digit d go: all smaller digits + earlier blocks
@@ -309,7 +339,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         if constexpr (MODE == RXM_UNPACK) {
             vout[pos] = k & ((1u << a.id_bits) - 1u);
         } else if constexpr (MODE == RXM_PACK) {
-            vout[pos] = ((k >> a.pack_shift) << a.id_bits) | stage_v[i];
+            vout[pos] = stage_v[i];
         } else {
             const uint32_t v = stage_v[i];
             if (kout) kout[pos] = k;
@@ -406,6 +436,9 @@ __global__ void __launch_bounds__(TOPSCAN_THREADS) exclusive_scan_one_block_kern
 constexpr int EMIT_IPT = 4;
 struct EmitArgs {
     int P, gx;
+    // packed two-pass tile sort: tile_keys receives one byte per instance (the
+    // low lo_bits of its tile) and ids the word (tile >> lo_bits) << id_bits | id
+    int packed, lo_bits, id_bits;
     const uint32_t *order;
     const uint4 *rects;
     const uint32_t *block_prefix;
@@ -495,8 +528,14 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
         const uint32_t nr = min((uint32_t)(EMIT_BLOCK * EMIT_IPT), tot - r0);
         for (uint32_t i = threadIdx.x; i < nr; i += EMIT_BLOCK) {
             const uint32_t li = (i / EMIT_IPT) * RS + i % EMIT_IPT;
-            a.tile_keys[base + r0 + i] = kbuf[li];
-            a.ids[base + r0 + i] = ibuf[li];
+            if (a.packed) {
+                const uint32_t tile = kbuf[li];
+                reinterpret_cast<uint8_t *>(a.tile_keys)[base + r0 + i] = (uint8_t)(tile & ((1u << a.lo_bits) - 1u));
+                a.ids[base + r0 + i] = ((tile >> a.lo_bits) << a.id_bits) | ibuf[li];
+            } else {
+                a.tile_keys[base + r0 + i] = kbuf[li];
+                a.ids[base + r0 + i] = ibuf[li];
+            }
         }
         __syncthreads();
     }
@@ -645,7 +684,12 @@ hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, vo
     a.block_prefix = at<const uint32_t>(geom, L.emit_sums);
     // emit into the buffer pair that the tile passes will end in KEYS/POINT_LIST
     // (the packed form: emit -> b, first pass -> KEYS, second -> POINT_LIST)
-    const bool odd = tile_sort_packed(g.tiles, P) || (tile_sort_passes(g.tiles) & 1);
+    const bool packed = tile_sort_packed(g.tiles, P);
+    const bool odd = packed || (tile_sort_passes(g.tiles) & 1);
+    const int bits = tile_bits(g.tiles);
+    a.packed = packed ? 1 : 0;
+    a.lo_bits = bits / 2;
+    a.id_bits = 32 - (bits - bits / 2);
     a.tile_keys = at<uint32_t>(binning, odd ? B.keys_b : B.off[GSR_BIN_KEYS]);
     a.ids = at<uint32_t>(binning, odd ? B.vals_b : B.off[GSR_BIN_POINT_LIST]);
     hipLaunchKernelGGL(emit_kernel, dim3(emit_blocks(P)), dim3(EMIT_BLOCK), 0, s, a);
@@ -670,7 +714,8 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
     a.totals = at<uint32_t>(binning, B.totals);
     uint2 *ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
     if (tile_sort_packed(g.tiles, P)) {
-        // pass 1: the low tile bits; (tile, id) in b -> packed words in KEYS
+        // pass 1: the low tile digit (emit's bytes in b) moves the packed words
+        // (emit's words in b) to KEYS
         const int lo = bits / 2, hi = bits - lo;
         a.kin = keys[1];
         a.vin = vals[1];
@@ -679,7 +724,6 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
         a.shift = 0;
         a.nbits = lo;
         a.dmask = (1u << lo) - 1u;
-        a.pack_shift = lo;
         a.id_bits = 32 - hi;
         a.totals = at<uint32_t>(binning, B.totals1);
         hipError_t e = items == TSORT_ITEMS_BIG ? radix_pass<TSORT_ITEMS_BIG, RXM_PACK>(a, s)
