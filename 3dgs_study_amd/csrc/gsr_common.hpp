@@ -33,7 +33,10 @@ constexpr int RX_THREADS = 256;
 constexpr int DSORT_ITEMS = GSR_DSORT_ITEMS;
 // The depth sort of many Gaussians (config E: 5M) likewise takes 8 items per
 // thread: 285 -> 256 us at E; 1M (config C) is unchanged either way.
-constexpr int DSORT_ITEMS_BIG = 8;
+#ifndef GSR_DSORT_ITEMS_BIG
+#define GSR_DSORT_ITEMS_BIG 8
+#endif
+constexpr int DSORT_ITEMS_BIG = GSR_DSORT_ITEMS_BIG;
 constexpr int DSORT_BIG_N = 2 << 20;
 __host__ __device__ inline int dsort_items(int P) { return P > DSORT_BIG_N ? DSORT_ITEMS_BIG : DSORT_ITEMS; }
 constexpr int TSORT_ITEMS = GSR_TSORT_ITEMS;

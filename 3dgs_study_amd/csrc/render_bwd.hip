@@ -63,6 +63,17 @@ __device__ __forceinline__ float swz_stage(float c, float d, int lane) {
     return keep + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send), 0x1F | (K << 10)));
 }
 
+// The same step for an odd register out (c paired with a zero): every lane adds
+// its partner's copy, no selects.  Lanes with bit K clear get exactly
+// swz_stage<K>(c, 0)'s sum; lanes with bit K set get that sum too instead of 0,
+// and no slot lane reads those copies: every slot lane's value is bit for bit
+// what the zero-padded stage gives (tests/test_reduce_layout.py simulates the
+// whole exchange sequence).
+template <int K>
+__device__ __forceinline__ float swz_fold(float c) {
+    return c + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, c), 0x1F | (K << 10)));
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const volatile f32x4 lds_f32x4;
 __device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
@@ -224,12 +235,12 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         const float t1 = swz_stage<8>(o2, o3, lane);
         const float t2 = swz_stage<8>(o4, o5, lane);
         const float t3 = swz_stage<8>(o6, o7, lane);
-        const float t4 = swz_stage<8>(o8, 0.f, lane);
+        const float t4 = swz_fold<8>(o8);
         const float u0 = swz_stage<4>(t0, t1, lane);
         const float u1 = swz_stage<4>(t2, t3, lane);
-        const float u2 = swz_stage<4>(t4, 0.f, lane);
+        const float u2 = swz_fold<4>(t4);
         const float w0 = swz_stage<2>(u0, u1, lane);
-        const float w1 = swz_stage<2>(u2, 0.f, lane);
+        const float w1 = swz_fold<2>(u2);
         const float x0 = swz_stage<1>(w0, w1, lane);
         const float v = swap32_sum(x0, x0);  // both halves: the full sum
         // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
