@@ -50,8 +50,12 @@ constexpr int FWD_GROUP = GSR_FWD_GROUP;  // Gaussians per blend iteration
 // skip threshold are redone exactly from (u, v) (blend_fix).
 //   rec[k][0] = {K6, K4, K5, K1}, rec[k][1] = {K2, K3, opacity, r},
 //   rec[k][2] = {g, b, -, lane},  rec[k][3] = {u, v, -, -}
+// Record ns (after the survivors) is all zeros: opacity 0 blends nothing, so the
+// odd count's second Gaussian needs no mask (render_fwd 145 -> 142 us at C,
+// 374-379 -> 370 us at E, although the compiler then spills 4 VGPRs on the rare
+// exact re-check path).
 struct FwdChunk {
-    float4 rec[64][4];
+    float4 rec[65][4];
 };
 
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(8))) render_fwd_kernel(RenderFwdArgs a) {
@@ -69,7 +73,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
     uint32_t last = 0;
     uint32_t work = 0;  // wave-uniform: surviving Gaussians walked (~ the backward's replay work)
-    float live = inside ? 1.0f : 0.0f;  // 0 once the pixel has stopped (or lies outside the image)
+    // the pixel's skip threshold on alpha: upstream's 1/255 while it blends, 2
+    // (above any alpha) once it has stopped or when it lies outside the image
+    float thr = inside ? 1.0f / 255.0f : 2.0f;
     __shared__ FwdChunk stage[BLEND_WAVES];
     FwdChunk &st = stage[BLEND_WAVES == 1 ? 0 : w];
     if (__any(inside) && n > 0) {
@@ -92,6 +98,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 st.rec[slot][3] = make_float4(u, v, 0.0f, 0.0f);
             }
             const int ns = __builtin_popcountll(mask);
+            if (lane < 3) st.rec[ns][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             work += ns;
             // FWD_GROUP Gaussians per iteration: their LDS reads, powers and exps are
             // independent, so each wave has that much instruction-level parallelism
@@ -103,7 +110,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 bool near = false;
 #pragma unroll
                 for (int g = 0; g < FWD_GROUP; g++) {
-                    const int kg = min(k + g, ns - 1);
+                    const int kg = k + g;  // ns itself: the zero record
                     const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r2 = st.rec[kg][2];
                     li[g] = __float_as_int(r2.w);
                     const float t1 = fmaf(r1.x, ly, fmaf(r0.w, lx, r0.y)), t2 = fmaf(r1.y, ly, r0.z);
@@ -118,7 +125,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 if (__builtin_expect(__ballot(near) != 0, 0)) {  // rare: exact skip decisions (gsr_blend.hpp)
 #pragma unroll
                     for (int g = 0; g < FWD_GROUP; g++) {
-                        const int kg = min(k + g, ns - 1);
+                        const int kg = k + g;
                         const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r3 = st.rec[kg][3];
                         // d = mean - pixel = (u - x, v - y), exact like upstream's subtraction
                         if (blend_near(pw[g], op[g] * G[g]))
@@ -131,19 +138,18 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 // (selects on VGPRs only: the per-Gaussian SALU work of bool masks
                 // and exec juggling, one scalar unit per CU, bounded this loop).
                 // a = the alpha this pixel takes: 0 when upstream would skip the
-                // Gaussian (power > 0, alpha < 1/255, pixel finished) — a zero alpha
-                // leaves T and C unchanged.  T >= 1e-4 holds for every live pixel, so
-                // the stop test can only fire for a > 0, exactly upstream's test.
+                // Gaussian (power > 0, alpha < 1/255, pixel finished: thr = 2) — a
+                // zero alpha leaves T and C unchanged.  T >= 1e-4 holds for every
+                // live pixel, so the stop test can only fire for a > 0, exactly
+                // upstream's test.
 #pragma unroll
                 for (int g = 0; g < FWD_GROUP; g++) {
-                    const bool use = g == 0 || k + g < ns;  // wave-uniform
                     float av = pw[g] > 0.0f ? 0.0f : al[g];
-                    av = al[g] < 1.0f / 255.0f ? 0.0f : av;
-                    av = use ? av * live : 0.0f;
+                    av = al[g] < thr ? 0.0f : av;
                     const float test_T = T * (1 - av);
                     const bool sat = test_T < 0.0001f;  // this Gaussian is not blended; the pixel stops
                     av = sat ? 0.0f : av;
-                    live = sat ? 0.0f : live;
+                    thr = sat ? 2.0f : thr;
                     const float wgt = av * T;
                     C0 += cr[g] * wgt;
                     C1 += cg[g] * wgt;
@@ -151,7 +157,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                     T = sat ? T : test_T;
                     last = av > 0.0f ? (uint32_t)(pos + li[g] + 1) : last;
                 }
-                if (!__any(live > 0.0f)) return true;
+                if (!__any(thr < 1.0f)) return true;
             }
             return false;
         };
