@@ -52,13 +52,13 @@ constexpr int FWD_GROUP = GSR_FWD_GROUP;  // Gaussians per blend iteration
 //   rec[k][2] = {g, b, -, lane},  rec[k][3] = {u, v, -, -}
 // Record ns (after the survivors) is all zeros: opacity 0 blends nothing, so the
 // odd count's second Gaussian needs no mask (render_fwd 145 -> 142 us at C,
-// 374-379 -> 370 us at E, although the compiler then spills 4 VGPRs on the rare
-// exact re-check path).
+// 374-379 -> 370 us at E).  It takes 66 VGPRs: 7 waves per SIMD (forced to 8,
+// the compiler spilled 4 VGPRs to scratch, 1-2 us slower and +20 % traffic).
 struct FwdChunk {
     float4 rec[65][4];
 };
 
-__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(8))) render_fwd_kernel(RenderFwdArgs a) {
+__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(7))) render_fwd_kernel(RenderFwdArgs a) {
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
     if (tile < 0) return;
