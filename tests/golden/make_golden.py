@@ -18,6 +18,8 @@ Captured:
                    rasterizer kwargs render() produces for both input branches
   render_tiny.npz  the same capture with its tensor values (tiny scene) for replay on GPU
   loss.npz         utils/loss_utils.py:17-108         l1_loss / ssim on small images
+  ply.npz          scene/gaussian_model.py:218-318    save_ply's structured vertex array (names,
+                   formats, bytes) and the parameters load_ply rebuilds, SH degrees 0/1/3
 """
 from __future__ import annotations
 
@@ -50,7 +52,7 @@ class _CpuDevice:
 
     def __enter__(self):
         self._orig = {}
-        for name in ("zeros", "zeros_like", "empty", "ones"):
+        for name in ("zeros", "zeros_like", "empty", "ones", "tensor"):
             fn = getattr(torch, name)
             self._orig[name] = fn
 
@@ -218,6 +220,103 @@ def capture_boundary():
     np.savez_compressed(OUT / "render_tiny.npz", **arrays)
 
 
+def capture_ply():
+    """Run the reference's GaussianModel.save_ply / load_ply (scene/gaussian_model.py:
+    218-318) with a recording stand-in for the absent ``plyfile`` package: ``PlyElement.
+    describe`` captures the structured vertex array and element name save_ply builds,
+    ``PlyData.read`` serves load_ply a captured array (also with its properties in a
+    shuffled order, which load_ply's name sorts must undo).  Records the parameters
+    going in, the array's field names and bytes, and the parameters load_ply rebuilt."""
+    captured = {}
+
+    class _Element:
+        def __init__(self, data, name):
+            self.data, self.name = data, name
+            self.properties = [types.SimpleNamespace(name=n) for n in data.dtype.names]
+
+        def __getitem__(self, key):
+            return self.data[key]
+
+    class PlyElement:
+        @staticmethod
+        def describe(data, name):
+            captured["element"] = (np.array(data, copy=True), name)
+            return _Element(data, name)
+
+    class PlyData:
+        to_read = None
+
+        def __init__(self, elements):
+            self.elements = elements
+
+        def write(self, path):
+            captured["written_to"] = path
+
+        @classmethod
+        def read(cls, path):
+            return cls([_Element(cls.to_read, "vertex")])
+
+    plyfile = types.ModuleType("plyfile")
+    plyfile.PlyData, plyfile.PlyElement = PlyData, PlyElement
+    knn_pkg, knn_c = types.ModuleType("simple_knn"), types.ModuleType("simple_knn._C")
+    knn_c.distCUDA2 = None  # create_from_pcd only; not called here
+    utils_pkg = types.ModuleType("utils")
+    names = ("plyfile", "simple_knn", "simple_knn._C", "utils", "utils.general_utils", "utils.system_utils",
+             "utils.sh_utils", "utils.graphics_utils")
+    saved = {k: sys.modules.get(k) for k in names}
+    sys.modules.update({"plyfile": plyfile, "simple_knn": knn_pkg, "simple_knn._C": knn_c, "utils": utils_pkg})
+    for sub in ("general_utils", "system_utils", "sh_utils", "graphics_utils"):
+        setattr(utils_pkg, sub, _load(f"utils.{sub}", REF / "utils" / f"{sub}.py"))
+    gm = _load("ref_gaussian_model", REF / "scene" / "gaussian_model.py")
+
+    sys.path.insert(0, str(REPO / "3dgs_study_amd"))
+    import synthetic
+
+    out = {}
+    tmp = OUT / "_ply_tmp"
+    for deg in (0, 1, 3):
+        g = synthetic.make_gaussians(53, deg, seed=40 + deg)
+        model = gm.GaussianModel(deg)
+        model._xyz = torch.nn.Parameter(g.xyz.clone())
+        model._features_dc = torch.nn.Parameter(g.features_dc.clone())
+        model._features_rest = torch.nn.Parameter(g.features_rest.clone())
+        model._opacity = torch.nn.Parameter(g.opacity.clone())
+        model._scaling = torch.nn.Parameter(g.scaling.clone())
+        model._rotation = torch.nn.Parameter(g.rotation.clone())
+        captured.clear()
+        model.save_ply(str(tmp / "point_cloud.ply"))
+        rec, el_name = captured["element"]
+        assert el_name == "vertex"
+        key = f"d{deg}_"
+        for n in ("xyz", "features_dc", "features_rest", "opacity", "scaling", "rotation"):
+            out[key + "in_" + n] = getattr(g, n).numpy()
+        out[key + "names"] = np.array(rec.dtype.names)
+        out[key + "formats"] = np.array([rec.dtype.fields[n][0].str for n in rec.dtype.names])
+        out[key + "body"] = np.frombuffer(rec.tobytes(), dtype=np.uint8)
+        # load_ply on the captured array, and on the same columns in a shuffled order
+        perm = np.random.default_rng(deg).permutation(len(rec.dtype.names))
+        shuffled = np.empty(rec.shape[0], dtype=[(rec.dtype.names[i], "f4") for i in perm])
+        for n in rec.dtype.names:
+            shuffled[n] = rec[n]
+        out[key + "shuffled_names"] = np.array(shuffled.dtype.names)
+        for tag, arr in (("load_", rec), ("load_shuffled_", shuffled)):
+            PlyData.to_read = arr
+            back = gm.GaussianModel(deg)
+            with _CpuDevice():
+                back.load_ply(str(tmp / "point_cloud.ply"))
+            assert back.active_sh_degree == deg
+            for n in ("xyz", "features_dc", "features_rest", "opacity", "scaling", "rotation"):
+                out[key + tag + n] = getattr(back, "_" + n).detach().numpy()
+    if tmp.exists():
+        tmp.rmdir()
+    for k, v in saved.items():
+        if v is None:
+            sys.modules.pop(k, None)
+        else:
+            sys.modules[k] = v
+    np.savez_compressed(OUT / "ply.npz", **out)
+
+
 def capture_loss():
     lu = _load("ref_loss_utils", REF / "utils" / "loss_utils.py")
     g = torch.Generator().manual_seed(11)
@@ -236,5 +335,6 @@ if __name__ == "__main__":
     capture_cameras()
     capture_boundary()
     capture_loss()
+    capture_ply()
     for p in sorted(OUT.glob("*.npz")) + sorted(OUT.glob("*.json")):
         print(p.name, p.stat().st_size)

@@ -2,10 +2,12 @@
 scene/dataset_readers.py:156-185) and distCUDA2 (mean squared distance to the 3
 nearest neighbours, scene/gaussian_model.py:153-155).
 
-PLY: CPU tests (byte layout of the header plyfile writes, bit-exact round trips,
-ascii / big-endian / uchar reading).  No .ply file ships in the reference, so the
-byte layout is pinned by the header plyfile emits for the reference's dtype list
-(``PlyElement.describe`` of 'f4' fields -> "property float <name>").
+PLY: CPU tests pinned to the reference's own save_ply / load_ply, run in the build
+container under a recording ``plyfile`` stand-in (tests/golden/ply.npz, made by
+tests/golden/make_golden.py:capture_ply): the vertex array's names, formats and
+bytes, and the parameters load_ply rebuilds (also from a shuffled property order).
+Plus bit-exact round trips and ascii / big-endian / uchar reading.  The header text
+itself is plyfile's (absent here): "property float <name>" for an 'f4' field.
 kNN: the C ABI's argument checks on CPU; exactness against scipy's cKDTree on GPU
 (simple-knn itself is an absent submodule: its published contract is the exact
 mean of the three smallest squared distances to other points)."""
@@ -52,6 +54,68 @@ def test_save_load_round_trip_is_bit_exact(tmp_path, degree):
     for a, b in zip(g.params(), h.params()):
         assert a.shape == b.shape
         assert torch.equal(a, b)
+
+
+_PARAMS = ("xyz", "features_dc", "features_rest", "opacity", "scaling", "rotation")
+
+
+def _golden_ply():
+    from pathlib import Path
+
+    return np.load(Path(__file__).parent / "golden" / "ply.npz")
+
+
+def _golden_model(z, key):
+    deg = int(key[1])
+    t = {n: torch.from_numpy(z[key + "in_" + n]) for n in _PARAMS}
+    return synthetic.SynthGaussians(t["xyz"], t["features_dc"], t["features_rest"], t["scaling"], t["rotation"],
+                                    t["opacity"], deg, deg)
+
+
+@pytest.mark.parametrize("degree", [0, 1, 3])
+def test_save_ply_equals_reference_save_ply(tmp_path, degree):
+    """The body save_ply writes is, byte for byte, the structured array the reference's
+    own save_ply (scene/gaussian_model.py:240-258) hands PlyElement.describe, with the
+    same property names, order and formats (tests/golden/make_golden.py:capture_ply)."""
+    z, key = _golden_ply(), f"d{degree}_"
+    path = str(tmp_path / "point_cloud.ply")
+    ply_io.save_ply(path, _golden_model(z, key))
+    head, body = open(path, "rb").read().split(b"end_header\n", 1)
+    props = [ln.split() for ln in head.decode().split("\n")[3:-1]]
+    assert [p[2] for p in props] == list(z[key + "names"])
+    # plyfile names an f4 field "float"
+    assert all(p[1] == "float" for p in props) and set(z[key + "formats"]) == {"<f4"}
+    assert body == z[key + "body"].tobytes()
+
+
+@pytest.mark.parametrize("degree", [0, 1, 3])
+@pytest.mark.parametrize("order", ["canonical", "shuffled"])
+def test_load_ply_equals_reference_load_ply(tmp_path, degree, order):
+    """load_ply rebuilds the parameters the reference's own load_ply (scene/
+    gaussian_model.py:267-318) rebuilt from the same vertex data, bit for bit — also
+    from a file whose properties come in a shuffled order (its numeric-suffix sorts)."""
+    z, key = _golden_ply(), f"d{degree}_"
+    names = list(z[key + "names"])
+    rec = np.frombuffer(z[key + "body"].tobytes(), dtype=[(n, "<f4") for n in names])
+    if order == "shuffled":
+        names = list(z[key + "shuffled_names"])
+    hdr = ["ply", "format binary_little_endian 1.0", f"element vertex {rec.shape[0]}"]
+    hdr += [f"property float {n}" for n in names]
+    body = np.empty(rec.shape[0], dtype=[(n, "<f4") for n in names])
+    for n in names:
+        body[n] = rec[n]
+    path = tmp_path / "m.ply"
+    _write(path, hdr, body.tobytes())
+    h = ply_io.load_ply(str(path), degree)
+    tag = "load_" if order == "canonical" else "load_shuffled_"
+    for n in _PARAMS:
+        want = z[key + tag + n]
+        got = getattr(h, n).numpy()
+        assert got.shape == want.shape and got.dtype == want.dtype, n
+        np.testing.assert_array_equal(got, want, err_msg=n)
+    # and the reference's round trip is the identity on the parameters it saved
+    for n in _PARAMS:
+        np.testing.assert_array_equal(z[key + tag + n], z[key + "in_" + n], err_msg=n)
 
 
 def test_load_rejects_wrong_sh_degree(tmp_path):
