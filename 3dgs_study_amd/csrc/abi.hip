@@ -216,7 +216,7 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
                          const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
                          float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
                          float *drgb, float *dscales, float *drot, void *stream, int dsh_planar = 0,
-                         int phases = 3) {
+                         int phases = 3, const gsr_leaf_grads *leaf = nullptr) {
     // phases: bit 0 = accumulator memset + render_bwd (+ the colour gradient into
     // drgb), bit 1 = preprocess_bwd.  The view-parallel exchange runs them as two
     // calls and starts its all-gather of drgb in between.
@@ -224,10 +224,18 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     if (in->P == 0) return GSR_OK;
     if (!radii || !geom || !img || !accum || !dL_dout_color || (num_rendered > 0 && !binning))
         return fail(GSR_ERR_ARGS, "backward scratch/inputs are NULL");
-    if (!dmeans2D || !dcolors || !dopacity || !dmeans3D || !dcov3D)
+    const gsr_leaf_grads L = leaf ? *leaf : gsr_leaf_grads{};
+    if (L.dsh_dc && (!in->sh || in->M <= 0 || (in->M > 1 && !L.dsh_rest)))
+        return fail(GSR_ERR_ARGS, "leaf dsh: needs sh and dsh_rest (M > 1)");
+    if ((L.dscaling || L.drotation) && !in->scales) return fail(GSR_ERR_ARGS, "leaf dscaling/drotation: needs scales");
+    if (L.drotation && (!L.rotation_norm || !in->rotations))
+        return fail(GSR_ERR_ARGS, "leaf drotation: needs rotations and rotation_norm");
+    if (L.dopacity && !in->opacities) return fail(GSR_ERR_ARGS, "leaf dopacity: needs opacities");
+    if (!dmeans2D || !dcolors || (!dopacity && !L.dopacity) || !dmeans3D || !dcov3D)
         return fail(GSR_ERR_ARGS, "backward outputs are NULL");
-    if (in->sh && in->M > 0 && !dsh && !drgb) return fail(GSR_ERR_ARGS, "dsh is NULL");
-    if (in->scales && (!dscales || !drot)) return fail(GSR_ERR_ARGS, "dscales/drot are NULL");
+    if (in->sh && in->M > 0 && !dsh && !drgb && !L.dsh_dc) return fail(GSR_ERR_ARGS, "dsh is NULL");
+    if (in->scales && ((!dscales && !L.dscaling) || (!drot && !L.drotation)))
+        return fail(GSR_ERR_ARGS, "dscales/drot are NULL");
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
     float *acc = (float *)accum;
@@ -251,7 +259,12 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     // with the colour gradient taken by the exchange, preprocess_bwd still reads the
     // SH rows for dL/dmean3D's view-direction term but writes no dsh
     BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, colors ? nullptr : dsh, dscales, drot, nullptr,
-                 dsh_planar, colors ? 1 : 0};
+                 dsh_planar, colors ? 1 : 0, L};
+    if (colors) o.leaf.dsh_dc = o.leaf.dsh_rest = nullptr;  // the exchange owns the SH gradient
+    if (L.dsh_dc) o.dsh = nullptr;
+    if (L.dscaling) o.dscales = nullptr;
+    if (L.drotation) o.drot = nullptr;
+    if (L.dopacity) o.dopacity = nullptr;
     return step(timed(GSR_STAGE_PREPROCESS_BWD, s, [&] { return launch_preprocess_bwd(*in, radii, geom, acc, o, s); }), "preprocess backward", dbg, s);
 }
 
@@ -261,6 +274,14 @@ int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, c
                  void *stream) {
     return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
                          dopacity, dmeans3D, dcov3D, dsh, nullptr, dscales, drot, stream);
+}
+
+int gsr_backward_leaves(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                        const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
+                        float *dscales, float *drot, const gsr_leaf_grads *leaf, void *stream) {
+    return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
+                         dopacity, dmeans3D, dcov3D, dsh, nullptr, dscales, drot, stream, leaf ? leaf->dsh_planar : 0, 3, leaf);
 }
 
 int gsr_backward_planar(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,

@@ -4,10 +4,9 @@
 // pixel (l & 7, l >> 3)).  A wave streams the tile's depth-sorted list in
 // chunks of 64 entries, one entry per lane: the lane gathers the entry's 48-B
 // splat record, tests in parallel whether the Gaussian can reach ANY pixel of
-// the quadrant, and a ballot turns the chunk into a bit mask.  The wave then
-// walks only the set bits; each Gaussian's parameters are broadcast from the
-// owning lane with v_readlane into SGPRs, so the per-pixel math reads scalar
-// operands and no LDS or workgroup barrier is involved.
+// the quadrant, and a ballot turns the chunk into a bit mask.  The survivors'
+// records go to a per-wave LDS image (QuadChunk) in list order, and the wave
+// walks them with uniform-address LDS reads (broadcast): no workgroup barrier.
 #pragma once
 
 #include "gsr_common.hpp"
@@ -63,10 +62,10 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
 
 // power and G = exp(power) of one (pixel, Gaussian), for upstream's
 // `power > 0` skip and alpha = min(0.99, opacity * expf(power)) with its
-// `alpha < 1/255` skip.  The blend loops evaluate power as d^T conic' d
-// (conic' = -conic/2, contracted) and exp in hardware (v_exp_f32 of
-// power * log2 e): both within a few ulp of upstream's float expression and
-// the correctly rounded expf.  Where that could move a skip decision — alpha
+// `alpha < 1/255` skip.  The blend loops evaluate power as the quadrant-relative
+// quadratic of the staged record (quad_power, the same instructions in both
+// kernels) and exp in hardware (v_exp_f32 of power * log2 e): both within a few
+// ulp of upstream's float expression and the correctly rounded expf.  Where that could move a skip decision — alpha
 // within 2^-12 relative of 1/255 (the combined error is below 2^-16), or a
 // positive power (the conic is positive definite, so only rounding makes one)
 // — the pair is redone exactly as the CPU restatement does it (blend_fix):
@@ -78,8 +77,16 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
 // Gaussian cost render_fwd 20 % and render_bwd 7 % (exec-mask juggling that
 // broke the two Gaussians' interleaving); this form costs 15 % / 6 % (config C:
 // 132 -> 152 us, 247 -> 261 us; of that the positive-power test is 8 / 3 us and
-// the double-precision call ~0 / 3 us).  The forward and backward share the
-// decisions bit for bit.
+// the double-precision call ~0 / 3 us).  Both kernels flag from the same fast
+// power and G, so they re-check the same pairs and share every decision bit for
+// bit (a pair that only one of them re-checked could be skipped by one and
+// blended by the other, corrupting the backward's replay of that pixel).  The
+// positive-power test needs no band: upstream's float expression
+// -0.5 (a dx^2 + c dy^2) - b dx dy has the sign of the exact form (<= 0) unless
+// the conic's condition number exceeds ~2^21 (absolute rounding <= 4 ulp of
+// a dx^2 + c dy^2, the form >= that times 1/(2 kappa)) — a 2-D covariance
+// eigenvalue above ~6e5 px^2 given the 0.3 px^2 low-pass — so short of such a
+// conic a fast power <= 0 never hides an upstream skip.
 __device__ __forceinline__ bool blend_near(float power, float opacity_times_G) {
     return power > 0.0f || fabsf(opacity_times_G * 255.0f - 1.0f) < 0x1p-12f;
 }
@@ -122,35 +129,45 @@ __device__ __forceinline__ void blend_fix(float &power, float &G, float dx, floa
 // that the compiler's waitcnt pass sees it and marks the older loads as landed.
 __device__ __forceinline__ void wait_vmcnt_4() { __builtin_amdgcn_s_waitcnt(0x0F74); }
 
-// Per-wave LDS image of the current chunk: entry k's 48-B splat record at
-// byte 48k (lane-contiguous b128 stores are conflict-free at this stride).  The
-// per-Gaussian loop reads the record back with uniform-address ds_reads
-// (broadcast) — LDS-pipe work instead of nine or ten VALU v_readlanes.
-struct ChunkStage {
-    float4 rec[65][3];  // render_bwd.hip keeps its survivors in 1..64 (0 = a zero record)
+// Per-wave LDS image of a chunk's surviving Gaussians, shared by the forward and
+// the backward (so both evaluate the power with the same instructions on the same
+// values: their fast skip decisions, and with them their exact re-checks, agree bit
+// for bit).  Each record carries the power as a quadratic in the pixel's offset
+// (x, y) in 0..7 from the quadrant's first pixel:
+//   p(x, y) = K6 + K4 x + K5 y + K1 x^2 + K2 x y + K3 y^2
+// (conic' = -conic/2, centre offset (u, v) = mean - quadrant origin: K1 = c'a,
+// K2 = 2 c'b, K3 = c'c, K4 = -2 (c'a u + c'b v), K5 = -2 (c'b u + c'c v),
+// K6 = p(0, 0)) — five FMAs per pixel instead of the eight of d^T conic' d — and
+// the mean itself, for the exact re-check (d = mean - pixel, one rounding, as
+// upstream) and the backward's d.
+//   rec[k][0] = {K6, K4, K5, K1}, rec[k][1] = {K2, K3, opacity, r},
+//   rec[k][2] = {g, b, id bits, lane},  rec[k][3] = {mean.x, mean.y, -, -}
+// A zero record (opacity 0: alpha 0, never blended) pads an odd survivor count.
+struct QuadChunk {
+    float4 rec[66][4];  // render_fwd: survivors 0..ns-1, zero at ns; render_bwd: zero at 0, survivors 1..ns
 };
-__device__ __forceinline__ void stage_chunk(ChunkStage &st, int lane, const float4 &A, const float4 &B,
-                                            const float4 &C) {
-    st.rec[lane][0] = A;
-    st.rec[lane][1] = B;
-    st.rec[lane][2] = C;
+__device__ __forceinline__ void stage_quad(float4 *rec, const float4 &A, const float4 &B, const float4 &C, float qx0,
+                                           float qy0, int lane) {
+    const float u = A.x - qx0, v = A.y - qy0;  // exact for means near the quadrant
+    const float ca = A.z, cb = A.w, cc = B.x;
+    const float hu = fmaf(ca, u, cb * v), hv = fmaf(cb, u, cc * v);
+    rec[0] = make_float4(fmaf(u, hu, v * hv), -2.0f * hu, -2.0f * hv, ca);
+    rec[1] = make_float4(2.0f * cb, cc, B.y, B.z);
+    rec[2] = make_float4(B.w, C.x, C.y, __int_as_float(lane));
+    rec[3] = make_float4(A.x, A.y, 0.0f, 0.0f);
 }
-
-// Compacted chunk image: only the entries that survived the cull, in chunk
-// order (slot = first + number of survivors in lower lanes), each record's last word
-// holding the entry's lane (its list position minus the chunk start).  The
-// Gaussian loops then walk slots 0..n-1 with an affine index — no find-first-set
-// chains on the scalar unit between one pair's LDS reads and the next's.
-__device__ __forceinline__ int stage_survivors(ChunkStage &st, int lane, bool rel, uint64_t mask, const float4 &A,
-                                               const float4 &B, const float4 &C, int first = 0) {
-    if (rel) {
-        const int slot = first + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        st.rec[slot][0] = A;
-        st.rec[slot][1] = B;
-        st.rec[slot][2] = make_float4(C.x, C.y, C.z, __int_as_float(lane));
-    }
-    return __builtin_popcountll(mask);
+__device__ __forceinline__ void stage_zero(float4 *rec, int lane) {
+    if (lane < 4) rec[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// the fast power of record (r0, r1) at quadrant offset (lx, ly): render_fwd and
+// render_bwd use exactly this sequence
+__device__ __forceinline__ float quad_power(const float4 &r0, const float4 &r1, float lx, float ly) {
+    const float t1 = fmaf(r1.x, ly, fmaf(r0.w, lx, r0.y)), t2 = fmaf(r1.y, ly, r0.z);
+    return fmaf(t2, ly, fmaf(t1, lx, r0.x));
+}
+// compacted slot of a surviving lane: first + survivors in lower lanes
+__device__ __forceinline__ int survivor_slot(uint64_t mask, int first) {
+    return first + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
 __device__ __forceinline__ float bcast(float v, int k) {

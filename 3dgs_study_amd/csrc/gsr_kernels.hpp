@@ -35,6 +35,7 @@ struct BwdOutputs {
     float *drgb;  // instead of dsh: the clamp-masked colour gradient [P,3] (view-parallel exchange)
     int dsh_planar;  // dsh laid out [M][P][3] (coefficient planes) instead of [P][M][3]
     int sh_dir;      // read the SH rows for dL/dmean3D's direction term although dsh and drgb are NULL
+    gsr_leaf_grads leaf;  // leaf gradients of the caller's activations (NULL outputs: not requested)
 };
 hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, const void *geom, const float *accum,
                                  const BwdOutputs &o, hipStream_t s);

@@ -96,6 +96,24 @@ __device__ inline void lds_to_rows(const float *lds, int g0, int n, int RW_, flo
 }
 
 
+// Columns [c0, c0 + w) of LDS rows (stride S) -> global rows [g0, g0 + n) of width
+// w, overwritten or (add) added to what is there (AccumulateGrad's grad += new):
+// the SH cat's two leaves, dsh_dc (w = 3) and dsh_rest (w = 3M - 3).
+template <int THREADS>
+__device__ inline void lds_cols_to_rows(const float *lds, int S, int c0, int w, int g0, int n,
+                                        float *__restrict__ dst, bool add) {
+    const int total = n * w;
+    const float invw = 1.0f / (float)w;
+    float *base = dst + (size_t)g0 * w;
+    for (int e = threadIdx.x; e < total; e += THREADS) {
+        int r = (int)((float)e * invw);
+        r += ((r + 1) * w <= e) ? 1 : 0;
+        r -= (r * w > e) ? 1 : 0;
+        const float v = lds[r * S + c0 + (e - r * w)];
+        base[e] = add ? base[e] + v : v;
+    }
+}
+
 // The reverse into M coefficient planes: LDS rows (stride RW + 1, RW = 3M) of
 // Gaussians [g0, g0 + n) -> plane k = dst + k * plane_stride, floats
 // [3 g0, 3 (g0 + n)) of each, i.e. dL/dsh laid out [M][P][3] (the tensor

@@ -20,6 +20,7 @@ struct PreBwdArgs {
     float focal_x, focal_y;
     const int32_t *radii;
     const uint8_t *clamped;
+    const float *splat_f;  // the forward's splat records as floats (opacity at 12 i + 5), when in.opacities is NULL
     const float *accum;
     BwdOutputs o;
 };
@@ -89,6 +90,58 @@ __device__ __forceinline__ void sh_backward(const float *sh, float *dsh, int deg
 
 constexpr int PB_THREADS = 256;
 
+// dL/dSH of a degree-3 row (48 floats in registers) into the two leaves of the
+// caller's SH cat (gsr_leaf_grads): floats 0-2 to dsh_dc [P,1,3], floats 3-47 to
+// dsh_rest [P,15,3].  The 180-B rest rows pass through a per-wave LDS image of 32
+// rows at a time and leave as coalesced 16-B stores over the wave's contiguous
+// slice (per-lane stores at a 180-B stride ran 2x slower in sh_exchange.hip).
+// Every thread of the workgroup calls it (barriers).
+__device__ __forceinline__ void leaf_sh_store_direct(const gsr_leaf_grads &L, int P, int idx, bool live,
+                                                     const float rowv[48]) {
+    __shared__ __attribute__((aligned(16))) float stage[PB_THREADS / 64][32 * 45];
+    const bool add = (L.accumulate & 1) != 0;
+    if (live)
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            float *p = L.dsh_dc + 3 * (size_t)idx + c;
+            *p = add ? *p + rowv[c] : rowv[c];
+        }
+    const int lane = threadIdx.x & 63;
+    float *buf = stage[threadIdx.x >> 6];
+    const size_t wave_g0 = (size_t)blockIdx.x * PB_THREADS + (threadIdx.x & ~63u);
+    const size_t limit = (size_t)45 * P;  // floats in dsh_rest
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        if ((lane >> 5) == h)
+#pragma unroll
+            for (int j = 0; j < 45; j++) buf[(lane & 31) * 45 + j] = rowv[3 + j];
+        __syncthreads();
+        const size_t f0 = (wave_g0 + 32 * h) * 45;  // the half's first float in dsh_rest
+#pragma unroll
+        for (int m = 0; m < 6; m++) {
+            const int i = lane + 64 * m;  // float4 of the half's 32 x 45 floats
+            if (i < 360) {
+                const size_t f = f0 + 4 * (size_t)i;
+                const float4 v = *reinterpret_cast<const float4 *>(buf + 4 * i);
+                if (f + 4 <= limit) {
+                    float4 *d = reinterpret_cast<float4 *>(L.dsh_rest + f);
+                    if (add) {
+                        const float4 o = *d;
+                        *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+                    } else {
+                        *d = v;
+                    }
+                } else {
+                    const float vv[4] = {v.x, v.y, v.z, v.w};
+                    for (int c = 0; c < 4; c++)
+                        if (f + c < limit) L.dsh_rest[f + c] = add ? L.dsh_rest[f + c] + vv[c] : vv[c];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // What the SH stage (after the rows reach LDS) needs from the geometry stage.
 struct ShStage {
     f3 dmean;      // dL/dmean3D so far
@@ -96,8 +149,8 @@ struct ShStage {
     bool vis;
 };
 __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 mean, const float gin[7],
-                                       const float4 acc0, const float4 acc1, float accb, int32_t rad, uint32_t cl,
-                                       const Mat4 &V, const Mat4 &Pm);
+                                       const float4 acc0, const float4 acc1, float accb, float opac, int32_t rad,
+                                       uint32_t cl, const Mat4 &V, const Mat4 &Pm);
 
 // One workgroup = PB_THREADS consecutive Gaussians.  Each thread loads its own
 // inputs first and, at SH degree 3, its own 192-B SH row after them (12 x 16 B
@@ -115,7 +168,9 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
     // the rows are needed for dL/dmean3D's view-direction term even when the
     // exchange takes the colour gradient instead of dsh
-    const bool stage = in.sh != nullptr && (a.o.dsh != nullptr || a.o.drgb != nullptr || a.o.sh_dir) && in.M > 0;
+    const bool stage = in.sh != nullptr &&
+                       (a.o.dsh != nullptr || a.o.drgb != nullptr || a.o.sh_dir || a.o.leaf.dsh_dc != nullptr) &&
+                       in.M > 0;
     constexpr bool DIRECT = RWC == 48;  // each thread's own row in registers, no LDS
     const int idx = g0 + (int)threadIdx.x;
     const bool live = idx < in.P;
@@ -139,6 +194,9 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const float4 acc0 = *reinterpret_cast<const float4 *>(acc);      // mean2D.x, mean2D.y, conic.x, conic.y
     const float4 acc1 = *reinterpret_cast<const float4 *>(acc + 4);  // conic.w, opacity, color r, color g
     const float accb = acc[8];                                       // color b
+    // the sums' per-Gaussian opacity factor: the caller's opacities (coalesced), else
+    // the forward's splat record (4 B out of every 48)
+    const float opac = in.opacities ? in.opacities[li] : a.splat_f[12 * (size_t)li + 5];
     const int32_t rad = a.radii[li];
     const uint32_t cl = a.clamped[li];
     float rowv[DIRECT ? 48 : 1];
@@ -158,9 +216,9 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     // pin the per-Gaussian loads ahead of the rows (the compiler would otherwise
     // sink them into the branch below, behind the rows, and wait for all of them)
     asm volatile("" ::"v"(acc0.x), "v"(acc0.y), "v"(acc0.z), "v"(acc0.w), "v"(acc1.x), "v"(acc1.y), "v"(acc1.z),
-                 "v"(acc1.w), "v"(accb), "v"(rad), "v"(cl));
+                 "v"(acc1.w), "v"(accb), "v"(opac), "v"(rad), "v"(cl));
     ShStage st{};
-    if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, rad, cl, V, Pm);
+    if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, opac, rad, cl, V, Pm);
     if (stage && !DIRECT) __syncthreads();
     if (live) {
         f3 dmean = st.dmean;
@@ -191,6 +249,7 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
                     d4[b] = make_float4(rowv[4 * b], rowv[4 * b + 1], rowv[4 * b + 2], rowv[4 * b + 3]);
             }
         }
+        if (a.o.leaf.dsh_dc) leaf_sh_store_direct(a.o.leaf, in.P, idx, live, rowv);
         return;
     }
     if (stage && a.o.dsh) {
@@ -200,13 +259,84 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
         else
             lds_to_rows<PB_THREADS, RWC>(sh_lds, g0, n, RW, a.o.dsh);
     }
+    if (stage && a.o.leaf.dsh_dc) {  // the two leaves of the caller's SH cat
+        __syncthreads();
+        const bool add = (a.o.leaf.accumulate & 1) != 0;
+        lds_cols_to_rows<PB_THREADS>(sh_lds, RW + 1, 0, 3, g0, n, a.o.leaf.dsh_dc, add);
+        if (RW > 3) lds_cols_to_rows<PB_THREADS>(sh_lds, RW + 1, 3, RW - 3, g0, n, a.o.leaf.dsh_rest, add);
+    }
+}
+
+// F.normalize's backward as torch's autograd runs it for q = x / clamp_min(||x||,
+// eps).expand_as(x) (DivBackward0, ExpandBackward0's sum, ClampMinBackward0,
+// LinalgVectorNormBackward0 for ord 2, and the sum of the two paths into x),
+// operation for operation: g = dL/dq, n_raw = ||x|| as torch computed it.  Every
+// x / n and x / n_raw torch forms is the quotient q it already produced (the same
+// division of the same operands; n = n_raw wherever the norm term is not masked),
+// so the leaf x itself is not read.  File-wide fp contraction is off, as in
+// torch's kernels.
+__device__ __forceinline__ void normalize_backward(const float g[4], const float q[4], float n_raw, float eps,
+                                                   float dx[4]) {
+    const float n = n_raw != n_raw ? n_raw : fmaxf(n_raw, eps);  // clamp_min keeps a NaN
+    float og[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) og[k] = -g[k] * (q[k] / n);  // -grad * ((self / other) / other)
+    const float s = (og[0] + og[1]) + (og[2] + og[3]);  // sum_to_size over the expanded dim (torch's GPU
+                                                        // reduction pairs the 4 terms; measured bit for bit)
+    const float gm = n_raw >= eps ? s : 0.0f;                        // where(self >= min, grad, 0)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float xn = n_raw == 0.0f ? 0.0f : q[k];  // (self / norm).masked_fill_(norm == 0, 0)
+        dx[k] = g[k] / n + gm * xn;
+    }
+}
+
+// The activation gradients of one Gaussian (zeros for a culled one) go either to
+// upstream's outputs or, where the caller asked for them (gsr_leaf_grads), through
+// the activation's backward into its leaf's gradient.
+__device__ __forceinline__ void write_activation_grads(const PreBwdArgs &a, int idx, float dop, float opac,
+                                                       const float ds[3], const float dq[4], const float gin[7],
+                                                       bool has_sr) {
+    const BwdOutputs &o = a.o;
+    const gsr_leaf_grads &L = o.leaf;
+    auto put = [&](float *p, size_t i, float v, int bit) { p[i] = (L.accumulate & bit) ? p[i] + v : v; };
+    if (L.dopacity) {
+        const float sg = opac;  // = in.opacities[idx] (required with the leaf dopacity)
+        put(L.dopacity, idx, (dop * (1.0f - sg)) * sg, 4);  // sigmoid_backward: grad * (1 - y) * y
+    } else if (o.dopacity) {
+        o.dopacity[idx] = dop;
+    }
+    if (!has_sr) {  // precomputed cov3D: upstream's zero-initialised dscales / drot
+        if (o.dscales)
+            for (int k = 0; k < 3; k++) o.dscales[3 * (size_t)idx + k] = 0.f;
+        if (o.drot)
+            for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = 0.f;
+        return;
+    }
+    if (L.dscaling) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) put(L.dscaling, 3 * (size_t)idx + k, ds[k] * gin[k], 2);  // exp: grad * result
+    } else if (o.dscales) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) o.dscales[3 * (size_t)idx + k] = ds[k];
+    }
+    if (L.drotation) {
+        float dx[4];
+        normalize_backward(dq, gin + 3, L.rotation_norm[idx], L.rotation_eps, dx);  // gin[3..6] = q
+#pragma unroll
+        for (int k = 0; k < 4; k++) put(L.drotation, 4 * (size_t)idx + k, dx[k], 8);
+    } else if (o.drot) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = dq[k];
+    }
 }
 
 __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 mean, const float gin[7],
-                                       const float4 acc0, const float4 acc1, float accb, int32_t rad, uint32_t cl,
-                                       const Mat4 &V, const Mat4 &Pm) {
+                                       const float4 acc0, const float4 acc1, float accb, float opac, int32_t rad,
+                                       uint32_t cl, const Mat4 &V, const Mat4 &Pm) {
     const gsr_inputs &in = a.in;
     const BwdOutputs &o = a.o;
+    const bool has_sr = in.scales != nullptr;
     ShStage st{};
     st.vis = rad > 0;
     if (!st.vis) {
@@ -214,21 +344,18 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
             o.dmeans2D[3 * (size_t)idx + k] = 0.f;
             o.dcolors[3 * (size_t)idx + k] = 0.f;
             o.dmeans3D[3 * (size_t)idx + k] = 0.f;
-            if (o.dscales) o.dscales[3 * (size_t)idx + k] = 0.f;
         }
-        o.dopacity[idx] = 0.f;
         if (o.drgb)
             for (int k = 0; k < 3; k++) o.drgb[3 * (size_t)idx + k] = 0.f;
         for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = 0.f;
-        if (o.drot)
-            for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = 0.f;
+        const float zs[3] = {0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
+        write_activation_grads(a, idx, 0.f, opac, zs, zq, gin, has_sr);
         return st;  // dmeans3D (zero) and the dsh row are written by the caller
     }
     const float dcol[3] = {acc1.z, acc1.w, accb};
     o.dcolors[3 * (size_t)idx + 0] = dcol[0];
     o.dcolors[3 * (size_t)idx + 1] = dcol[1];
     o.dcolors[3 * (size_t)idx + 2] = dcol[2];
-    o.dopacity[idx] = acc1.y;
 
     // ---- 3D covariance (recomputed exactly as the forward did)
     float c3[6];
@@ -260,15 +387,18 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
     const float ca = cov2D.m[0][0] += 0.3f;
     const float cb = cov2D.m[0][1];
     const float cc = cov2D.m[1][1] += 0.3f;
-    const float gx = -0.5f * acc0.z, gy = -0.5f * acc0.w, gz = -0.5f * acc1.x;  // dL/dconic x, y, w
+    // render_bwd.hip accumulates sum g5 (dx, dy) and sum g5 (dx^2, dx dy, dy^2) with
+    // g5 = G dL/dalpha per pixel; the per-Gaussian factors — the opacity (W =
+    // opacity g5), -conic/2 (the forward's conic, preprocess.hip) and (W, H) of
+    // dL/dmean2D — are applied here
+    const float sx = opac * acc0.x, sy = opac * acc0.y;
+    const float gx = -0.5f * (opac * acc0.z), gy = -0.5f * (opac * acc0.w);  // dL/dconic x, y
+    const float gz = -0.5f * (opac * acc1.x);                                // dL/dconic w
     const float denom = ca * cc - cb * cb;
-    // render_bwd.hip accumulates sum W (dx, dy) and sum W (dx^2, dx dy, dy^2); the
-    // per-Gaussian factors -conic/2 (the forward's conic, preprocess.hip) and
-    // (W, H) of dL/dmean2D are applied here
     const float det_inv = 1.f / denom;
     const float kx = cc * det_inv, ky = -cb * det_inv, kz = ca * det_inv;
-    const float g2x = -0.5f * (kx * acc0.x + ky * acc0.y) * (float)in.W;
-    const float g2y = -0.5f * (ky * acc0.x + kz * acc0.y) * (float)in.H;
+    const float g2x = -0.5f * (kx * sx + ky * sy) * (float)in.W;
+    const float g2y = -0.5f * (ky * sx + kz * sy) * (float)in.H;
     o.dmeans2D[3 * (size_t)idx + 0] = g2x;
     o.dmeans2D[3 * (size_t)idx + 1] = g2y;
     o.dmeans2D[3 * (size_t)idx + 2] = 0.f;
@@ -339,7 +469,8 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
     st.dmean = dmean;
 
     // ---- computeCov3D backward: dSigma -> dM = 2 M dSigma -> dscale, drot (q as given)
-    if (in.scales && o.dscales && o.drot) {
+    float ds[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
+    if (has_sr) {
         const float qr = q[0], qx = q[1], qy = q[2], qz = q[3];
         const M3 R = quat_to_rot(qr, qx, qy, qz);
         M3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
@@ -358,25 +489,20 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
         const M3 Rt = m3_transpose(R);
         M3 dMt = m3_transpose(dM);
         for (int k = 0; k < 3; k++)
-            o.dscales[3 * (size_t)idx + k] =
-                (Rt.m[k][0] * dMt.m[k][0] + Rt.m[k][1] * dMt.m[k][1]) + Rt.m[k][2] * dMt.m[k][2];
+            ds[k] = (Rt.m[k][0] * dMt.m[k][0] + Rt.m[k][1] * dMt.m[k][1]) + Rt.m[k][2] * dMt.m[k][2];
         for (int k = 0; k < 3; k++)
             for (int j = 0; j < 3; j++) dMt.m[k][j] *= sm[k];
 #define D(i, j) dMt.m[i][j]
-        o.drot[4 * (size_t)idx + 0] = 2 * qz * (D(0, 1) - D(1, 0)) + 2 * qy * (D(2, 0) - D(0, 2)) + 2 * qx * (D(1, 2) - D(2, 1));
-        o.drot[4 * (size_t)idx + 1] = 2 * qy * (D(1, 0) + D(0, 1)) + 2 * qz * (D(2, 0) + D(0, 2)) +
-                                      2 * qr * (D(1, 2) - D(2, 1)) - 4 * qx * (D(2, 2) + D(1, 1));
-        o.drot[4 * (size_t)idx + 2] = 2 * qx * (D(1, 0) + D(0, 1)) + 2 * qr * (D(2, 0) - D(0, 2)) +
-                                      2 * qz * (D(1, 2) + D(2, 1)) - 4 * qy * (D(2, 2) + D(0, 0));
-        o.drot[4 * (size_t)idx + 3] = 2 * qr * (D(0, 1) - D(1, 0)) + 2 * qx * (D(2, 0) + D(0, 2)) +
-                                      2 * qy * (D(1, 2) + D(2, 1)) - 4 * qz * (D(1, 1) + D(0, 0));
+        dq[0] = 2 * qz * (D(0, 1) - D(1, 0)) + 2 * qy * (D(2, 0) - D(0, 2)) + 2 * qx * (D(1, 2) - D(2, 1));
+        dq[1] = 2 * qy * (D(1, 0) + D(0, 1)) + 2 * qz * (D(2, 0) + D(0, 2)) + 2 * qr * (D(1, 2) - D(2, 1)) -
+                4 * qx * (D(2, 2) + D(1, 1));
+        dq[2] = 2 * qx * (D(1, 0) + D(0, 1)) + 2 * qr * (D(2, 0) - D(0, 2)) + 2 * qz * (D(1, 2) + D(2, 1)) -
+                4 * qy * (D(2, 2) + D(0, 0));
+        dq[3] = 2 * qr * (D(0, 1) - D(1, 0)) + 2 * qx * (D(2, 0) + D(0, 2)) + 2 * qy * (D(1, 2) + D(2, 1)) -
+                4 * qz * (D(1, 1) + D(0, 0));
 #undef D
-    } else {
-        if (o.dscales)
-            for (int k = 0; k < 3; k++) o.dscales[3 * (size_t)idx + k] = 0.f;
-        if (o.drot)
-            for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = 0.f;
     }
+    write_activation_grads(a, idx, acc1.y, opac, ds, dq, gin, has_sr);
     return st;
 }
 
@@ -389,11 +515,13 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     a.focal_x = in.W / (2.0f * in.tan_fovx);
     a.radii = radii;
     a.clamped = at<uint8_t>(geom, G.off[GSR_GEOM_CLAMPED]);
+    a.splat_f = at<float>(geom, G.off[GSR_GEOM_SPLATS]);
     a.accum = accum;
     a.o = o;
-    const bool stage = in.sh && (o.dsh || o.drgb || o.sh_dir) && in.M > 0;
+    const bool stage = in.sh && (o.dsh || o.drgb || o.sh_dir || o.leaf.dsh_dc) && in.M > 0;
     const bool direct = stage && 3 * in.M == 48 && ((uintptr_t)in.sh & 15u) == 0 &&
-                        (!a.o.dsh || a.o.dsh_planar || ((uintptr_t)a.o.dsh & 15u) == 0);
+                        (!a.o.dsh || a.o.dsh_planar || ((uintptr_t)a.o.dsh & 15u) == 0) &&
+                        (!o.leaf.dsh_dc || ((uintptr_t)o.leaf.dsh_rest & 15u) == 0);
     const size_t lds = stage && !direct ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     const dim3 grid((in.P + PB_THREADS - 1) / PB_THREADS);
     switch (3 * in.M) {  // see launch_preprocess

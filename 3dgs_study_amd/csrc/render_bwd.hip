@@ -80,6 +80,11 @@ __device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
     const f32x4 v = *p;
     return make_float4(v.x, v.y, v.z, v.w);
 }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 ld2(const volatile char *p) {  // the record's mean: 8 of its last 16 B
+    const f32x2 v = *(__attribute__((address_space(3))) const volatile f32x2 *)p;
+    return make_float2(v.x, v.y);
+}
 
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(6))) render_bwd_kernel(RenderBwdArgs a) {
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
@@ -93,6 +98,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float fx = (float)px, fy = (float)py;
+    const float lx = (float)(lane & 7), ly = (float)(lane >> 3);  // offset in the quadrant (quad_power)
     const uint2 r = a.ranges[tile];
 
     const size_t HW = (size_t)a.W * a.H;
@@ -112,13 +118,16 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     for (int o = 32; o >= 1; o >>= 1) end = max(end, __shfl_xor(end, o));
     if (end <= 0) return;
 
-    __shared__ ChunkStage stage[BLEND_WAVES];
-    ChunkStage &st = stage[BLEND_WAVES == 1 ? 0 : w];
-    // record 0: the dummy b of an odd survivor count — zeros replay as a skipped
-    // Gaussian (alpha 0, finite colour), and its atomic is never issued
-    if (lane < 3) st.rec[0][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __shared__ QuadChunk stage[BLEND_WAVES];
+    QuadChunk &st = stage[0];
+    // record 0: the dummy b of an odd survivor count — a zero record replays as a
+    // skipped Gaussian (alpha 0, finite colour), and its atomic is never issued
+    stage_zero(st.rec[0], lane);
     float T = T_final;
-    float R0 = 0.f, R1 = 0.f, R2 = 0.f;
+    // upstream's accum_rec enters dL/dalpha only as sum_c (c_c - accum_rec_c) dL/dpix_c,
+    // so the replay carries its projection D = sum_c accum_rec_c dL/dpix_c (advanced
+    // eagerly: after a blended Gaussian it already holds the next Gaussian's value)
+    float D = 0.f;
     const uint32_t *list = a.point_list + r.x;
 
     // The role-swapped reduce-scatter below leaves Gaussian a's nine sums in lanes
@@ -126,7 +135,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // of ONE register (and again 32 lanes up), so each Gaussian costs one atomic
     // wave-instruction: nine lanes into one 64-B accumulator row = one memory-side
     // atomic request.  (Derived by simulating the exchange stages; tests/
-    // test_gpu_parity.py checks every gradient.)
+    // test_reduce_layout.py and the gradient parity tests check it.)
     int slot_a = -1, slot_b = -1;
     {
         constexpr int8_t LA[9] = {0, 8, 4, 12, 2, 10, 6, 14, 1};
@@ -140,97 +149,77 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     const bool act_a = slot_a >= 0, act_b = slot_b >= 0;
     // lanes 16-31 (and 48-63) keep Gaussian b's sums in the first exchange stage
     const bool h16 = (lane & 16) != 0;
-    // dL/dpix of the first exchange stage's partner pixel (lane ^ 16)
-    const float qdpx0 = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, dpx0), 0x401F));
-    const float qdpx1 = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, dpx1), 0x401F));
-    const float qdpx2 = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, dpx2), 0x401F));
 
-    struct Pre {
-        float dx, dy, G, alpha, power;
-        bool valid;
-    };
-    // power and G as render_fwd.hip computes them, bit for bit (same expression,
-    // same exact re-check near the skip thresholds, done by finish_pair)
-    auto prepare = [&](float4 p0, float4 p1) {
-        Pre q;
-        q.dx = p0.x - fx;
-        q.dy = p0.y - fy;
-        const float ux = p0.z * q.dx + p0.w * q.dy;  // conic' * d with conic' = -conic/2 (splat record)
-        const float uy = p0.w * q.dx + p1.x * q.dy;
-        q.power = q.dx * ux + q.dy * uy;
-        q.G = __expf(q.power);
-        return q;
-    };
-    // valid needs lo + k < last_contributor, power <= 0 and alpha >= 1/255
-    auto finish = [&](Pre &q, float4 p1, int k, int lim, bool live) {
-        q.alpha = fminf(0.99f, p1.y * q.G);
-        q.valid = live && k < lim && !(q.power > 0.0f) && !(q.alpha < 1.0f / 255.0f);
-    };
-    // The per-pixel quantities the nine sums of one Gaussian are made of.
+    // The per-pixel quantities the nine sums of one Gaussian are made of: g5 =
+    // G dL/dalpha, d = mean - pixel, t = alpha T.  The opacity factor of
+    // W = opacity g5 is per Gaussian: preprocess_bwd.hip applies it to the sums.
     struct Part {
-        float W, dx, dy, g5, t;
+        float g5, dx, dy, t;
     };
-    // Branch-free replay step: a skipped pixel sees alpha = 0 (T and the running
-    // colour R unchanged) and zero gradients.  R is upstream's accum_rec advanced
-    // eagerly: after a blended Gaussian it already holds
-    // last_alpha * last_color + (1 - last_alpha) * accum_rec.
-    auto replay = [&](const Pre &q, float op, float cr, float cg, float cb) {
-        const float av = q.valid ? q.alpha : 0.0f;
+    // One Gaussian of the replay (record r0..r3, list position k): power and G as
+    // render_fwd.hip computes them (quad_power, the same instructions on the same
+    // staged values, and the same exact re-check near the skip thresholds, done by
+    // the caller), then upstream's back-to-front step, branch-free: a skipped pixel
+    // sees alpha = 0 (T and D unchanged) and zero gradients.
+    auto replay = [&](float pw, float G, const float4 &r1, const float4 &r2, const float2 &r3, int lim) {
+        const float op = r1.z;
+        const float alpha = fminf(0.99f, op * G);
+        const int k = __float_as_int(r2.w);  // entry lo + k = upstream `contributor`
+        const bool valid = k < lim && !(pw > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const float av = valid ? alpha : 0.0f;
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
         T = T * inv_1ma;
-        const float e0 = cr - R0, e1 = cg - R1, e2 = cb - R2;
-        const float dot = e0 * dpx0 + e1 * dpx1 + e2 * dpx2;
-        R0 += av * e0;
-        R1 += av * e1;
-        R2 += av * e2;
+        const float cd = fmaf(r2.x, dpx1, r1.w * dpx0) + r2.y * dpx2;  // sum_c colour_c dL/dpix_c
+        const float dot = cd - D;                                      // sum_c (colour_c - accum_rec_c) dL/dpix_c
+        D = fmaf(av, dot, D);
         // dL/dalpha (upstream: sum_c (c - accum_rec) dL_dpix_c * T - T_final/(1-alpha) * bg.dL_dpix)
-        const float dL_dalpha = q.valid ? dot * T + inv_1ma * nTbg : 0.0f;
-        // dG/d(delta) = -G conic d; with W = G * opacity * dL/dalpha the per-pixel
-        // terms are dmean2D = -W (conic d) (W/2, H/2) and dconic = -W/2 (dx^2,
-        // dx dy, dy^2).  conic, (W, H) and -1/2 are per-Gaussian constants applied
-        // once in preprocess_bwd.hip, so the accumulator holds sum W (dx, dy) and
-        // sum W (dx^2, dx dy, dy^2).  G is finite (power <= 0 for the positive-
-        // definite conic), so an invalid pixel's zero dL/dalpha zeroes them all.
+        const float dL_dalpha = valid ? fmaf(dot, T, inv_1ma * nTbg) : 0.0f;
+        // dG/d(delta) = -G conic d; with W = opacity G dL/dalpha the per-pixel terms
+        // are dmean2D = -W (conic d) (W/2, H/2) and dconic = -W/2 (dx^2, dx dy,
+        // dy^2); conic, (W, H), -1/2 and the opacity are per-Gaussian constants
+        // applied once in preprocess_bwd.hip, so the accumulator holds sum g5 (dx,
+        // dy) and sum g5 (dx^2, dx dy, dy^2).  G is finite (power <= 0 for the
+        // positive-definite conic), so an invalid pixel's zero dL/dalpha zeroes them.
         Part p;
-        p.g5 = q.G * dL_dalpha;
-        p.W = p.g5 * op;
-        p.dx = q.dx;
-        p.dy = q.dy;
+        p.g5 = G * dL_dalpha;
+        p.dx = r3.x - fx;
+        p.dy = r3.y - fy;
         p.t = av * T;  // dchannel/dcolor
         return p;
     };
 
     // Reduce-scatter of a pair's 18 sums and their two atomic wave instructions.
     // First stage (xor 16) with swapped roles: lanes 16-31 keep b's values and
-    // send a's, so the nine outputs need only the ten selects of the five base
-    // quantities instead of eighteen selects of the products.  Then four more
-    // ds_swizzle stages (xor 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per
+    // send a's, and what crosses is three base quantities (g5, dx, dy) and the
+    // three colour products of the Gaussian the receiving lane keeps, not its nine
+    // sums: each lane forms both pixels' geometric products itself, the partner's
+    // terms fused into FMAs.  Then four
+    // more ds_swizzle stages (xor 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per
     // output register) and one final v_permlane32 self-swap adding the two halves.
     auto reduce_emit = [&](const Part &pa, const Part &pb, uint32_t gida, uint32_t gidb, bool two) {
-        const float kW = h16 ? pb.W : pa.W, sW = h16 ? pa.W : pb.W;
+        const float k5 = h16 ? pb.g5 : pa.g5, s5 = h16 ? pa.g5 : pb.g5;
         const float kx = h16 ? pb.dx : pa.dx, sx = h16 ? pa.dx : pb.dx;
         const float ky = h16 ? pb.dy : pa.dy, sy = h16 ? pa.dy : pb.dy;
-        const float k5 = h16 ? pb.g5 : pa.g5, s5 = h16 ? pa.g5 : pb.g5;
         const float kt = h16 ? pb.t : pa.t, st_ = h16 ? pa.t : pb.t;
-        // the partner (lane ^ 16) sends its five base quantities of the Gaussian
-        // this lane keeps, and this lane forms both pixels' nine products (five
-        // exchanges instead of nine, the partner's terms fused into FMAs)
         auto x16 = [&](float send) {
             return __builtin_bit_cast(float,
                                       __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send), 0x1F | (16 << 10)));
         };
-        const float rW = x16(sW), rx = x16(sx), ry = x16(sy), r5 = x16(s5), rt = x16(st_);
-        const float k0 = kW * kx, k1 = kW * ky;
-        const float r0 = rW * rx, r1 = rW * ry;
+        // the colour terms cross as the sender's own products t dL/dpix_c (no
+        // registers held for the partner pixel's dL/dpix)
+        const float r5 = x16(s5), rx = x16(sx), ry = x16(sy);
+        const float rt0 = x16(st_ * dpx0), rt1 = x16(st_ * dpx1), rt2 = x16(st_ * dpx2);
+        const float k0 = k5 * kx, k1 = k5 * ky;
+        const float r0 = r5 * rx, r1 = r5 * ry;
         const float o0 = k0 + r0;
         const float o1 = k1 + r1;
         const float o2 = fmaf(k0, kx, r0 * rx);
         const float o3 = fmaf(k0, ky, r0 * ry);
         const float o4 = fmaf(k1, ky, r1 * ry);
         const float o5 = k5 + r5;
-        const float o6 = fmaf(kt, dpx0, rt * qdpx0);
-        const float o7 = fmaf(kt, dpx1, rt * qdpx1);
-        const float o8 = fmaf(kt, dpx2, rt * qdpx2);
+        const float o6 = fmaf(kt, dpx0, rt0);
+        const float o7 = fmaf(kt, dpx1, rt1);
+        const float o8 = fmaf(kt, dpx2, rt2);
         const float t0 = swz_stage<8>(o0, o1, lane);
         const float t1 = swz_stage<8>(o2, o3, lane);
         const float t2 = swz_stage<8>(o4, o5, lane);
@@ -257,36 +246,36 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     auto replay_chunk = [&](int lo, float4 A, float4 B, float4 C) {
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         const uint64_t mask = __ballot(rel);
-        const int ns = stage_survivors(st, lane, rel, mask, A, B, C, 1);
+        if (rel) stage_quad(st.rec[survivor_slot(mask, 1)], A, B, C, (float)qx0, (float)qy0, lane);
+        const int ns = __builtin_popcountll(mask);
         const int lim = last_contrib - lo;  // entry lo + l replays for this pixel iff l < lim
         // byte offset of record b = k - 1 + 1 in a VGPR (asm barrier: keep it there)
         uint32_t boff = (uint32_t)(ns - 1) * (uint32_t)sizeof(st.rec[0]);
         asm volatile("" : "+v"(boff));
-        const char *sbase = reinterpret_cast<const char *>(&st.rec[0][0]);
+        const volatile char *sbase = reinterpret_cast<const volatile char *>(&st.rec[0][0]);
         for (int k = ns - 1; k >= 0; k -= 2) {
             const bool two = k >= 1;  // wave-uniform
             // whole 16-B reads (volatile: the load vectorizer would otherwise split
             // the records into 8-B pieces around the unused fields)
             lds_f32x4 *rb = (lds_f32x4 *)(sbase + boff);
             const float4 b0 = ld4(rb + 0), b1 = ld4(rb + 1), b2 = ld4(rb + 2);
-            const float4 a0 = ld4(rb + 3), a1 = ld4(rb + 4), a2 = ld4(rb + 5);
+            const float4 a0 = ld4(rb + 4), a1 = ld4(rb + 5), a2 = ld4(rb + 6);
+            const float2 b3 = ld2(sbase + boff + 48), a3 = ld2(sbase + boff + 112);
             boff -= 2 * (uint32_t)sizeof(st.rec[0]);
-            const int la = __float_as_int(a2.w), lb = __float_as_int(b2.w);
-            Pre qa = prepare(a0, a1), qb = prepare(b0, b1);
-            const bool na = blend_near(qa.power, a1.y * qa.G), nb = blend_near(qb.power, b1.y * qb.G);
+            float pa = quad_power(a0, a1, lx, ly), pb = quad_power(b0, b1, lx, ly);
+            float Ga = __expf(pa), Gb = __expf(pb);
+            const bool na = blend_near(pa, a1.z * Ga), nb = blend_near(pb, b1.z * Gb);
             if (__builtin_expect(__ballot(na || nb) != 0, 0)) {  // rare: exact skip decisions (gsr_blend.hpp)
-                if (na) blend_fix(qa.power, qa.G, qa.dx, qa.dy, a0.z, a0.w, a1.x);
-                if (nb) blend_fix(qb.power, qb.G, qb.dx, qb.dy, b0.z, b0.w, b1.x);
+                if (na) blend_fix(pa, Ga, a3.x - fx, a3.y - fy, a0.w, 0.5f * a1.x, a1.y);
+                if (nb) blend_fix(pb, Gb, b3.x - fx, b3.y - fy, b0.w, 0.5f * b1.x, b1.y);
             }
-            finish(qa, a1, la, lim, true);  // entry lo + l = upstream `contributor`
-            finish(qb, b1, lb, lim, two);
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
-            const Part pa = replay(qa, a1.y, a1.z, a1.w, a2.x);  // back to front: a before b
-            const Part pb = replay(qb, b1.y, b1.z, b1.w, b2.x);
-            const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.y));
-            const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.y));
-            reduce_emit(pa, pb, gida, gidb, two);
+            const Part qa = replay(pa, Ga, a1, a2, a3, lim);  // back to front: a before b
+            const Part qb = replay(pb, Gb, b1, b2, b3, two ? lim : 0);
+            const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.z));
+            const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.z));
+            reduce_emit(qa, qb, gida, gidb, two);
         }
     };
     // Double-buffered backwards stream, unrolled by two so the buffers swap roles

@@ -33,31 +33,15 @@ struct RenderFwdArgs {
     int maxc;
 };
 
-#ifndef GSR_FWD_GROUP
-#define GSR_FWD_GROUP 2
-#endif
-constexpr int FWD_GROUP = GSR_FWD_GROUP;  // Gaussians per blend iteration
+constexpr int FWD_GROUP = 2;  // Gaussians per blend iteration (the zero record after the survivors pads an odd count)
 
-// Per-wave LDS image of a chunk's surviving Gaussians for the forward.  Each
-// record carries the power as a quadratic in the pixel's offset (x, y) in 0..7
-// from the quadrant's first pixel:
-//   p(x, y) = K6 + K4 x + K5 y + K1 x^2 + K2 x y + K3 y^2
-// (conic' = -conic/2, centre offset (u, v) = mean - quadrant origin: K1 = c'a,
-// K2 = 2 c'b, K3 = c'c, K4 = -2 (c'a u + c'b v), K5 = -2 (c'b u + c'c v),
-// K6 = p(0, 0)), five FMAs per pixel instead of the eight of d^T conic' d.
-// It is within a few ulp of upstream's expression like that one (the expansion
-// keeps the terms at the magnitude of the form itself); the rare pairs near a
-// skip threshold are redone exactly from (u, v) (blend_fix).
-//   rec[k][0] = {K6, K4, K5, K1}, rec[k][1] = {K2, K3, opacity, r},
-//   rec[k][2] = {g, b, -, lane},  rec[k][3] = {u, v, -, -}
-// Record ns (after the survivors) is all zeros: opacity 0 blends nothing, so the
-// odd count's second Gaussian needs no mask (render_fwd 145 -> 142 us at C,
-// 374-379 -> 370 us at E).  It takes 66 VGPRs: 7 waves per SIMD (forced to 8,
-// the compiler spilled 4 VGPRs to scratch, 1-2 us slower and +20 % traffic).
-struct FwdChunk {
-    float4 rec[65][4];
-};
-
+// The survivors of a chunk are staged as QuadChunk records (gsr_blend.hpp): the
+// power is a quadratic in the lane's quadrant offset, five FMAs per pixel, the
+// same instructions render_bwd uses.  The zero record after the survivors lets
+// the odd count's second Gaussian blend nothing without a mask (render_fwd
+// 145 -> 142 us at C, 374-379 -> 370 us at E).  It takes 66 VGPRs: 7 waves per
+// SIMD (forced to 8, the compiler spilled 4 VGPRs to scratch, 1-2 us slower and
+// +20 % traffic).  Three or four Gaussians per iteration spilled.
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(7))) render_fwd_kernel(RenderFwdArgs a) {
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
@@ -67,6 +51,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float lx = (float)(lane & 7), ly = (float)(lane >> 3);  // offset in the quadrant
+    const float fpx = (float)px, fpy = (float)py;
     const uint2 r = a.ranges[tile];
     const int n = (int)(r.y - r.x);
 
@@ -76,8 +61,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // the pixel's skip threshold on alpha: upstream's 1/255 while it blends, 2
     // (above any alpha) once it has stopped or when it lies outside the image
     float thr = inside ? 1.0f / 255.0f : 2.0f;
-    __shared__ FwdChunk stage[BLEND_WAVES];
-    FwdChunk &st = stage[BLEND_WAVES == 1 ? 0 : w];
+    __shared__ QuadChunk stage[BLEND_WAVES];
+    QuadChunk &st = stage[BLEND_WAVES == 1 ? 0 : w];
     if (__any(inside) && n > 0) {
         const uint32_t *list = a.point_list + r.x;
         const int nm1 = n - 1;
@@ -86,19 +71,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
             const uint64_t mask = __ballot(rel);
-            if (rel) {  // compacted: slot = survivors in lower lanes
-                const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                const float u = A.x - (float)qx0, v = A.y - (float)qy0;  // exact (see blend_fix)
-                const float ca = A.z, cb = A.w, cc = B.x;
-                const float hu = ca * u + cb * v, hv = cb * u + cc * v;
-                st.rec[slot][0] = make_float4(u * hu + v * hv, -2.0f * hu, -2.0f * hv, ca);
-                st.rec[slot][1] = make_float4(2.0f * cb, cc, B.y, B.z);
-                st.rec[slot][2] = make_float4(B.w, C.x, 0.0f, __int_as_float(lane));
-                st.rec[slot][3] = make_float4(u, v, 0.0f, 0.0f);
-            }
+            if (rel) stage_quad(st.rec[survivor_slot(mask, 0)], A, B, C, (float)qx0, (float)qy0, lane);
             const int ns = __builtin_popcountll(mask);
-            if (lane < 3) st.rec[ns][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            stage_zero(st.rec[ns], lane);
             work += ns;
             // FWD_GROUP Gaussians per iteration: their LDS reads, powers and exps are
             // independent, so each wave has that much instruction-level parallelism
@@ -113,8 +88,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                     const int kg = k + g;  // ns itself: the zero record
                     const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r2 = st.rec[kg][2];
                     li[g] = __float_as_int(r2.w);
-                    const float t1 = fmaf(r1.x, ly, fmaf(r0.w, lx, r0.y)), t2 = fmaf(r1.y, ly, r0.z);
-                    pw[g] = fmaf(t2, ly, fmaf(t1, lx, r0.x));
+                    pw[g] = quad_power(r0, r1, lx, ly);
                     G[g] = __expf(pw[g]);
                     op[g] = r1.z;
                     near = near || blend_near(pw[g], op[g] * G[g]);
@@ -127,9 +101,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                     for (int g = 0; g < FWD_GROUP; g++) {
                         const int kg = k + g;
                         const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r3 = st.rec[kg][3];
-                        // d = mean - pixel = (u - x, v - y), exact like upstream's subtraction
+                        // d = mean - pixel with upstream's single rounding
                         if (blend_near(pw[g], op[g] * G[g]))
-                            blend_fix(pw[g], G[g], r3.x - lx, r3.y - ly, r0.w, 0.5f * r1.x, r1.y);
+                            blend_fix(pw[g], G[g], r3.x - fpx, r3.y - fpy, r0.w, 0.5f * r1.x, r1.y);
                     }
                 }
 #pragma unroll

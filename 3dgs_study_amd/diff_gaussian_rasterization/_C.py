@@ -21,6 +21,7 @@ ROCm device, otherwise these functions raise.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 from pathlib import Path
 
@@ -54,7 +55,7 @@ EXPORTED = (
     "gsr_l1_ssim_scratch_bytes", "gsr_l1_ssim", "gsr_adam_step", "gsr_densify_stats",
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
-    "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys",
+    "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -86,6 +87,50 @@ def get_footprint() -> str:
     return _footprint
 
 
+class GsrLeafGrads(ctypes.Structure):
+    """Mirror of ``gsr_leaf_grads`` in include/gsr.h."""
+    _fields_ = [("dsh_dc", ctypes.c_void_p), ("dsh_rest", ctypes.c_void_p), ("dscaling", ctypes.c_void_p),
+                ("dopacity", ctypes.c_void_p), ("drotation", ctypes.c_void_p), ("rotation_norm", ctypes.c_void_p),
+                ("rotation_eps", ctypes.c_float), ("accumulate", ctypes.c_int32), ("dsh_planar", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class LeafGrads:
+    """Outputs (and their inputs) of ``rasterize_gaussians_backward(leaf=...)``: the
+    leaf gradients of the caller's activations written by the library itself
+    (gsr_backward_leaves, include/gsr.h).  Every tensor is float32, contiguous, on
+    the rasterizer's device; ``accumulate`` bits add into an output instead of
+    overwriting it (1 dsh, 2 dscaling, 4 dopacity, 8 drotation).  ``dopacity``
+    needs the backward's ``opacities``; ``drotation`` needs ``rotation_norm`` (the
+    norms torch's F.normalize computed, [P,1])."""
+
+    _SHAPES = {"dsh_dc": lambda P, M: (P, 1, 3), "dsh_rest": lambda P, M: (P, M - 1, 3),
+               "dscaling": lambda P, M: (P, 3), "dopacity": lambda P, M: (P, 1), "drotation": lambda P, M: (P, 4),
+               "rotation_norm": lambda P, M: (P, 1)}
+
+    def __init__(self, dsh_dc=None, dsh_rest=None, dscaling=None, dopacity=None, drotation=None,
+                 rotation_norm=None, rotation_eps=1e-12, accumulate=0):
+        self.dsh_dc, self.dsh_rest, self.dscaling, self.dopacity, self.drotation = (dsh_dc, dsh_rest, dscaling,
+                                                                                    dopacity, drotation)
+        self.rotation_norm = rotation_norm
+        self.rotation_eps, self.accumulate = float(rotation_eps), int(accumulate)
+
+    def struct(self, P, M, device, dsh_planar=False) -> GsrLeafGrads:
+        ptr = {}
+        for name, shape in self._SHAPES.items():
+            t = getattr(self, name)
+            if t is None or (name == "dsh_rest" and M <= 1):
+                ptr[name] = None
+                continue
+            if (t.dtype != torch.float32 or t.device != device or not t.is_contiguous()
+                    or t.numel() != math.prod(shape(P, M))):
+                raise RuntimeError(f"leaf gradient {name}: expected a contiguous float32 tensor of shape "
+                                   f"{shape(P, M)} on {device}")
+            ptr[name] = t.data_ptr()
+        return GsrLeafGrads(rotation_eps=self.rotation_eps, accumulate=self.accumulate,
+                            dsh_planar=int(bool(dsh_planar)), **ptr)
+
+
 class GsrAdamSegment(ctypes.Structure):
     """Mirror of ``gsr_adam_segment`` in include/gsr.h."""
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
@@ -93,7 +138,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 
@@ -131,6 +176,8 @@ def load_library():
     lib.gsr_backward.restype = ctypes.c_int
     lib.gsr_backward_planar.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward_planar.restype = ctypes.c_int
+    lib.gsr_backward_leaves.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [ctypes.POINTER(GsrLeafGrads), vp]
+    lib.gsr_backward_leaves.restype = ctypes.c_int
     for name in ("gsr_backward_colors", "gsr_backward_colors_render", "gsr_backward_colors_finish"):
         getattr(lib, name).argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
         getattr(lib, name).restype = ctypes.c_int
@@ -262,7 +309,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                  viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
                                  geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None, dsh_planar=False,
-                                 on_drgb=None):
+                                 on_drgb=None, leaf=None, opacities=None):
     """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)
 
     Not upstream (keyword-only extensions; the defaults are upstream's behaviour):
@@ -273,11 +320,19 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     (strides (3, 3P, 1); gsr_backward_planar), same values.
     ``on_drgb`` (with ``drgb_out``) — called once drgb is queued on the stream and
     before the per-Gaussian backward is (gsr_backward_colors_render / _finish), so
-    the caller can start exchanging drgb under it."""
+    the caller can start exchanging drgb under it.
+    ``leaf`` — a ``LeafGrads`` (diff_gaussian_rasterization.leaf_grads): the library
+    writes the requested leaf gradients of the caller's activations itself
+    (gsr_backward_leaves) and returns None in place of the activation gradients
+    they replace (dsh, dopacity, dscales, drot).
+    ``opacities`` — the forward's opacity input [P,1] (upstream's backward reads
+    it from the geom buffer; passed here it is read coalesced); required with a
+    leaf opacity gradient."""
     lib = load_library()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
-    s, keep, device, M = _inputs(background, means3D, colors, None, scales, rotations, scale_modifier, cov3D_precomp,
-                                 viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
+    s, keep, device, M = _inputs(background, means3D, colors, opacities, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos,
+                                 False, debug)
     P = s.P
     f32 = dict(dtype=torch.float32, device=device)
     dmeans2D = torch.empty((P, 3), **f32)
@@ -285,7 +340,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dopacity = torch.empty((P, 1), **f32)
     dmeans3D = torch.empty((P, 3), **f32)
     dcov3D = torch.empty((P, 6), **f32)
-    if drgb_out is not None:
+    if leaf is not None and drgb_out is not None:
+        raise RuntimeError("rasterize_gaussians_backward: leaf and drgb_out are exclusive")
+    if leaf is not None and leaf.dsh_dc is not None:
+        dsh = None
+    elif drgb_out is not None:
         dsh = None
     elif dsh_planar:
         dsh = torch.empty((M, P, 3), **f32).permute(1, 0, 2)
@@ -293,6 +352,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         dsh = torch.empty((P, M, 3), **f32)
     dscales = torch.empty((P, 3), **f32)
     drot = torch.empty((P, 4), **f32)
+    if leaf is not None:
+        dopacity = None if leaf.dopacity is not None else dopacity
+        dscales = None if leaf.dscaling is not None else dscales
+        drot = None if leaf.drotation is not None else drot
     if P == 0:
         return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
     accum = torch.empty((lib.gsr_accum_bytes(P),), dtype=torch.uint8, device=device)
@@ -303,16 +366,21 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                 or drgb_out.numel() < 3 * P):
             raise RuntimeError("drgb_out must be a contiguous float32 tensor of >= 3P elements on the input device")
         fn, last = lib.gsr_backward_colors, drgb_out.data_ptr()
-    elif dsh_planar and M > 0 and P > 0:
+    elif dsh_planar and dsh is not None and M > 0 and P > 0:
         fn, last = lib.gsr_backward_planar, dsh.data_ptr()
     else:
         fn, last = lib.gsr_backward, _ptr(dsh)
-    call = lambda f: f(ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),  # noqa: E731
-                       binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
-                       int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), dcolors.data_ptr(),
-                       dopacity.data_ptr(), dmeans3D.data_ptr(), dcov3D.data_ptr(), last,
-                       dscales.data_ptr(), drot.data_ptr(), _stream(device))
-    if drgb_out is not None and on_drgb is not None:
+    if leaf is not None:
+        fn, last = lib.gsr_backward_leaves, _ptr(dsh)
+    head = lambda: (ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),  # noqa: E731
+                    binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+                    int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), dcolors.data_ptr(),
+                    _ptr(dopacity), dmeans3D.data_ptr(), dcov3D.data_ptr(), last, _ptr(dscales), _ptr(drot))
+    call = lambda f: f(*head(), _stream(device))  # noqa: E731
+    if leaf is not None:
+        lg = leaf.struct(P, M, device, dsh_planar)
+        _check(lib.gsr_backward_leaves(*head(), ctypes.byref(lg), _stream(device)), "rasterize_gaussians_backward")
+    elif drgb_out is not None and on_drgb is not None:
         _check(call(lib.gsr_backward_colors_render), "rasterize_gaussians_backward")
         on_drgb()
         _check(call(lib.gsr_backward_colors_finish), "rasterize_gaussians_backward")

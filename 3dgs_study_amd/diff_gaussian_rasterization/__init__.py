@@ -35,6 +35,7 @@ kernel; on failure a CPU copy of the arguments is written to
 """
 from __future__ import annotations
 
+import os
 from typing import NamedTuple
 
 import torch
@@ -45,9 +46,148 @@ from . import _C
 from ._C import get_footprint, set_footprint  # noqa: E402
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "set_sh_grad_sink",
-           "set_footprint", "get_footprint"]
+           "set_footprint", "get_footprint", "set_fused_leaf_grads"]
 
 _sh_grad_sink = None
+_fused_leaf_grads = os.environ.get("GSR_FUSED_LEAF_GRADS", "1") != "0"
+last_leaf_plan = ()  # the activations whose leaf gradients the last backward wrote itself
+
+
+def set_fused_leaf_grads(on: bool) -> bool:
+    """Enable (default; env GSR_FUSED_LEAF_GRADS=0 disables) writing the leaf
+    gradients of the caller's activations from the rasterizer backward (see
+    ``_leaf_plan``); returns the previous setting."""
+    global _fused_leaf_grads
+    prev, _fused_leaf_grads = _fused_leaf_grads, bool(on)
+    return prev
+
+
+# ---------------------------------------------------------------- fused leaf gradients
+# The reference hands the rasterizer activations of GaussianModel's leaves
+# (scene/gaussian_model.py:106-126): shs = cat(_features_dc, _features_rest, dim=1),
+# scales = exp(_scaling), opacities = sigmoid(_opacity), rotations =
+# F.normalize(_rotation).  Upstream's backward returns the activation gradients and
+# torch then runs the cat's slice copies (a 192 MB transposing copy for f_rest at
+# 1M Gaussians, SH3), the exp / sigmoid / normalize backwards (~20 small kernels)
+# and AccumulateGrad.  When the autograd graph is exactly that — checked node by
+# node at backward time — the library writes each leaf's gradient itself, with
+# torch's operation order (bit-identical results), and the Function returns None
+# for that input, so torch skips the activation's backward.  Anything else keeps
+# upstream's path for that input: another graph shape, hooks on the activation or
+# the leaf (tensor hooks, retain_grad, post-accumulate hooks: the view-parallel
+# exchange's all-reduce hooks), create_graph, autograd.grad / backward(inputs=...)
+# not accumulating into the leaf, or an existing .grad that is not a dense
+# contiguous float32 tensor.  Hooks registered directly on an AccumulateGrad node
+# are invisible from Python: such callers disable this with set_fused_leaf_grads.
+def _acc_leaf(node):
+    return node.variable if node is not None and type(node).__name__ == "AccumulateGrad" else None
+
+
+def _leaf_state(leaf, shape, device):
+    """-1: not fusable; 0: no .grad yet (write it); 1: add into the existing .grad."""
+    if (leaf is None or not leaf.is_leaf or not leaf.requires_grad or leaf.dtype != torch.float32
+            or leaf.device != device or tuple(leaf.shape) != tuple(shape) or not leaf.is_contiguous()
+            or leaf._backward_hooks or getattr(leaf, "_post_accumulate_grad_hooks", None)):
+        return -1
+    g = leaf.grad
+    if g is None:
+        return 0
+    if (g.layout != torch.strided or g.dtype != torch.float32 or g.device != device
+            or tuple(g.shape) != tuple(shape) or not g.is_contiguous() or g.requires_grad):
+        return -1
+    return 1
+
+
+def _plain_activation(t) -> bool:
+    return not t._backward_hooks and not t.retains_grad
+
+
+def _will_run(node) -> bool:
+    try:  # raises inside autograd.grad for leaf nodes: not an accumulating backward
+        return bool(torch._C._will_engine_execute_node(node))
+    except Exception:
+        return False
+
+
+def _leaf_plan(sh, colors_precomp, opacities, scales, rotations, needs, sink_takes_sh):
+    """{name: (leaf tensors, state, extras)} for the activations whose leaf gradients
+    the backward may write itself (see above); called inside backward."""
+    if torch.is_grad_enabled():  # create_graph: the activations' backwards must be recorded
+        return {}
+    plan = {}
+    device = opacities.device
+    P = opacities.shape[0]
+    try:
+        if needs[2] and not sink_takes_sh and sh.numel() and colors_precomp.numel() == 0 and _plain_activation(sh):
+            n = sh.grad_fn
+            if (type(n).__name__ == "CatBackward0" and n._saved_dim in (1, -2) and len(n.next_functions) == 2
+                    and sh.dim() == 3 and sh.shape[2] == 3):
+                M = sh.shape[1]
+                dc, rest = _acc_leaf(n.next_functions[0][0]), _acc_leaf(n.next_functions[1][0])
+                a, b = _leaf_state(dc, (P, 1, 3), device), _leaf_state(rest, (P, M - 1, 3), device)
+                if a >= 0 and a == b and _will_run(n.next_functions[0][0]) and _will_run(n.next_functions[1][0]):
+                    plan["sh"] = ((dc, rest), a, None)
+        if needs[5] and scales.numel() and _plain_activation(scales):
+            n = scales.grad_fn
+            if type(n).__name__ == "ExpBackward0" and n._saved_result.data_ptr() == scales.data_ptr():
+                leaf = _acc_leaf(n.next_functions[0][0])
+                st = _leaf_state(leaf, (P, 3), device)
+                if st >= 0 and _will_run(n.next_functions[0][0]):
+                    plan["scales"] = ((leaf,), st, None)
+        if needs[4] and opacities.numel() and _plain_activation(opacities):
+            n = opacities.grad_fn
+            if type(n).__name__ == "SigmoidBackward0" and n._saved_result.data_ptr() == opacities.data_ptr():
+                leaf = _acc_leaf(n.next_functions[0][0])
+                st = _leaf_state(leaf, (P, 1), device)
+                if st >= 0 and _will_run(n.next_functions[0][0]):
+                    plan["opacities"] = ((leaf,), st, None)
+        if needs[6] and rotations.numel() and _plain_activation(rotations):
+            d = rotations.grad_fn
+            if type(d).__name__ == "DivBackward0" and len(d.next_functions) == 2:
+                acc, e = d.next_functions[0][0], d.next_functions[1][0]
+                c = e.next_functions[0][0] if type(e).__name__ == "ExpandBackward0" else None
+                nrm = c.next_functions[0][0] if type(c).__name__ == "ClampMinBackward0" else None
+                if (type(nrm).__name__ == "LinalgVectorNormBackward0" and float(nrm._saved_ord) == 2.0
+                        and tuple(nrm._saved_dim) in ((1,), (-1,)) and nrm._saved_keepdim
+                        and nrm.next_functions[0][0] is acc):
+                    leaf = _acc_leaf(acc)
+                    st = _leaf_state(leaf, (P, 4), device)
+                    norm = nrm._saved_result
+                    if (st >= 0 and norm.shape == (P, 1) and norm.dtype == torch.float32 and norm.device == device
+                            and d._saved_self.data_ptr() == leaf.data_ptr() and _will_run(acc)):
+                        plan["rotations"] = ((leaf,), st, (norm.contiguous(), float(c._saved_min)))
+    except (AttributeError, RuntimeError, TypeError):
+        return {}
+    return plan
+
+
+def _leaf_outputs(plan):
+    """The LeafGrads of a plan: the existing .grad where it accumulates, else fresh tensors."""
+    kw, fresh, acc = {}, [], 0
+
+    def out(leaf, state, bit):
+        nonlocal acc
+        if state == 1:
+            acc |= bit
+            return leaf.grad
+        t = torch.empty_like(leaf, memory_format=torch.contiguous_format)
+        fresh.append((leaf, t))
+        return t
+
+    if "sh" in plan:
+        (dc, rest), st, _ = plan["sh"]
+        kw["dsh_dc"], kw["dsh_rest"] = out(dc, st, 1), out(rest, st, 1)
+    if "scales" in plan:
+        (leaf,), st, _ = plan["scales"]
+        kw["dscaling"] = out(leaf, st, 2)
+    if "opacities" in plan:
+        (leaf,), st, _ = plan["opacities"]
+        kw["dopacity"] = out(leaf, st, 4)
+    if "rotations" in plan:
+        (leaf,), st, (norm, eps) = plan["rotations"]
+        kw["drotation"] = out(leaf, st, 8)
+        kw["rotation_norm"], kw["rotation_eps"] = norm, eps
+    return _C.LeafGrads(accumulate=acc, **kw), fresh
 
 
 def set_sh_grad_sink(sink):
@@ -89,6 +229,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.num_rendered = num_rendered
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom, binning,
                               img)
+        ctx.opacities = opacities  # an input (no reference cycle): its grad_fn for the fused leaf gradients
         ctx.mark_non_differentiable(radii)
         return color, radii
 
@@ -100,21 +241,36 @@ class _RasterizeGaussians(torch.autograd.Function):
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree, rs.campos,
                 geom, ctx.num_rendered, binning, img, rs.debug)
         sink = _sh_grad_sink
-        if sink is not None and sh.numel() > 0 and colors_precomp.numel() == 0 and sink.accepts(sh, means3D):
+        sink_takes_sh = sink is not None and sh.numel() > 0 and colors_precomp.numel() == 0 and sink.accepts(sh,
+                                                                                                           means3D)
+        plan = (_leaf_plan(sh, colors_precomp, ctx.opacities, scales, rotations, ctx.needs_input_grad, sink_takes_sh)
+                if _fused_leaf_grads and means3D.size(0) > 0 and not sink_takes_sh else {})
+        global last_leaf_plan
+        last_leaf_plan = tuple(sorted(plan))
+        if plan:
+            leaf, fresh = _leaf_outputs(plan)
+            (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
+                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True, leaf=leaf, opacities=ctx.opacities),
+                args, rs.debug, "snapshot_bw.dump", "backward")
+            for p, g in fresh:
+                p.grad = g
+            return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
+        if sink_takes_sh:
             rec = sink.record(means3D.size(0))
             # the record's exchange starts as soon as the colour gradient is queued,
             # under the per-Gaussian backward
             push = lambda: sink.push(rec, rs.campos, rs.sh_degree)  # noqa: E731
             (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
-                lambda *a: _C.rasterize_gaussians_backward(*a, drgb_out=rec[4:], on_drgb=push), args, rs.debug,
+                lambda *a: _C.rasterize_gaussians_backward(*a, drgb_out=rec[4:], on_drgb=push,
+                                                           opacities=ctx.opacities), args, rs.debug,
                 "snapshot_bw.dump", "backward")
         else:
             # dsh as the [P,M,3] view of coefficient planes: the reference's SH cat
             # backward (get_features) then slices an f_dc gradient that already has
             # _features_dc's layout, and AccumulateGrad keeps it without a copy
             (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
-                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True), args, rs.debug, "snapshot_bw.dump",
-                "backward")
+                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True, opacities=ctx.opacities), args,
+                rs.debug, "snapshot_bw.dump", "backward")
         return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
 
 

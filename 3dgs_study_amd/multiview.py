@@ -112,7 +112,10 @@ class GradAllReduce:
         self.numel = sum(p.numel() for p in self.params)
         self._reduced = [p for p in self.params if self._sh is None or not any(p is q for q in self._sh[1:])]
         self._counts = {id(p): 0 for p in self._reduced}
-        if self.overlap:
+        # hooks only while there is something to exchange: with one rank the
+        # rasterizer may then write the leaves' gradients itself (diff_gaussian_
+        # rasterization's fused leaf gradients skip leaves that carry hooks)
+        if self.overlap and self._active():
             for p in self._reduced:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._launch))
 
@@ -252,19 +255,23 @@ class GradAllReduce:
 
 @torch.no_grad()
 def reduce_densification_stats(xyz_gradient_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
-                               group=None, force: bool = False) -> None:
-    """Combine the ranks' densification statistics in place before a densify step:
-    SUM of the accumulated screen-space gradient norms and of the visibility counts,
-    MAX of the largest screen radii (scene/gaussian_model.py:565-581 accumulates them
-    per view; train.py:126-127 and :130-136 use them), so every rank densifies and
-    prunes the same Gaussians and the replicas stay identical."""
+                               group=None, force: bool = False):
+    """The ranks' densification statistics combined for a densify step: SUM of the
+    accumulated screen-space gradient norms and of the visibility counts, MAX of the
+    largest screen radii (scene/gaussian_model.py:565-581 accumulates them per view;
+    train.py:126-127 and :130-136 use them), so every rank densifies and prunes the
+    same Gaussians and the replicas stay identical.  Returns reduced copies
+    (xyz_gradient_accum, denom, max_radii2D) and leaves the per-rank accumulators
+    as they are, so calling it again (another caller, a non-densify iteration)
+    cannot count a rank's views twice; densify_and_prune reads the copies and the
+    accumulators are reset as upstream resets them (densification_postfix)."""
     if not (dist.is_initialized() and (dist.get_world_size(group) > 1 or force)):
-        return
+        return xyz_gradient_accum.clone(), denom.clone(), max_radii2D.clone()
     both = torch.cat([xyz_gradient_accum.reshape(-1), denom.reshape(-1)])
+    mx = max_radii2D.clone()
     w1 = dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group, async_op=True)
-    w2 = dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX, group=group, async_op=True)
+    w2 = dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group, async_op=True)
     w1.wait()
     w2.wait()
     n = xyz_gradient_accum.numel()
-    xyz_gradient_accum.copy_(both[:n].view_as(xyz_gradient_accum))
-    denom.copy_(both[n:].view_as(denom))
+    return both[:n].view_as(xyz_gradient_accum), both[n:].view_as(denom), mx

@@ -216,11 +216,12 @@ class TrainState:
                 return group["lr"]
 
     def reduce_densification_stats(self, group=None):
-        """View-parallel: SUM / SUM / MAX the per-rank statistics over the group before a
-        densify step (multiview.reduce_densification_stats)."""
+        """View-parallel: the per-rank statistics SUM / SUM / MAX-reduced over the group
+        for a densify step, as copies (xyz_gradient_accum, denom, max_radii2D); the
+        per-rank accumulators are left alone (multiview.reduce_densification_stats)."""
         import multiview
 
-        multiview.reduce_densification_stats(self.xyz_gradient_accum, self.denom, self.max_radii2D, group)
+        return multiview.reduce_densification_stats(self.xyz_gradient_accum, self.denom, self.max_radii2D, group)
 
     @torch.no_grad()
     def densification_stats(self, out: dict):

@@ -356,6 +356,8 @@ def main():
         if world == 1 and args.render_steps > 0:
             del out
             line["config_E_render"] = render_rates("E", dev, args.render_steps, 3)
+            if _C.get_footprint() != "rect":  # upstream's instance set (I ~ 110M): the tile sort's stress case
+                line["config_E_render_rect"] = render_rates("E", dev, args.render_steps, 3, footprint="rect")
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
@@ -415,10 +417,23 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
             "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "stages_source": STAGES_SOURCE["split"]}
 
 
-def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0) -> dict:
+def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0, footprint=None) -> dict:
     """Forward-only throughput of reference render() (render.py:37-49 renders under
     torch.no_grad()) at a forward-only config (E: 5M Gaussians, 4K, SH3): frames/s,
-    Mpix/s, the per-stage split, and render_fwd's algorithmic bytes ÷ its live time."""
+    Mpix/s, the per-stage split, and the largest stage's algorithmic bytes ÷ its live
+    time.  ``footprint`` ("rect": upstream's instance set, I = num_rendered as upstream
+    bins it) overrides the package default for this measurement."""
+    from diff_gaussian_rasterization import set_footprint
+
+    prev = set_footprint(footprint) if footprint else None
+    try:
+        return _render_rates(cfg_name, dev, steps, warmup, view)
+    finally:
+        if prev is not None:
+            set_footprint(prev)
+
+
+def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int) -> dict:
     import torch
 
     import synthetic

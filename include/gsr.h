@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 5
+#define GSR_ABI_VERSION 6
 
 enum gsr_status {
     GSR_OK = 0,
@@ -138,6 +138,48 @@ int gsr_backward_planar(const gsr_inputs *in, const int32_t *radii, const void *
                         const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
                         float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
                         float *dscales, float *drot, void *stream);
+
+/* Leaf gradients of the caller's activations, written by the per-Gaussian
+ * backward itself (not upstream).  The reference feeds the rasterizer
+ * activations of GaussianModel's leaf parameters (scene/gaussian_model.py:
+ * 106-126): shs = cat(_features_dc, _features_rest, dim=1), scales =
+ * exp(_scaling), opacities = sigmoid(_opacity), rotations =
+ * F.normalize(_rotation) (norm clamped at rotation_eps).  Upstream returns
+ * dsh / dscales / dopacity / drot and torch's autograd then runs the cat slice
+ * copies, exp / sigmoid / normalize backwards and AccumulateGrad; with a
+ * non-NULL output here the library writes the leaf's gradient directly, with
+ * torch's operation order (exp: d * scales; sigmoid: (d * (1 - o)) * o;
+ * normalize: the Div / Expand / ClampMin / LinalgVectorNorm backwards), and
+ * the corresponding activation gradient is not written (that output pointer
+ * may be NULL).  accumulate bit k adds into output k (AccumulateGrad's
+ * `grad += new`) instead of overwriting: bit 0 dsh_dc + dsh_rest, bit 1
+ * dscaling, bit 2 dopacity, bit 3 drotation.  Inputs by output:
+ *   dsh_dc [P,1,3], dsh_rest [P,M-1,3] (NULL when M == 1): in->sh required;
+ *   dscaling [P,3]: in->scales (= exp(_scaling)) required;
+ *   dopacity [P,1]: in->opacities (= sigmoid(_opacity)) required;
+ *   drotation [P,4]: in->rotations (= F.normalize(_rotation), the quotient
+ *                    torch computed) and rotation_norm [P] (the row norms
+ *                    torch computed, LinalgVectorNormBackward0's result) required.
+ * (The backward reads in->opacities whenever it is given; without it the
+ * opacity comes from the forward's geom buffer.) */
+typedef struct gsr_leaf_grads {
+    float *dsh_dc;
+    float *dsh_rest;
+    float *dscaling;
+    float *dopacity;
+    float *drotation;
+    const float *rotation_norm;
+    float rotation_eps;
+    int32_t accumulate;
+    int32_t dsh_planar;  /* a (non-leaf) dsh output is written as gsr_backward_planar's planes */
+    int32_t reserved;
+} gsr_leaf_grads;
+
+/* gsr_backward with the leaf outputs above (leaf may be NULL = gsr_backward). */
+int gsr_backward_leaves(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                        const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
+                        float *dscales, float *drot, const gsr_leaf_grads *leaf, void *stream);
 
 /* View-parallel exchange of the SH gradient (3dgs_study_amd/multiview.py;
  * SURVEY.md §8e).  Upstream has no multi-GPU path; these two calls split

@@ -245,3 +245,36 @@ def cov3d(scales, scale_modifier, rotations):
     lib.oracle_cov3d(ctypes.c_int(P), _p(scales), ctypes.c_float(scale_modifier), _p(_f32(rotations).reshape(P, 4)),
                      _p(out))
     return out
+
+
+def activation_leaf_grads(dsh, dopacity, dscales, drot, opacities, scales, rotations, rotation_norm,
+                          rotation_eps=1e-12, sum_order="pairwise"):
+    """Leaf gradients of the reference's activations (scene/gaussian_model.py:106-126)
+    from the rasterizer's activation gradients, in float32 with torch autograd's
+    operation order — what gsr_leaf_grads asks the library for (include/gsr.h):
+    get_features' cat -> the two slices of dsh; exp(_scaling) -> dscales * scales;
+    sigmoid(_opacity) -> (dopacity * (1 - o)) * o; F.normalize(_rotation) -> the
+    Div / Expand (sum) / ClampMin / LinalgVectorNorm backwards, summed, written
+    with the quotient q = rotations torch produced for every x / n it divides
+    (rotation_norm: the norms torch computed).  numpy
+    float32 scalar ops round like the kernel (no contraction).  ``sum_order``: how
+    the normalize backward's 4-term sum (ExpandBackward0) is added — "pairwise"
+    ((a + b) + (c + d)) as torch's GPU reduction and the library do, "sequential"
+    as torch's CPU reduction does."""
+    f = np.float32
+    out = {"dsh_dc": dsh[:, :1].copy(), "dsh_rest": dsh[:, 1:].copy(),
+           "dscaling": (dscales.astype(f) * scales.astype(f)).astype(f),
+           "dopacity": ((dopacity.astype(f) * (f(1) - opacities.astype(f))) * opacities.astype(f)).astype(f)}
+    g, q = drot.astype(f), rotations.astype(f)
+    nr = rotation_norm.reshape(-1, 1).astype(f)
+    eps = f(rotation_eps)
+    n = np.where(np.isnan(nr), nr, np.maximum(nr, eps))
+    og = -g * (q / n)
+    if sum_order == "pairwise":
+        s = (og[:, 0:1] + og[:, 1:2]) + (og[:, 2:3] + og[:, 3:4])
+    else:
+        s = ((og[:, 0:1] + og[:, 1:2]) + og[:, 2:3]) + og[:, 3:4]
+    gm = np.where(nr >= eps, s, f(0))
+    xn = np.where(nr == 0, f(0), q)
+    out["drotation"] = (g / n + gm * xn).astype(f)
+    return out

@@ -35,11 +35,14 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 5
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 6
     # 12 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 48 + 11 * 8
     assert _C.GsrInputs.footprint.offset == 40
     assert _C.GsrInputs.bg.offset == 48
+    # 6 pointers, then rotation_eps and three int32 (struct gsr_leaf_grads)
+    assert ctypes.sizeof(_C.GsrLeafGrads) == 6 * 8 + 16
+    assert _C.GsrLeafGrads.rotation_eps.offset == 48 and _C.GsrLeafGrads.dsh_planar.offset == 56
 
 
 def test_scratch_layouts_are_aligned_and_disjoint(lib):

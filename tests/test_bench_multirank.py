@@ -1,0 +1,45 @@
+"""bench.py's N > 1 path (the driver's multi-GPU scaling run, bench.py:main), rehearsed
+on one GPU: `torch.distributed.run --nproc-per-node N bench.py --gpus N` with the
+ranks sharing cuda:0 over gloo (GSR_DIST_BACKEND=gloo; the measured configuration is
+RCCL, one rank per GPU).  Each run is a fresh process tree; the JSON line rank 0
+prints must describe N views per step, the backend, and a finite whole-job rate —
+the barrier / max-over-ranks timing and value = N * steps / elapsed run exactly as
+in the scaling run."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("exchange", ["sh-colour", "allreduce"])
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_multirank_line(n, exchange):
+    env = dict(os.environ, GSR_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(n),
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--full-steps", "0", "--render-steps", "0",
+           "--footprint-steps", "0", "--grad-exchange", exchange]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    d = lines[0]
+    assert d["n_gpus"] == n and d["config"]["views_per_step"] == n
+    assert d["config"]["collective_backend"] == "gloo"
+    assert d["scaling"] == "weak" and d["steps"] == 3 and d["warmup"] == 1
+    assert d["value"] > 0 and d["value"] == pytest.approx(n * 3 / (d["ms_per_step"] * 3e-3), rel=1e-3)
+    assert ("all-gather" in d["config"]["parallelism"]) == (exchange == "sh-colour")

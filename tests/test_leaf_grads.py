@@ -1,0 +1,240 @@
+"""Fused leaf gradients (diff_gaussian_rasterization._leaf_plan): the backward writes
+the gradients of GaussianModel's leaves itself when the caller's activations are
+exactly the reference's (scene/gaussian_model.py:106-126: cat, exp, sigmoid,
+F.normalize) and nothing else observes them; every other graph keeps upstream's
+activation gradients.
+
+CPU: the graph matching and gating rules, driven by a stand-in autograd Function
+whose backward runs the same planner.  GPU: the fused leaf gradients against the
+plain path (set_fused_leaf_grads(False)) bit for bit at configs B and C, with
+fresh and accumulating .grad, two views per backward, and the Python branches."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import diff_gaussian_rasterization as dgr
+
+
+def _leaves(P=6, M=16, requires=True):
+    g = torch.Generator().manual_seed(0)
+    mk = lambda *s: torch.randn(*s, generator=g).requires_grad_(requires)  # noqa: E731
+    return dict(xyz=mk(P, 3), f_dc=mk(P, 1, 3), f_rest=mk(P, M - 1, 3), opacity=mk(P, 1), scaling=mk(P, 3),
+                rotation=mk(P, 4))
+
+
+class _Probe(torch.autograd.Function):
+    """Stands in for _RasterizeGaussians: its backward records the planner's answer."""
+    seen = []
+
+    @staticmethod
+    def forward(ctx, means3D, sh, opacities, scales, rotations):
+        ctx.save_for_backward(sh, scales, rotations)
+        ctx.opacities, ctx.means_shape = opacities, means3D.shape
+        return means3D.sum() + sh.sum() + opacities.sum() + scales.sum() + rotations.sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        sh, scales, rotations = ctx.saved_tensors
+        needs = (ctx.needs_input_grad[0], False, ctx.needs_input_grad[1], False, ctx.needs_input_grad[2],
+                 ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+        plan = dgr._leaf_plan(sh, torch.empty(0), ctx.opacities, scales, rotations, needs, False)
+        _Probe.seen.append({k: v[1] for k, v in plan.items()})
+        return (torch.zeros(ctx.means_shape),) + tuple(torch.zeros_like(x) for x in (sh, ctx.opacities, scales,
+                                                                                     rotations))
+
+
+def _activations(L, normalize=None):
+    sh = torch.cat((L["f_dc"], L["f_rest"]), dim=1)  # get_features
+    rot = F.normalize(L["rotation"]) if normalize is None else normalize(L["rotation"])
+    return L["xyz"], sh, torch.sigmoid(L["opacity"]), torch.exp(L["scaling"]), rot
+
+
+def _plan(L, run=lambda out: out.backward(), **kw):
+    _Probe.seen.clear()
+    acts = _activations(L, **kw)
+    out = _Probe.apply(*acts)
+    run(out)
+    return _Probe.seen[-1] if _Probe.seen else None
+
+
+ALL = {"sh": 0, "scales": 0, "opacities": 0, "rotations": 0}
+
+
+def test_reference_graph_is_fused():
+    assert _plan(_leaves()) == ALL
+    assert _plan(_leaves(M=1)) == ALL  # SH degree 0: an empty f_rest leaf
+
+
+def test_existing_grad_accumulates():
+    L = _leaves()
+    for k in L:
+        L[k].grad = torch.ones_like(L[k])
+    assert _plan(L) == {k: 1 for k in ALL}
+    L["f_rest"].grad = None  # the two SH leaves must agree
+    assert "sh" not in _plan(L)
+    L["scaling"].grad = torch.ones(6, 3).t().contiguous().t()  # not contiguous
+    assert "scales" not in _plan(L)
+
+
+def test_hooks_and_observers_keep_upstream_path():
+    L = _leaves()
+    L["scaling"].register_post_accumulate_grad_hook(lambda p: None)  # the exchange's all-reduce hooks
+    L["f_dc"].register_hook(lambda g: g)
+    assert _plan(L) == {"opacities": 0, "rotations": 0}
+    L = _leaves()
+    _Probe.seen.clear()
+    acts = list(_activations(L))
+    acts[2].retain_grad()
+    _Probe.apply(*acts).backward()
+    assert "opacities" not in _Probe.seen[-1]
+
+
+def test_other_graphs_keep_upstream_path():
+    hand = lambda r: r / r.norm(dim=1, keepdim=True)  # noqa: E731
+    assert "rotations" not in _plan(_leaves(), normalize=hand)
+    L = _leaves()
+    L["f_dc"].requires_grad_(False)
+    assert "sh" not in _plan(L)
+    L = _leaves()
+    assert _plan(L, run=lambda out: out.backward(inputs=[L["xyz"]])) == {}
+    assert _plan(L, run=lambda out: torch.autograd.grad(out, [L["rotation"]])) == {}
+    assert _plan(L, run=lambda out: out.backward(create_graph=True)) == {}
+
+
+def test_oracle_leaf_formulas_equal_torch_autograd():
+    """oracle.activation_leaf_grads (the arithmetic gsr_leaf_grads asks the library
+    for) equals torch's own CPU autograd of cat / exp / sigmoid / F.normalize bit for
+    bit."""
+    from oracle import oracle as o
+
+    P, g = 50_000, torch.Generator().manual_seed(0)
+    L = {k: v.detach().requires_grad_() for k, v in _leaves(P).items()}
+    L["rotation"].data[:7] *= 1e-3  # short quaternions
+    _, sh, op, sc, rot = _activations(L)
+    norm = rot.grad_fn.next_functions[1][0].next_functions[0][0].next_functions[0][0]._saved_result.detach().clone()
+    d = [torch.randn(t.shape, generator=g) for t in (sh, op, sc, rot)]
+    torch.autograd.backward([sh, op, sc, rot], d)
+    lg = o.activation_leaf_grads(d[0].numpy(), d[1].numpy(), d[2].numpy(), d[3].numpy(), op.detach().numpy(),
+                                 sc.detach().numpy(), rot.detach().numpy(), norm.numpy(),
+                                 sum_order="sequential")  # torch's CPU reduction (its GPU one pairs: the library's)
+    for name, leaf in (("dsh_dc", "f_dc"), ("dsh_rest", "f_rest"), ("dscaling", "scaling"), ("dopacity", "opacity"),
+                       ("drotation", "rotation")):
+        np.testing.assert_array_equal(lg[name], L[leaf].grad.numpy(), err_msg=name)
+
+
+def test_switch():
+    prev = dgr.set_fused_leaf_grads(False)
+    try:
+        assert dgr._fused_leaf_grads is False
+    finally:
+        dgr.set_fused_leaf_grads(prev)
+
+
+# ---------------------------------------------------------------- GPU: fused == plain
+def _isolated_scene(W=256, H=192, per_quadrant=3, seed=0):
+    """Small Gaussians (0.55 px after the 0.3 low-pass) whose means sit within 0.5 px
+    of an 8x8 quadrant's centre: each reaches one quadrant only, so its accumulator
+    row gets exactly one atomic and the backward is deterministic run to run (in
+    general the atomics' order varies and gradients differ in the last bits)."""
+    import synthetic
+
+    cam = synthetic.make_camera(W, H, view=1)
+    rng = np.random.default_rng(seed)
+    qx, qy = np.meshgrid(np.arange(W // 8), np.arange(H // 8))
+    q = np.stack([qx.ravel(), qy.ravel()], 1).repeat(per_quadrant, 0)
+    pix = q * 8 + 3.5 + rng.uniform(-0.5, 0.5, q.shape)
+    z = rng.uniform(4.0, 8.0, len(pix))
+    fx = W / (2 * np.tan(cam.FoVx / 2))
+    fy = H / (2 * np.tan(cam.FoVy / 2))
+    pc = np.stack([(pix[:, 0] - (W - 1) / 2) / fx * z, (pix[:, 1] - (H - 1) / 2) / fy * z, z, np.ones_like(z)], 1)
+    c2w = torch.linalg.inv(cam.world_view_transform.T.double()).numpy()
+    xyz = (pc @ c2w.T)[:, :3].astype(np.float32)
+    g = synthetic.make_gaussians(len(xyz), 3, seed=seed, scale_range=(0.0005, 0.001))
+    g.xyz = torch.from_numpy(xyz)
+    return cam, g
+
+
+def _run(cam, g, dev, dL, fused, views=1, pre_grad=False, python_branch=False):
+    import train_step
+
+    gd = g.to(dev, requires_grad=True)
+    if pre_grad:
+        for p in gd.params():
+            p.grad = torch.full_like(p, 0.25)
+    prev = dgr.set_fused_leaf_grads(fused)
+    try:
+        loss = 0
+        for v in range(views):
+            out = train_step.render(cam.to(dev), gd, torch.zeros(3, device=dev), scaling_modifier=1.0 + 0.1 * v,
+                                    convert_SHs_python=python_branch, compute_cov3D_python=python_branch)
+            loss = loss + (out["render"] * dL).sum()
+        loss.backward()
+        plan = dgr.last_leaf_plan
+    finally:
+        dgr.set_fused_leaf_grads(prev)
+    torch.cuda.synchronize()
+    return [p.grad.cpu() for p in gd.params()], out["viewspace_points"].grad.cpu(), plan
+
+
+NAMES = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
+FUSED = ("opacities", "rotations", "scales", "sh")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [{}, {"pre_grad": True}, {"views": 2}, {"python_branch": True}],
+                         ids=["fresh", "accumulate", "two_views", "python_branch"])
+def test_fused_leaf_grads_bit_identical(dev, kw):
+    """Deterministic scene: the fused leaf gradients equal the plain path's (torch's
+    cat / exp / sigmoid / normalize backwards + AccumulateGrad) bit for bit, for a
+    fresh .grad, an existing one, two views into one backward, and the Python branch
+    (only the opacity is a sigmoid leaf there)."""
+    from helpers import random_dL
+
+    cam, g = _isolated_scene()
+    dL = torch.from_numpy(random_dL(cam.image_height, cam.image_width)).to(dev) * 1e4
+    ref, ref_vs, plan0 = _run(cam, g, dev, dL, False, **kw)
+    ref2, _, _ = _run(cam, g, dev, dL, False, **kw)
+    got, got_vs, plan = _run(cam, g, dev, dL, True, **kw)
+    assert plan0 == () and plan == (("opacities",) if kw.get("python_branch") else FUSED)
+    from helpers import rel_l2
+
+    for name, a, b, b2 in zip(NAMES, got, ref, ref2):
+        np.testing.assert_array_equal(b.numpy(), b2.numpy(), err_msg=f"{name}: plain path not deterministic")
+        assert a.shape == b.shape and a.is_contiguous(), name
+        assert float(b.abs().max()) > 0, name
+        if name == "rotation" and kw.get("views", 1) > 1:
+            # two renders: autograd sums the four normalize-backward terms into the
+            # leaf in its own engine order, the fused path per render (ulp-level)
+            assert rel_l2(a.numpy(), b.numpy()) <= 1e-6
+            continue
+        np.testing.assert_array_equal(a.numpy(), b.numpy(), err_msg=name)
+    np.testing.assert_array_equal(got_vs.numpy(), ref_vs.numpy())
+
+
+def _compare_tol(W, H, P, dev):
+    """Full-size scenes: atomics reorder the accumulator sums run to run, so fused vs
+    plain is checked to rel-L2 1e-6 (the plain path against itself shows the same)."""
+    from helpers import case, random_dL, rel_l2
+
+    cam, g = case(P, W, H, 3, seed=2, view=1)
+    dL = torch.from_numpy(random_dL(H, W)).to(dev)
+    got, got_vs, plan = _run(cam, g, dev, dL, True)
+    ref, ref_vs, plan0 = _run(cam, g, dev, dL, False)
+    assert plan0 == () and plan == FUSED
+    for name, a, b in zip(NAMES, got, ref):
+        assert a.shape == b.shape and a.is_contiguous(), name
+        assert rel_l2(a.numpy(), b.numpy()) <= 1e-6, name
+    assert rel_l2(got_vs.numpy(), ref_vs.numpy()) <= 1e-6
+
+
+@pytest.mark.gpu
+def test_fused_leaf_grads_config_b(dev):
+    _compare_tol(800, 800, 100_000, dev)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+def test_fused_leaf_grads_config_c(dev):
+    _compare_tol(1920, 1080, 1_000_000, dev)

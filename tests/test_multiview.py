@@ -485,8 +485,13 @@ def _stats_worker(rank, world, port, out):
     acc = torch.rand(P, 1, generator=g)
     den = torch.randint(0, 3, (P, 1), generator=g).float()
     mx = torch.rand(P, generator=g) * 10
-    reduce_densification_stats(acc, den, mx)
-    out[rank] = (acc, den, mx)
+    loc = (acc.clone(), den.clone(), mx.clone())
+    red = reduce_densification_stats(acc, den, mx)
+    # copies: the per-rank accumulators are untouched, so a second call gives the same
+    assert all(torch.equal(a, b) for a, b in zip((acc, den, mx), loc))
+    again = reduce_densification_stats(acc, den, mx)
+    assert all(torch.equal(a, b) for a, b in zip(red, again))
+    out[rank] = red
     dist.destroy_process_group()
 
 
@@ -694,11 +699,10 @@ def _rccl_worker(rank, world, port, out):
             ar()
             ar.remove_hooks()
         stats = [torch.rand(30_000, 1, device=dev), torch.rand(30_000, 1, device=dev), torch.rand(30_000, device=dev)]
-        ref = [t.clone() for t in stats]
-        reduce_densification_stats(*stats, force=True)
+        red = reduce_densification_stats(*stats, force=True)
         torch.cuda.synchronize()
         res[mode] = ([p.grad.detach().cpu().clone() for p in params],
-                     all(torch.equal(a, b) for a, b in zip(stats, ref)))
+                     all(torch.equal(a, b) for a, b in zip(stats, red)))
     out[rank] = res
     dist.destroy_process_group()
 

@@ -57,7 +57,7 @@ class OracleC:
     def rasterize_gaussians_backward(self, bg, means3D, radii, colors, scales, rotations, scale_modifier,
                                      cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh,
                                      degree, campos, geomBuffer, R, binningBuffer, imageBuffer, debug,
-                                     dsh_planar=False):
+                                     dsh_planar=False, leaf=None, opacities=None):
         self.calls.append("bwd")
         f = self.states[int(geomBuffer[0])]
         assert R == f["num_rendered"]
@@ -67,6 +67,26 @@ class OracleC:
         if dsh_planar:  # the library's coefficient-plane layout: same values, strides (3, 3P, 1)
             i = NAMES.index("dsh")
             out[i] = out[i].permute(1, 0, 2).contiguous().permute(1, 0, 2)
+        self.last_leaf = None
+        if leaf is not None:  # gsr_leaf_grads: the leaves' gradients written in place of dsh/dopacity/dscales/drot
+            n = self._np
+            lg = self.o.activation_leaf_grads(b["dsh"], b["dopacity"], b["dscales"], b["drot"],
+                                              n(opacities) if opacities is not None else b["dopacity"],
+                                              n(scales) if scales.numel() else b["dscales"],
+                                              n(rotations) if rotations.numel() else b["drot"],
+                                              n(leaf.rotation_norm) if leaf.rotation_norm is not None
+                                              else np.ones(len(b["drot"]), np.float32), leaf.rotation_eps,
+                                              sum_order="sequential")  # as CPU torch adds (its GPU reduction pairs)
+            self.last_leaf = []
+            for name, bit, idx in (("dsh_dc", 1, "dsh"), ("dsh_rest", 1, "dsh"), ("dscaling", 2, "dscales"),
+                                   ("dopacity", 4, "dopacity"), ("drotation", 8, "drot")):
+                t = getattr(leaf, name)
+                if t is None:
+                    continue
+                v = torch.from_numpy(lg[name]).reshape(t.shape)
+                t.copy_(t + v if leaf.accumulate & bit else v)
+                out[NAMES.index(idx)] = None
+                self.last_leaf.append(name)
         return tuple(out)
 
     def mark_visible(self, means3D, viewmatrix, projmatrix):
@@ -159,6 +179,10 @@ def test_reference_render_through_drop_in(reference_render, branch):
     (img * dL).sum().backward()
     assert shim.calls == ["fwd", "bwd"]
     b = shim.last_grads
+    # the reference's own graph (get_features cat, exp, sigmoid, normalize) takes the
+    # fused leaf gradients (diff_gaussian_rasterization._leaf_plan)
+    assert shim.last_leaf == (["dsh_dc", "dsh_rest", "dscaling", "dopacity", "drotation"] if branch == "native"
+                              else ["dopacity"])
     # densification statistic input (train.py:127 -> gaussian_model.py:576-580)
     np.testing.assert_array_equal(out["viewspace_points"].grad.numpy(), b["dmeans2D"])
     vis = state["radii"] > 0
