@@ -231,7 +231,8 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     if (L.drotation && (!L.rotation_norm || !in->rotations))
         return fail(GSR_ERR_ARGS, "leaf drotation: needs rotations and rotation_norm");
     if (L.dopacity && !in->opacities) return fail(GSR_ERR_ARGS, "leaf dopacity: needs opacities");
-    if (!dmeans2D || !dcolors || (!dopacity && !L.dopacity) || !dmeans3D || !dcov3D)
+    if (!dmeans2D || (!dcolors && in->colors_precomp) || (!dopacity && !L.dopacity) || !dmeans3D ||
+        (!dcov3D && in->cov3D_precomp))
         return fail(GSR_ERR_ARGS, "backward outputs are NULL");
     if (in->sh && in->M > 0 && !dsh && !drgb && !L.dsh_dc) return fail(GSR_ERR_ARGS, "dsh is NULL");
     if (in->scales && ((!dscales && !L.dscaling) || (!drot && !L.drotation)))

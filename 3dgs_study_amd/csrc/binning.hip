@@ -42,10 +42,6 @@
 #include "gsr_math.hpp"
 #include "gsr_wave.hpp"
 
-#ifndef GSR_RANK_LDS
-#define GSR_RANK_LDS 0
-#endif
-
 namespace gsr {
 
 constexpr int RX_WAVES = RX_THREADS / 64;
@@ -258,12 +254,6 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     __shared__ uint32_t sfb[SEG], sst[SEG];
     // RXM_UNPACK stages the packed words alone (the value is in the word)
     __shared__ uint32_t stage_k[TILE_N], stage_v[MODE == RXM_UNPACK ? 1 : TILE_N];
-#if GSR_RANK_LDS
-    // per-wave peer masks: lane bits of the round's items, by digit (cleared by
-    // each digit group's first lane after the group has read its mask)
-    __shared__ unsigned long long pmask[RX_WAVES][RADIX];
-    for (int k = 0; k < RX_WAVES; k++) pmask[k][threadIdx.x] = 0ull;
-#endif
     if (pass_skipped(a)) return;
     // three-pass depth sort: the third pass is the last one
     const bool final3 = a.role == RX_DEPTH_THIRD && a.ctrl[CTRL_DSORT_PASSES] == 3;
@@ -303,19 +293,8 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         const uint64_t live = __ballot(ok);
         if (!live) break;
         const uint32_t d = (kk[r] >> a.shift) & a.dmask;
-#if GSR_RANK_LDS
-        // lanes of the round with this digit: one LDS atomic OR and one read per
-        // item instead of nbits ballots and their per-lane mask selects
-        if (ok) atomicOr(&pmask[w][d], 1ull << lane);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const uint64_t peers = ok ? pmask[w][d] : 0ull;
-        const uint32_t below = count_below(peers);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        if (ok && below == 0) pmask[w][d] = 0ull;  // in program order after every lane's read
-#else
         const uint64_t peers = match_digit(d, live, a.nbits);
         const uint32_t below = count_below(peers);
-#endif
         const uint32_t c = cnt[w][d];
         rk[r] = c + below;
         if (ok && below == 0) cnt[w][d] = c + (uint32_t)__popcll(peers);

@@ -116,12 +116,15 @@ __device__ __attribute__((noinline)) float exp_rn_f32(float x) {
     p = __builtin_fma(p, r, 1.0);
     return (float)__builtin_ldexp(p, (int)n);
 }
-// the exact power and G of a flagged pair (conic' = -conic/2 from the splat record)
+// the exact power and G of a flagged pair (conic' = -conic/2 from the splat record).
+// Upstream skips a positive power: G = 0 then gives alpha 0, which both blend
+// loops skip, so their fast paths need no `power > 0` select (every positive fast
+// power is flagged, and a fast power <= 0 stands for upstream's, see above).
 __device__ __forceinline__ void blend_fix(float &power, float &G, float dx, float dy, float ca, float cb, float cc) {
 #pragma clang fp contract(off)
     const float cx = -2.0f * ca, cy = -2.0f * cb, cz = -2.0f * cc;  // exact
     power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-    G = exp_rn_f32(power);
+    G = power > 0.0f ? 0.0f : exp_rn_f32(power);
 }
 
 // s_waitcnt vmcnt(4) expcnt(7) lgkmcnt(15): everything but the 4 youngest

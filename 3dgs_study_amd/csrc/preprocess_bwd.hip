@@ -342,20 +342,24 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
     if (!st.vis) {
         for (int k = 0; k < 3; k++) {
             o.dmeans2D[3 * (size_t)idx + k] = 0.f;
-            o.dcolors[3 * (size_t)idx + k] = 0.f;
             o.dmeans3D[3 * (size_t)idx + k] = 0.f;
         }
+        if (o.dcolors)
+            for (int k = 0; k < 3; k++) o.dcolors[3 * (size_t)idx + k] = 0.f;
         if (o.drgb)
             for (int k = 0; k < 3; k++) o.drgb[3 * (size_t)idx + k] = 0.f;
-        for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = 0.f;
+        if (o.dcov3D)
+            for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = 0.f;
         const float zs[3] = {0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
         write_activation_grads(a, idx, 0.f, opac, zs, zq, gin, has_sr);
         return st;  // dmeans3D (zero) and the dsh row are written by the caller
     }
     const float dcol[3] = {acc1.z, acc1.w, accb};
-    o.dcolors[3 * (size_t)idx + 0] = dcol[0];
-    o.dcolors[3 * (size_t)idx + 1] = dcol[1];
-    o.dcolors[3 * (size_t)idx + 2] = dcol[2];
+    if (o.dcolors) {  // NULL: no precomputed colours to differentiate (the caller discards it)
+        o.dcolors[3 * (size_t)idx + 0] = dcol[0];
+        o.dcolors[3 * (size_t)idx + 1] = dcol[1];
+        o.dcolors[3 * (size_t)idx + 2] = dcol[2];
+    }
 
     // ---- 3D covariance (recomputed exactly as the forward did)
     float c3[6];
@@ -445,7 +449,8 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
     const float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
                          (2 * h_y * t.y) * tz3 * dL_dJ12;
     f3 dmean = xform_vec4x3_transpose(f3{dL_dtx, dL_dty, dL_dtz}, V);
-    for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = dc3[k];
+    if (o.dcov3D)  // NULL: no precomputed cov3D to differentiate
+        for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = dc3[k];
 
     // ---- preprocessCUDA (backward.cu): 2D-mean gradient through the projection
     const f4 m_hom = xform_point4x4(mean, Pm);

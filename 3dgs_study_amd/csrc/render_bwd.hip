@@ -156,16 +156,16 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     struct Part {
         float g5, dx, dy, t;
     };
-    // One Gaussian of the replay (record r0..r3, list position k): power and G as
+    // One Gaussian of the replay (record r1..r3, list position k): power and G as
     // render_fwd.hip computes them (quad_power, the same instructions on the same
     // staged values, and the same exact re-check near the skip thresholds, done by
     // the caller), then upstream's back-to-front step, branch-free: a skipped pixel
     // sees alpha = 0 (T and D unchanged) and zero gradients.
-    auto replay = [&](float pw, float G, const float4 &r1, const float4 &r2, const float2 &r3, int lim) {
+    auto replay = [&](float G, const float4 &r1, const float4 &r2, const float2 &r3, int lim) {
         const float op = r1.z;
         const float alpha = fminf(0.99f, op * G);
         const int k = __float_as_int(r2.w);  // entry lo + k = upstream `contributor`
-        const bool valid = k < lim && !(pw > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const bool valid = k < lim && !(alpha < 1.0f / 255.0f);  // power > 0 arrives as G = 0 (blend_fix)
         const float av = valid ? alpha : 0.0f;
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
         T = T * inv_1ma;
@@ -271,8 +271,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             }
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
-            const Part qa = replay(pa, Ga, a1, a2, a3, lim);  // back to front: a before b
-            const Part qb = replay(pb, Gb, b1, b2, b3, two ? lim : 0);
+            const Part qa = replay(Ga, a1, a2, a3, lim);  // back to front: a before b
+            const Part qb = replay(Gb, b1, b2, b3, lim);   // !two: b is the zero record (alpha 0)
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.z));
             const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.z));
             reduce_emit(qa, qb, gida, gidb, two);

@@ -112,14 +112,14 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 // (selects on VGPRs only: the per-Gaussian SALU work of bool masks
                 // and exec juggling, one scalar unit per CU, bounded this loop).
                 // a = the alpha this pixel takes: 0 when upstream would skip the
-                // Gaussian (power > 0, alpha < 1/255, pixel finished: thr = 2) — a
+                // Gaussian (alpha < 1/255 — a positive power arrives as G = 0 —
+                // or pixel finished: thr = 2) — a
                 // zero alpha leaves T and C unchanged.  T >= 1e-4 holds for every
                 // live pixel, so the stop test can only fire for a > 0, exactly
                 // upstream's test.
 #pragma unroll
                 for (int g = 0; g < FWD_GROUP; g++) {
-                    float av = pw[g] > 0.0f ? 0.0f : al[g];
-                    av = al[g] < thr ? 0.0f : av;
+                    float av = al[g] < thr ? 0.0f : al[g];  // (a positive power left G = 0: blend_fix)
                     const float test_T = T * (1 - av);
                     const bool sat = test_T < 0.0001f;  // this Gaussian is not blended; the pixel stops
                     av = sat ? 0.0f : av;

@@ -356,6 +356,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         dopacity = None if leaf.dopacity is not None else dopacity
         dscales = None if leaf.dscaling is not None else dscales
         drot = None if leaf.drotation is not None else drot
+        # gradients of absent inputs: upstream's zeros, discarded by the autograd
+        # wrapper; not written at all here (36 B per Gaussian)
+        dcolors = None if keep["colors"] is None else dcolors
+        dcov3D = None if keep["cov3D_precomp"] is None else dcov3D
     if P == 0:
         return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
     accum = torch.empty((lib.gsr_accum_bytes(P),), dtype=torch.uint8, device=device)
@@ -374,8 +378,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         fn, last = lib.gsr_backward_leaves, _ptr(dsh)
     head = lambda: (ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),  # noqa: E731
                     binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
-                    int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), dcolors.data_ptr(),
-                    _ptr(dopacity), dmeans3D.data_ptr(), dcov3D.data_ptr(), last, _ptr(dscales), _ptr(drot))
+                    int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), _ptr(dcolors),
+                    _ptr(dopacity), dmeans3D.data_ptr(), _ptr(dcov3D), last, _ptr(dscales), _ptr(drot))
     call = lambda f: f(*head(), _stream(device))  # noqa: E731
     if leaf is not None:
         lg = leaf.struct(P, M, device, dsh_planar)

@@ -120,7 +120,9 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
 
 /* Replaces RasterizeGaussiansBackwardCUDA -> Rasterizer::backward.
  * Every output is fully written (no pre-zeroing needed); dsh may be NULL when
- * in->sh is NULL, dscales/drot may be NULL when in->scales is NULL.
+ * in->sh is NULL, dscales/drot may be NULL when in->scales is NULL, dcolors
+ * when in->colors_precomp is NULL and dcov3D when in->cov3D_precomp is NULL
+ * (upstream returns zeros there, which its autograd wrapper discards).
  * Shapes: dmeans2D [P,3], dcolors [P,3], dopacity [P,1], dmeans3D [P,3],
  * dcov3D [P,6], dsh [P,M,3], dscales [P,3], drot [P,4]. */
 int gsr_backward(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning, const void *img,
