@@ -158,6 +158,11 @@ int gsr_point_list_keys(int32_t P, int32_t W, int32_t H, const void *geom, const
 const char *gsr_last_error(void) { return g_err.c_str(); }
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 
+#ifndef GSR_BUILD_ID
+#define GSR_BUILD_ID "unknown"
+#endif
+const char *gsr_build_id(void) { return GSR_BUILD_ID; }
+
 static int ensure_pinned() {
     if (g_pinned) return GSR_OK;
     // coherent: the kernel's system-scope stores land in host memory directly

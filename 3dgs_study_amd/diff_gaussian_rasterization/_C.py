@@ -56,6 +56,7 @@ EXPORTED = (
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
+    "gsr_build_id",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -215,6 +216,7 @@ def load_library():
     lib.gsr_knn_mean_dist2.restype = ctypes.c_int
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_abi_version.restype = ctypes.c_int
+    lib.gsr_build_id.restype = ctypes.c_char_p
     if lib.gsr_abi_version() != ABI_VERSION:
         raise ImportError(f"{path}: ABI version {lib.gsr_abi_version()} != {ABI_VERSION}; rebuild")
     _lib = lib

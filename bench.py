@@ -347,6 +347,8 @@ def main():
                 "valu_issue_frac": pmc_stage(dom).get("valu_issue_frac"),
             },
             "cpu_baseline": None,
+            # SHA-256 of the sources the loaded libgsr.so was built from (tools/build_id.py)
+            "build_id": _C.load_library().gsr_build_id().decode(),
         }
         if world == 1 and args.footprint_steps > 0:
             line["footprint_" + ("tight" if _C.get_footprint() == "rect" else "rect")] = footprint_rates(

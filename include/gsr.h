@@ -325,6 +325,9 @@ int gsr_knn_mean_dist2(int32_t P, const float *points, float *dist2, void *scrat
 
 const char *gsr_last_error(void);
 int gsr_abi_version(void);
+/* SHA-256 (hex) of the sources the library was built from (tools/build_id.py):
+ * build provenance for tests and benchmark records.  Not upstream. */
+const char *gsr_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -175,3 +175,14 @@ def lib_point_list_keys_validates():
     assert lib.gsr_point_list_keys(10, 16, 16, None, None, 5, None, None) != 0
     assert "NULL" in lib.gsr_last_error().decode()
     return True
+
+
+def test_library_was_built_from_this_tree(lib):
+    """Build provenance: the shipped libgsr.so carries the SHA-256 of the sources it
+    was compiled from (Makefile -> gsr_build_id); it must be this tree's."""
+    import sys
+
+    sys.path.insert(0, str(ROOT / "tools"))
+    from build_id import build_id
+
+    assert lib.gsr_build_id().decode() == build_id(), "libgsr.so is stale: rebuild (make -C 3dgs_study_amd/csrc)"
