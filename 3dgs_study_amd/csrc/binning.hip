@@ -42,24 +42,33 @@
 #include "gsr_math.hpp"
 #include "gsr_wave.hpp"
 
+#include <type_traits>
+
 namespace gsr {
 
 constexpr int RX_WAVES = RX_THREADS / 64;
 static_assert(RX_THREADS == RADIX, "one thread per digit in the per-block digit loops");
 
-// Lanes of the wave whose digit equals this lane's (restricted to `live`);
-// only the pass's nbits significant digit bits are compared.
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t live, int nbits) {
-    uint64_t m = live;
+// Lanes of the wave whose digit equals this lane's (restricted to `live`),
+// comparing the NB low digit bits (the digit is masked, so comparing more bits
+// than the pass has is harmless).  Per bit: s = the sign-extended bit (0 or ~0,
+// one v_bfe_i32), one ballot of s, and per mask half m &= ~(ballot ^ s) as ONE
+// v_bitop3_b32 (truth table 0x90: m & (ballot == s)): 4 VALU per bit.  (A runtime
+// bit count with a per-lane select of ballot / ~ballot compiled to ~11.)
+__device__ __forceinline__ uint32_t and_xnor(uint32_t m, uint32_t bal, uint32_t s) {
+    return __builtin_amdgcn_bitop3_b32(m, bal, s, 0x90);  // the builtin: the compiler pads its hazards
+}
+template <int NB>
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t live) {
+    uint32_t lo = (uint32_t)live, hi = (uint32_t)(live >> 32);
 #pragma unroll
-    for (int b = 0; b < RADIX_BITS; b++) {
-        if (b < nbits) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(bit);
-            m &= bit ? bal : ~bal;
-        }
+    for (int b = 0; b < NB; b++) {
+        const uint32_t s = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);  // feeds the ballot too
+        const uint64_t bal = __ballot(s != 0u);
+        lo = and_xnor(lo, (uint32_t)bal, s);
+        hi = and_xnor(hi, (uint32_t)(bal >> 32), s);
     }
-    return m;
+    return ((uint64_t)hi << 32) | lo;
 }
 // number of set bits of m below this lane
 __device__ __forceinline__ uint32_t count_below(uint64_t m) {
@@ -247,8 +256,9 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
     constexpr int SEG = MODE == RXM_UNPACK ? RADIX + 1 : 1;
     __shared__ uint32_t cnt[RX_WAVES][RADIX];
-    __shared__ uint32_t lstart[RADIX];   // block-local start of each digit's run
-    __shared__ uint32_t gstart[RADIX];   // global start of this block's run of each digit
+    // global start of this block's run of each digit, minus the run's start in
+    // the block (so an item's output position is gshift[digit] + its block slot)
+    __shared__ uint32_t gshift[RADIX];
     __shared__ uint32_t dstart[SEG];     // RXM_UNPACK: global start of each digit
     __shared__ uint32_t wsum[RX_WAVES];
     __shared__ uint32_t sfb[SEG], sst[SEG];
@@ -280,26 +290,36 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         const uint32_t t = a.totals[threadIdx.x];
         uint32_t tot;
         const uint32_t inc = block_inclusive_scan<RX_THREADS>(t, wsum, &tot);
-        gstart[threadIdx.x] = inc - t + a.hist[(size_t)threadIdx.x * a.NB + blk];
+        gshift[threadIdx.x] = inc - t + a.hist[(size_t)threadIdx.x * a.NB + blk];
         if constexpr (MODE == RXM_UNPACK) dstart[threadIdx.x] = inc - t;
     }
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) cnt[k][threadIdx.x] = 0;
     __syncthreads();
-    // stable ranks inside each wave's quarter
+    // stable ranks inside each wave's quarter (the bit count as a compile-time
+    // constant: 6 / 7 / 8-bit passes, anything else compares 8)
+    auto rank_items = [&](auto nbits) {
+        constexpr int NB = decltype(nbits)::value;
 #pragma unroll
-    for (int r = 0; r < ITEMS; r++) {
-        const bool ok = base + 64u * r < span.y;
-        const uint64_t live = __ballot(ok);
-        if (!live) break;
-        const uint32_t d = (kk[r] >> a.shift) & a.dmask;
-        const uint64_t peers = match_digit(d, live, a.nbits);
-        const uint32_t below = count_below(peers);
-        const uint32_t c = cnt[w][d];
-        rk[r] = c + below;
-        if (ok && below == 0) cnt[w][d] = c + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    }
+        for (int r = 0; r < ITEMS; r++) {
+            const bool ok = base + 64u * r < span.y;
+            const uint64_t live = __ballot(ok);
+            if (!live) break;
+            const uint32_t d = (kk[r] >> a.shift) & a.dmask;
+            const uint64_t peers = match_digit<NB>(d, live);
+            const uint32_t below = count_below(peers);
+            const uint32_t c = cnt[w][d];
+            rk[r] = c + below;
+            if (ok && below == 0) cnt[w][d] = c + (uint32_t)__popcll(peers);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        }
+    };
+    if (a.nbits == 6)
+        rank_items(std::integral_constant<int, 6>{});
+    else if (a.nbits == 7)
+        rank_items(std::integral_constant<int, 7>{});
+    else
+        rank_items(std::integral_constant<int, RADIX_BITS>{});
     __syncthreads();
     {  // block-local digit runs, and each wave's start inside its digit's run
         uint32_t c[RX_WAVES], sum = 0;
@@ -310,7 +330,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         }
         uint32_t tot;
         const uint32_t start = block_inclusive_scan<RX_THREADS>(sum, wsum, &tot) - sum;
-        lstart[threadIdx.x] = start;
+        gshift[threadIdx.x] -= start;  // this thread's own digit
         uint32_t off = start;
 #pragma unroll
         for (int k = 0; k < RX_WAVES; k++) {
@@ -335,7 +355,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     for (uint32_t i = threadIdx.x; i < nb; i += RX_THREADS) {
         const uint32_t k = stage_k[i];
         const uint32_t d = (k >> a.shift) & a.dmask;
-        const uint32_t pos = gstart[d] + (i - lstart[d]);
+        const uint32_t pos = gshift[d] + i;
         if constexpr (MODE == RXM_UNPACK) {
             vout[pos] = k & ((1u << a.id_bits) - 1u);
         } else if constexpr (MODE == RXM_PACK) {
