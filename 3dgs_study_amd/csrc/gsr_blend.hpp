@@ -144,19 +144,21 @@ __device__ __forceinline__ void wait_vmcnt_4() { __builtin_amdgcn_s_waitcnt(0x0F
 // the mean itself, for the exact re-check (d = mean - pixel, one rounding, as
 // upstream) and the backward's d.
 //   rec[k][0] = {K6, K4, K5, K1}, rec[k][1] = {K2, K3, opacity, r},
-//   rec[k][2] = {g, b, id bits, lane},  rec[k][3] = {mean.x, mean.y, -, -}
+//   rec[k][2] = {g, b, id bits, tag},  rec[k][3] = {mean.x, mean.y, -, -}
+// with tag = the entry's list position + 1 (its n_contrib value) in render_fwd,
+// its lane (chunk offset) in render_bwd.
 // A zero record (opacity 0: alpha 0, never blended) pads an odd survivor count.
 struct QuadChunk {
     float4 rec[66][4];  // render_fwd: survivors 0..ns-1, zero at ns; render_bwd: zero at 0, survivors 1..ns
 };
 __device__ __forceinline__ void stage_quad(float4 *rec, const float4 &A, const float4 &B, const float4 &C, float qx0,
-                                           float qy0, int lane) {
+                                           float qy0, int tag) {
     const float u = A.x - qx0, v = A.y - qy0;  // exact for means near the quadrant
     const float ca = A.z, cb = A.w, cc = B.x;
     const float hu = fmaf(ca, u, cb * v), hv = fmaf(cb, u, cc * v);
     rec[0] = make_float4(fmaf(u, hu, v * hv), -2.0f * hu, -2.0f * hv, ca);
     rec[1] = make_float4(2.0f * cb, cc, B.y, B.z);
-    rec[2] = make_float4(B.w, C.x, C.y, __int_as_float(lane));
+    rec[2] = make_float4(B.w, C.x, C.y, __int_as_float(tag));
     rec[3] = make_float4(A.x, A.y, 0.0f, 0.0f);
 }
 __device__ __forceinline__ void stage_zero(float4 *rec, int lane) {

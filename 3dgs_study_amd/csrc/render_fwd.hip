@@ -34,6 +34,7 @@ struct RenderFwdArgs {
 };
 
 constexpr int FWD_GROUP = 2;  // Gaussians per blend iteration (the zero record after the survivors pads an odd count)
+static_assert(FWD_GROUP == 2, "the fast path below is written for pairs");
 
 // The survivors of a chunk are staged as QuadChunk records (gsr_blend.hpp): the
 // power is a quadratic in the lane's quadrant offset, five FMAs per pixel, the
@@ -71,7 +72,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
             const uint64_t mask = __ballot(rel);
-            if (rel) stage_quad(st.rec[survivor_slot(mask, 0)], A, B, C, (float)qx0, (float)qy0, lane);
+            if (rel) stage_quad(st.rec[survivor_slot(mask, 0)], A, B, C, (float)qx0, (float)qy0, pos + lane + 1);
             const int ns = __builtin_popcountll(mask);
             stage_zero(st.rec[ns], lane);
             work += ns;
@@ -108,29 +109,42 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 }
 #pragma unroll
                 for (int g = 0; g < FWD_GROUP; g++) al[g] = fminf(0.99f, op[g] * G[g]);
-                // upstream's front-to-back step without branches or lane-mask logic
-                // (selects on VGPRs only: the per-Gaussian SALU work of bool masks
-                // and exec juggling, one scalar unit per CU, bounded this loop).
                 // a = the alpha this pixel takes: 0 when upstream would skip the
-                // Gaussian (alpha < 1/255 — a positive power arrives as G = 0 —
-                // or pixel finished: thr = 2) — a
-                // zero alpha leaves T and C unchanged.  T >= 1e-4 holds for every
-                // live pixel, so the stop test can only fire for a > 0, exactly
-                // upstream's test.
-#pragma unroll
-                for (int g = 0; g < FWD_GROUP; g++) {
-                    float av = al[g] < thr ? 0.0f : al[g];  // (a positive power left G = 0: blend_fix)
-                    const float test_T = T * (1 - av);
-                    const bool sat = test_T < 0.0001f;  // this Gaussian is not blended; the pixel stops
-                    av = sat ? 0.0f : av;
-                    thr = sat ? 2.0f : thr;
-                    const float wgt = av * T;
-                    C0 += cr[g] * wgt;
-                    C1 += cg[g] * wgt;
-                    C2 += cb[g] * wgt;
-                    T = sat ? T : test_T;
-                    last = av > 0.0f ? (uint32_t)(pos + li[g] + 1) : last;
+                // Gaussian (alpha < 1/255 — a positive power arrives as G = 0 — or
+                // pixel finished: thr = 2); a zero alpha leaves T and C unchanged.
+                // Selects on VGPRs only: the per-Gaussian SALU work of bool masks and
+                // exec juggling, one scalar unit per CU, bounded this loop.
+                float a0 = al[0] < thr ? 0.0f : al[0];
+                float a1 = al[1] < thr ? 0.0f : al[1];
+                // Upstream's stop test: T (1 - a) < 1e-4 means that Gaussian is not
+                // blended and the pixel stops.  Both products are formed up front:
+                // T (1 - a0) (1 - a1), rounded step by step, is at most T (1 - a0) (a
+                // factor <= 1 never rounds a product up past its other factor), so
+                // the second test alone says whether either fires.  A finished pixel
+                // (thr = 2: a = 0) or one outside the image keeps T >= 1e-4 and never
+                // fires, so the rare branch runs at most once per stopping pixel; it
+                // only zeroes the alphas that upstream's step would not blend and
+                // picks the T that step leaves — the blend below is the same
+                // arithmetic in the same order either way.
+                float t0 = T * (1 - a0), t1 = t0 * (1 - a1);
+                if (__builtin_expect(__ballot(t1 < 0.0001f) != 0, 0)) {
+                    const bool s0 = t0 < 0.0001f, s1 = t1 < 0.0001f;  // s0 implies s1
+                    a0 = s0 ? 0.0f : a0;
+                    a1 = s1 ? 0.0f : a1;
+                    thr = s1 ? 2.0f : thr;
+                    t0 = s0 ? T : t0;
+                    t1 = s1 ? t0 : t1;
                 }
+                const float w0 = a0 * T, w1 = a1 * t0;
+                C0 += cr[0] * w0;
+                C1 += cg[0] * w0;
+                C2 += cb[0] * w0;
+                C0 += cr[1] * w1;
+                C1 += cg[1] * w1;
+                C2 += cb[1] * w1;
+                T = t1;
+                last = a0 > 0.0f ? (uint32_t)li[0] : last;  // the staged tag: list position + 1
+                last = a1 > 0.0f ? (uint32_t)li[1] : last;
                 if (!__any(thr < 1.0f)) return true;
             }
             return false;
