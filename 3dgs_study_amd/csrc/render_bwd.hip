@@ -156,20 +156,18 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     struct Part {
         float g5, dx, dy, t;
     };
-    // One Gaussian of the replay (record r1..r3, list position k): power and G as
+    // One Gaussian of the replay (colour r, records r2, r3, list position k): power, G and alpha as
     // render_fwd.hip computes them (quad_power, the same instructions on the same
     // staged values, and the same exact re-check near the skip thresholds, done by
     // the caller), then upstream's back-to-front step, branch-free: a skipped pixel
     // sees alpha = 0 (T and D unchanged) and zero gradients.
-    auto replay = [&](float G, const float4 &r1, const float4 &r2, const float2 &r3, int lim) {
-        const float op = r1.z;
-        const float alpha = fminf(0.99f, op * G);
+    auto replay = [&](float G, float alpha, float cr, const float4 &r2, const float2 &r3, int lim) {
         const int k = __float_as_int(r2.w);  // entry lo + k = upstream `contributor`
         const bool valid = k < lim && !(alpha < 1.0f / 255.0f);  // power > 0 arrives as G = 0 (blend_fix)
         const float av = valid ? alpha : 0.0f;
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
         T = T * inv_1ma;
-        const float cd = fmaf(r2.x, dpx1, r1.w * dpx0) + r2.y * dpx2;  // sum_c colour_c dL/dpix_c
+        const float cd = fmaf(r2.x, dpx1, cr * dpx0) + r2.y * dpx2;  // sum_c colour_c dL/dpix_c
         const float dot = cd - D;                                      // sum_c (colour_c - accum_rec_c) dL/dpix_c
         D = fmaf(av, dot, D);
         // dL/dalpha (upstream: sum_c (c - accum_rec) dL_dpix_c * T - T_final/(1-alpha) * bg.dL_dpix)
@@ -264,15 +262,24 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             boff -= 2 * (uint32_t)sizeof(st.rec[0]);
             float pa = quad_power(a0, a1, lx, ly), pb = quad_power(b0, b1, lx, ly);
             float Ga = __expf(pa), Gb = __expf(pb);
-            const bool na = blend_near(pa, a1.z * Ga), nb = blend_near(pb, b1.z * Gb);
+            // alpha = min(0.99, opacity G); the clamp cannot move a value into or out
+            // of the re-check band, so the band test takes the clamped value
+            float ala = fminf(0.99f, a1.z * Ga), alb = fminf(0.99f, b1.z * Gb);
+            const bool na = blend_near(pa, ala), nb = blend_near(pb, alb);
             if (__builtin_expect(__ballot(na || nb) != 0, 0)) {  // rare: exact skip decisions (gsr_blend.hpp)
-                if (na) blend_fix(pa, Ga, a3.x - fx, a3.y - fy, a0.w, 0.5f * a1.x, a1.y);
-                if (nb) blend_fix(pb, Gb, b3.x - fx, b3.y - fy, b0.w, 0.5f * b1.x, b1.y);
+                if (na) {
+                    blend_fix(pa, Ga, a3.x - fx, a3.y - fy, a0.w, 0.5f * a1.x, a1.y);
+                    ala = fminf(0.99f, a1.z * Ga);
+                }
+                if (nb) {
+                    blend_fix(pb, Gb, b3.x - fx, b3.y - fy, b0.w, 0.5f * b1.x, b1.y);
+                    alb = fminf(0.99f, b1.z * Gb);
+                }
             }
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
-            const Part qa = replay(Ga, a1, a2, a3, lim);  // back to front: a before b
-            const Part qb = replay(Gb, b1, b2, b3, lim);   // !two: b is the zero record (alpha 0)
+            const Part qa = replay(Ga, ala, a1.w, a2, a3, lim);  // back to front: a before b
+            const Part qb = replay(Gb, alb, b1.w, b2, b3, lim);   // !two: b is the zero record (alpha 0)
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.z));
             const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.z));
             reduce_emit(qa, qb, gida, gidb, two);

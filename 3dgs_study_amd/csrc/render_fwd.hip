@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 float pw[FWD_GROUP], al[FWD_GROUP], cr[FWD_GROUP], cg[FWD_GROUP], cb[FWD_GROUP];
                 float G[FWD_GROUP], op[FWD_GROUP];
                 int li[FWD_GROUP];
-                bool near = false;
+                bool near = false, all_done = false;
 #pragma unroll
                 for (int g = 0; g < FWD_GROUP; g++) {
                     const int kg = k + g;  // ns itself: the zero record
@@ -92,7 +92,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                     pw[g] = quad_power(r0, r1, lx, ly);
                     G[g] = __expf(pw[g]);
                     op[g] = r1.z;
-                    near = near || blend_near(pw[g], op[g] * G[g]);
+                    // the clamp cannot move a value into or out of the re-check band
+                    al[g] = fminf(0.99f, op[g] * G[g]);
+                    near = near || blend_near(pw[g], al[g]);
                     cr[g] = r1.w;
                     cg[g] = r2.x;
                     cb[g] = r2.y;
@@ -103,12 +105,12 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                         const int kg = k + g;
                         const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r3 = st.rec[kg][3];
                         // d = mean - pixel with upstream's single rounding
-                        if (blend_near(pw[g], op[g] * G[g]))
+                        if (blend_near(pw[g], al[g])) {
                             blend_fix(pw[g], G[g], r3.x - fpx, r3.y - fpy, r0.w, 0.5f * r1.x, r1.y);
+                            al[g] = fminf(0.99f, op[g] * G[g]);
+                        }
                     }
                 }
-#pragma unroll
-                for (int g = 0; g < FWD_GROUP; g++) al[g] = fminf(0.99f, op[g] * G[g]);
                 // a = the alpha this pixel takes: 0 when upstream would skip the
                 // Gaussian (alpha < 1/255 — a positive power arrives as G = 0 — or
                 // pixel finished: thr = 2); a zero alpha leaves T and C unchanged.
@@ -134,6 +136,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                     thr = s1 ? 2.0f : thr;
                     t0 = s0 ? T : t0;
                     t1 = s1 ? t0 : t1;
+                    all_done = !__any(thr < 1.0f);  // thr only changes here
                 }
                 const float w0 = a0 * T, w1 = a1 * t0;
                 C0 += cr[0] * w0;
@@ -145,7 +148,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 T = t1;
                 last = a0 > 0.0f ? (uint32_t)li[0] : last;  // the staged tag: list position + 1
                 last = a1 > 0.0f ? (uint32_t)li[1] : last;
-                if (!__any(thr < 1.0f)) return true;
+                if (all_done) return true;
             }
             return false;
         };
