@@ -33,8 +33,11 @@ struct RenderFwdArgs {
     int maxc;
 };
 
-constexpr int FWD_GROUP = 2;  // Gaussians per blend iteration (the zero record after the survivors pads an odd count)
-static_assert(FWD_GROUP == 2, "the fast path below is written for pairs");
+#ifndef GSR_FWD_GROUP
+#define GSR_FWD_GROUP 2
+#endif
+constexpr int FWD_GROUP = GSR_FWD_GROUP;  // Gaussians per blend iteration (zero records after the survivors pad the last group)
+static_assert(FWD_GROUP >= 1 && FWD_GROUP <= 3, "QuadChunk holds 64 survivors + 2 zero records");
 
 // The survivors of a chunk are staged as QuadChunk records (gsr_blend.hpp): the
 // power is a quadratic in the lane's quadrant offset, five FMAs per pixel, the
@@ -75,6 +78,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             if (rel) stage_quad(st.rec[survivor_slot(mask, 0)], A, B, C, (float)qx0, (float)qy0, pos + lane + 1);
             const int ns = __builtin_popcountll(mask);
             stage_zero(st.rec[ns], lane);
+            if (FWD_GROUP > 2) stage_zero(st.rec[ns + 1], lane);
             work += ns;
             // FWD_GROUP Gaussians per iteration: their LDS reads, powers and exps are
             // independent, so each wave has that much instruction-level parallelism
@@ -116,38 +120,41 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 // pixel finished: thr = 2); a zero alpha leaves T and C unchanged.
                 // Selects on VGPRs only: the per-Gaussian SALU work of bool masks and
                 // exec juggling, one scalar unit per CU, bounded this loop.
-                float a0 = al[0] < thr ? 0.0f : al[0];
-                float a1 = al[1] < thr ? 0.0f : al[1];
+                float av[FWD_GROUP], tt[FWD_GROUP];
+#pragma unroll
+                for (int g = 0; g < FWD_GROUP; g++) av[g] = al[g] < thr ? 0.0f : al[g];
                 // Upstream's stop test: T (1 - a) < 1e-4 means that Gaussian is not
-                // blended and the pixel stops.  Both products are formed up front:
-                // T (1 - a0) (1 - a1), rounded step by step, is at most T (1 - a0) (a
-                // factor <= 1 never rounds a product up past its other factor), so
-                // the second test alone says whether either fires.  A finished pixel
-                // (thr = 2: a = 0) or one outside the image keeps T >= 1e-4 and never
-                // fires, so the rare branch runs at most once per stopping pixel; it
-                // only zeroes the alphas that upstream's step would not blend and
-                // picks the T that step leaves — the blend below is the same
-                // arithmetic in the same order either way.
-                float t0 = T * (1 - a0), t1 = t0 * (1 - a1);
-                if (__builtin_expect(__ballot(t1 < 0.0001f) != 0, 0)) {
-                    const bool s0 = t0 < 0.0001f, s1 = t1 < 0.0001f;  // s0 implies s1
-                    a0 = s0 ? 0.0f : a0;
-                    a1 = s1 ? 0.0f : a1;
-                    thr = s1 ? 2.0f : thr;
-                    t0 = s0 ? T : t0;
-                    t1 = s1 ? t0 : t1;
+                // blended and the pixel stops.  All the group's products are formed up
+                // front: T (1 - a0) (1 - a1) ..., rounded step by step, never grows (a
+                // factor <= 1 never rounds a product up past its other factor), so the
+                // last test alone says whether any fires.  A finished pixel (thr = 2:
+                // a = 0) or one outside the image keeps T >= 1e-4 and never fires, so
+                // the rare branch runs at most once per stopping pixel; it only zeroes
+                // the alphas that upstream's step would not blend and picks the T each
+                // step leaves — the blend below is the same arithmetic in the same order
+                // either way.
+#pragma unroll
+                for (int g = 0; g < FWD_GROUP; g++) tt[g] = (g ? tt[g - 1] : T) * (1 - av[g]);
+                if (__builtin_expect(__ballot(tt[FWD_GROUP - 1] < 0.0001f) != 0, 0)) {
+#pragma unroll
+                    for (int g = 0; g < FWD_GROUP; g++) {
+                        const bool sg = tt[g] < 0.0001f;  // once one fires, the later ones do
+                        av[g] = sg ? 0.0f : av[g];
+                        tt[g] = sg ? (g ? tt[g - 1] : T) : tt[g];
+                        if (g == FWD_GROUP - 1) thr = sg ? 2.0f : thr;
+                    }
                     all_done = !__any(thr < 1.0f);  // thr only changes here
                 }
-                const float w0 = a0 * T, w1 = a1 * t0;
-                C0 += cr[0] * w0;
-                C1 += cg[0] * w0;
-                C2 += cb[0] * w0;
-                C0 += cr[1] * w1;
-                C1 += cg[1] * w1;
-                C2 += cb[1] * w1;
-                T = t1;
-                last = a0 > 0.0f ? (uint32_t)li[0] : last;  // the staged tag: list position + 1
-                last = a1 > 0.0f ? (uint32_t)li[1] : last;
+#pragma unroll
+                for (int g = 0; g < FWD_GROUP; g++) {
+                    const float w = av[g] * (g ? tt[g - 1] : T);
+                    C0 += cr[g] * w;
+                    C1 += cg[g] * w;
+                    C2 += cb[g] * w;
+                }
+                T = tt[FWD_GROUP - 1];
+#pragma unroll
+                for (int g = 0; g < FWD_GROUP; g++) last = av[g] > 0.0f ? (uint32_t)li[g] : last;  // tag: position + 1
                 if (all_done) return true;
             }
             return false;
