@@ -240,11 +240,11 @@ def _prep(t, name, device):
     """upstream `.contiguous()` + dtype/device checks; empty stays empty."""
     if t is None or t.numel() == 0:
         return None
-    if t.dtype != torch.float32:
+    if t.dtype is not torch.float32:
         raise TypeError(f"{name} must be float32 (got {t.dtype})")
     if t.device != device:
         raise RuntimeError(f"{name} is on {t.device}, expected {device}")
-    return t.contiguous()
+    return t if t.is_contiguous() else t.contiguous()
 
 
 def _stream(device):
@@ -284,6 +284,18 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
     ``footprint`` (keyword, not upstream): "rect" | "tight" for this call; None =
     the module setting (``set_footprint``, env GSR_FOOTPRINT, default "tight")."""
+    return _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                      viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                      prefiltered, debug, footprint)[:6]
+
+
+def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+               projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
+               footprint=None):
+    """rasterize_gaussians plus its validated inputs ``(struct, kept tensors, device,
+    M)``, which the autograd Function hands back to the backward (``inputs=``) so the
+    same tensors are not re-checked there: the host's backward path is on the
+    step's critical path once the GPU work is short."""
     lib = load_library()
     H, W = int(image_height), int(image_width)
     if footprint is not None and footprint not in FOOTPRINTS:
@@ -305,13 +317,13 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
                                   num_rendered.value, _ptr(radii), out_color.data_ptr(), stream),
            "rasterize_gaussians (render)")
-    return num_rendered.value, out_color, radii, geom, binning, img
+    return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M)
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                  viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
                                  geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None, dsh_planar=False,
-                                 on_drgb=None, leaf=None, opacities=None):
+                                 on_drgb=None, leaf=None, opacities=None, inputs=None):
     """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)
 
     Not upstream (keyword-only extensions; the defaults are upstream's behaviour):
@@ -329,44 +341,42 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     they replace (dsh, dopacity, dscales, drot).
     ``opacities`` — the forward's opacity input [P,1] (upstream's backward reads
     it from the geom buffer; passed here it is read coalesced); required with a
-    leaf opacity gradient."""
+    leaf opacity gradient.
+    ``inputs`` (private) — the forward's validated inputs (``_rasterize``): the
+    same tensors as the positional ones, not re-checked."""
     lib = load_library()
-    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
-    s, keep, device, M = _inputs(background, means3D, colors, opacities, scales, rotations, scale_modifier,
-                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos,
-                                 False, debug)
+    if inputs is None:
+        H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+        inputs = _inputs(background, means3D, colors, opacities, scales, rotations, scale_modifier, cov3D_precomp,
+                         viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
+    s, keep, device, M = inputs
     P = s.P
-    f32 = dict(dtype=torch.float32, device=device)
-    dmeans2D = torch.empty((P, 3), **f32)
-    dcolors = torch.empty((P, 3), **f32)
-    dopacity = torch.empty((P, 1), **f32)
-    dmeans3D = torch.empty((P, 3), **f32)
-    dcov3D = torch.empty((P, 6), **f32)
     if leaf is not None and drgb_out is not None:
         raise RuntimeError("rasterize_gaussians_backward: leaf and drgb_out are exclusive")
-    if leaf is not None and leaf.dsh_dc is not None:
-        dsh = None
-    elif drgb_out is not None:
+    f32 = dict(dtype=torch.float32, device=device)
+    empty = lambda *shape: torch.empty(shape, **f32)  # noqa: E731
+    # on the leaf path the gradients it replaces, and those of absent inputs
+    # (upstream's zeros, discarded by the autograd wrapper: 36 B per Gaussian), are
+    # neither allocated nor written
+    bare = leaf is not None
+    dmeans2D, dmeans3D = empty(P, 3), empty(P, 3)
+    dcolors = None if bare and keep["colors"] is None else empty(P, 3)
+    dcov3D = None if bare and keep["cov3D_precomp"] is None else empty(P, 6)
+    dopacity = None if bare and leaf.dopacity is not None else empty(P, 1)
+    dscales = None if bare and leaf.dscaling is not None else empty(P, 3)
+    drot = None if bare and leaf.drotation is not None else empty(P, 4)
+    if (bare and leaf.dsh_dc is not None) or drgb_out is not None:
         dsh = None
     elif dsh_planar:
-        dsh = torch.empty((M, P, 3), **f32).permute(1, 0, 2)
+        dsh = empty(M, P, 3).permute(1, 0, 2)
     else:
-        dsh = torch.empty((P, M, 3), **f32)
-    dscales = torch.empty((P, 3), **f32)
-    drot = torch.empty((P, 4), **f32)
-    if leaf is not None:
-        dopacity = None if leaf.dopacity is not None else dopacity
-        dscales = None if leaf.dscaling is not None else dscales
-        drot = None if leaf.drotation is not None else drot
-        # gradients of absent inputs: upstream's zeros, discarded by the autograd
-        # wrapper; not written at all here (36 B per Gaussian)
-        dcolors = None if keep["colors"] is None else dcolors
-        dcov3D = None if keep["cov3D_precomp"] is None else dcov3D
+        dsh = empty(P, M, 3)
     if P == 0:
         return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
     accum = torch.empty((lib.gsr_accum_bytes(P),), dtype=torch.uint8, device=device)
     grad = _prep(dL_dout_color, "dL_dout_color", device)
-    radii = radii.contiguous()
+    if not radii.is_contiguous():
+        radii = radii.contiguous()
     if drgb_out is not None:
         if (drgb_out.dtype != torch.float32 or drgb_out.device != device or not drgb_out.is_contiguous()
                 or drgb_out.numel() < 3 * P):

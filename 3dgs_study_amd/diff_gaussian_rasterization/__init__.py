@@ -85,15 +85,15 @@ def _acc_leaf(node):
 
 def _leaf_state(leaf, shape, device):
     """-1: not fusable; 0: no .grad yet (write it); 1: add into the existing .grad."""
-    if (leaf is None or not leaf.is_leaf or not leaf.requires_grad or leaf.dtype != torch.float32
-            or leaf.device != device or tuple(leaf.shape) != tuple(shape) or not leaf.is_contiguous()
+    if (leaf is None or not leaf.is_leaf or not leaf.requires_grad or leaf.dtype is not torch.float32
+            or leaf.device != device or leaf.shape != shape or not leaf.is_contiguous()
             or leaf._backward_hooks or getattr(leaf, "_post_accumulate_grad_hooks", None)):
         return -1
     g = leaf.grad
     if g is None:
         return 0
-    if (g.layout != torch.strided or g.dtype != torch.float32 or g.device != device
-            or tuple(g.shape) != tuple(shape) or not g.is_contiguous() or g.requires_grad):
+    if (g.layout != torch.strided or g.dtype is not torch.float32 or g.device != device
+            or g.shape != shape or not g.is_contiguous() or g.requires_grad):
         return -1
     return 1
 
@@ -120,31 +120,34 @@ def _leaf_plan(sh, colors_precomp, opacities, scales, rotations, needs, sink_tak
     try:
         if needs[2] and not sink_takes_sh and sh.numel() and colors_precomp.numel() == 0 and _plain_activation(sh):
             n = sh.grad_fn
-            if (type(n).__name__ == "CatBackward0" and n._saved_dim in (1, -2) and len(n.next_functions) == 2
-                    and sh.dim() == 3 and sh.shape[2] == 3):
+            nf = n.next_functions if type(n).__name__ == "CatBackward0" else ()
+            if len(nf) == 2 and n._saved_dim in (1, -2) and sh.dim() == 3 and sh.shape[2] == 3:
                 M = sh.shape[1]
-                dc, rest = _acc_leaf(n.next_functions[0][0]), _acc_leaf(n.next_functions[1][0])
+                dc, rest = _acc_leaf(nf[0][0]), _acc_leaf(nf[1][0])
                 a, b = _leaf_state(dc, (P, 1, 3), device), _leaf_state(rest, (P, M - 1, 3), device)
-                if a >= 0 and a == b and _will_run(n.next_functions[0][0]) and _will_run(n.next_functions[1][0]):
+                if a >= 0 and a == b and _will_run(nf[0][0]) and _will_run(nf[1][0]):
                     plan["sh"] = ((dc, rest), a, None)
         if needs[5] and scales.numel() and _plain_activation(scales):
             n = scales.grad_fn
             if type(n).__name__ == "ExpBackward0" and n._saved_result.data_ptr() == scales.data_ptr():
-                leaf = _acc_leaf(n.next_functions[0][0])
+                acc = n.next_functions[0][0]
+                leaf = _acc_leaf(acc)
                 st = _leaf_state(leaf, (P, 3), device)
-                if st >= 0 and _will_run(n.next_functions[0][0]):
+                if st >= 0 and _will_run(acc):
                     plan["scales"] = ((leaf,), st, None)
         if needs[4] and opacities.numel() and _plain_activation(opacities):
             n = opacities.grad_fn
             if type(n).__name__ == "SigmoidBackward0" and n._saved_result.data_ptr() == opacities.data_ptr():
-                leaf = _acc_leaf(n.next_functions[0][0])
+                acc = n.next_functions[0][0]
+                leaf = _acc_leaf(acc)
                 st = _leaf_state(leaf, (P, 1), device)
-                if st >= 0 and _will_run(n.next_functions[0][0]):
+                if st >= 0 and _will_run(acc):
                     plan["opacities"] = ((leaf,), st, None)
         if needs[6] and rotations.numel() and _plain_activation(rotations):
             d = rotations.grad_fn
-            if type(d).__name__ == "DivBackward0" and len(d.next_functions) == 2:
-                acc, e = d.next_functions[0][0], d.next_functions[1][0]
+            df = d.next_functions if type(d).__name__ == "DivBackward0" else ()
+            if len(df) == 2:
+                acc, e = df[0][0], df[1][0]
                 c = e.next_functions[0][0] if type(e).__name__ == "ExpandBackward0" else None
                 nrm = c.next_functions[0][0] if type(c).__name__ == "ClampMinBackward0" else None
                 if (type(nrm).__name__ == "LinalgVectorNormBackward0" and float(nrm._saved_ord) == 2.0
@@ -223,8 +226,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
                 rs.sh_degree, rs.campos, rs.prefiltered, rs.debug)
-        num_rendered, color, radii, geom, binning, img = _call_native(
-            _C.rasterize_gaussians, args, rs.debug, "snapshot_fw.dump", "forward")
+        num_rendered, color, radii, geom, binning, img, ctx.inputs = _call_native(
+            _C._rasterize, args, rs.debug, "snapshot_fw.dump", "forward")
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom, binning,
@@ -250,8 +253,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         if plan:
             leaf, fresh = _leaf_outputs(plan)
             (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
-                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True, leaf=leaf, opacities=ctx.opacities),
-                args, rs.debug, "snapshot_bw.dump", "backward")
+                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True, leaf=leaf, opacities=ctx.opacities,
+                                                           inputs=ctx.inputs), args, rs.debug, "snapshot_bw.dump",
+                "backward")
             for p, g in fresh:
                 p.grad = g
             return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
@@ -262,15 +266,16 @@ class _RasterizeGaussians(torch.autograd.Function):
             push = lambda: sink.push(rec, rs.campos, rs.sh_degree)  # noqa: E731
             (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
                 lambda *a: _C.rasterize_gaussians_backward(*a, drgb_out=rec[4:], on_drgb=push,
-                                                           opacities=ctx.opacities), args, rs.debug,
-                "snapshot_bw.dump", "backward")
+                                                           opacities=ctx.opacities, inputs=ctx.inputs), args,
+                rs.debug, "snapshot_bw.dump", "backward")
         else:
             # dsh as the [P,M,3] view of coefficient planes: the reference's SH cat
             # backward (get_features) then slices an f_dc gradient that already has
             # _features_dc's layout, and AccumulateGrad keeps it without a copy
             (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
-                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True, opacities=ctx.opacities), args,
-                rs.debug, "snapshot_bw.dump", "backward")
+                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True, opacities=ctx.opacities,
+                                                           inputs=ctx.inputs), args, rs.debug, "snapshot_bw.dump",
+                "backward")
         return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
 
 

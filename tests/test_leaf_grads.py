@@ -213,19 +213,25 @@ def test_fused_leaf_grads_bit_identical(dev, kw):
 
 
 def _compare_tol(W, H, P, dev):
-    """Full-size scenes: atomics reorder the accumulator sums run to run, so fused vs
-    plain is checked to rel-L2 1e-6 (the plain path against itself shows the same)."""
+    """Full-size scenes: the accumulator atomics reorder each Gaussian's sums run to
+    run, so the plain path does not repeat itself bit for bit either.  Fused vs plain
+    is held to that noise floor: rel-L2 within 4e-6 or 4x what two plain runs differ
+    by (measured ~1e-6 at config C for the rotation, whose normalize backward removes
+    the radial component and so cancels most of each gradient)."""
     from helpers import case, random_dL, rel_l2
 
     cam, g = case(P, W, H, 3, seed=2, view=1)
     dL = torch.from_numpy(random_dL(H, W)).to(dev)
     got, got_vs, plan = _run(cam, g, dev, dL, True)
     ref, ref_vs, plan0 = _run(cam, g, dev, dL, False)
+    ref2, _, _ = _run(cam, g, dev, dL, False)
     assert plan0 == () and plan == FUSED
-    for name, a, b in zip(NAMES, got, ref):
+    for name, a, b, b2 in zip(NAMES, got, ref, ref2):
         assert a.shape == b.shape and a.is_contiguous(), name
-        assert rel_l2(a.numpy(), b.numpy()) <= 1e-6, name
-    assert rel_l2(got_vs.numpy(), ref_vs.numpy()) <= 1e-6
+        noise = rel_l2(b2.numpy(), b.numpy())
+        assert noise <= 4e-6, name
+        assert rel_l2(a.numpy(), b.numpy()) <= max(4e-6, 4 * noise), name
+    assert rel_l2(got_vs.numpy(), ref_vs.numpy()) <= 4e-6
 
 
 @pytest.mark.gpu

@@ -41,15 +41,16 @@ def tick(name, t0):
 
 
 orig_pre, orig_render, orig_bwd = lib.gsr_forward_preprocess, lib.gsr_forward_render, lib.gsr_backward
+orig_leaves = lib.gsr_backward_leaves
 
 
 class Wrap:
     def __init__(self, f, name):
         self.f, self.name = f, name
 
-    def __call__(self, *a):
+    def __call__(self, *a, **kw):
         t0 = time.perf_counter()
-        r = self.f(*a)
+        r = self.f(*a, **kw)
         tick(self.name, t0)
         return r
 
@@ -57,6 +58,12 @@ class Wrap:
 lib.gsr_forward_preprocess = Wrap(orig_pre, "  ctypes gsr_forward_preprocess (incl. sync)")
 lib.gsr_forward_render = Wrap(orig_render, "  ctypes gsr_forward_render")
 lib.gsr_backward = Wrap(orig_bwd, "  ctypes gsr_backward")
+lib.gsr_backward_leaves = Wrap(orig_leaves, "  ctypes gsr_backward_leaves")
+import diff_gaussian_rasterization as dgr  # noqa: E402
+
+dgr._leaf_plan = Wrap(dgr._leaf_plan, " _leaf_plan")
+dgr._leaf_outputs = Wrap(dgr._leaf_outputs, " _leaf_outputs")
+_C._inputs = Wrap(_C._inputs, "  _C._inputs")
 orig_rg, orig_rgb = _C.rasterize_gaussians, _C.rasterize_gaussians_backward
 _C.rasterize_gaussians = Wrap(orig_rg, " _C.rasterize_gaussians")
 _C.rasterize_gaussians_backward = Wrap(orig_rgb, " _C.rasterize_gaussians_backward")
