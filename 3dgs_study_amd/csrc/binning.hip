@@ -101,6 +101,7 @@ struct RadixPass {
     // in blocks aligned to the first pass's digit runs (seg_totals: 2^seg_bits
     // segments, one low tile digit each) and fills the T tile ranges
     const uint32_t *seg_totals;
+    uint32_t *seg_table;   // [2][RADIX + 1]: RXM_PACK's block 0 writes it, RXM_UNPACK reads it
     int seg_bits;
     int id_bits;
     uint2 *ranges;
@@ -133,12 +134,31 @@ __device__ __forceinline__ uint32_t radix_block(int NB) {
     return x * q + min(x, r) + j;
 }
 
+// The second pass's segment table from the first pass's digit totals: segment
+// (low tile digit) s starts at block sfb[s] and item sst[s]; [RADIX] = the totals.
+// Written once, by the first pass's block 0 (its downsweep reads the totals
+// anyway), so the second pass's blocks load it instead of each scanning the totals.
+template <int TILE_N>
+__device__ __forceinline__ void write_seg_table(const RadixPass &a, uint32_t *wsum) {
+    const uint32_t c = (int)threadIdx.x < (1 << a.nbits) ? a.totals[threadIdx.x] : 0u;
+    const uint32_t nb = (c + (uint32_t)TILE_N - 1u) / (uint32_t)TILE_N;
+    uint32_t totb, totc;
+    const uint32_t ib = block_inclusive_scan<RX_THREADS>(nb, wsum, &totb);
+    const uint32_t ic = block_inclusive_scan<RX_THREADS>(c, wsum, &totc);
+    a.seg_table[threadIdx.x] = ib - nb;
+    a.seg_table[RADIX + 1 + threadIdx.x] = ic - c;
+    if (threadIdx.x == 0) {
+        a.seg_table[RADIX] = totb;
+        a.seg_table[2 * RADIX + 1] = totc;
+    }
+}
+
 // Items [x, y) of radix block blk.  Plain: TILE_N items per block.  RXM_UNPACK:
 // each segment (one digit run of the previous pass) starts a new block, so a
 // block's instances share their low tile digit and the digit counts per block
 // give the tile ranges; sfb / sst [RADIX + 1] (LDS) receive each segment's first
-// block and first item.  The grid has radix_blocks(n) + 2^seg_bits blocks, the
-// unused tail ones are empty.
+// block and first item (the table write_seg_table left).  The grid has
+// radix_blocks(n) + 2^seg_bits blocks, the unused tail ones are empty.
 template <int TILE_N, int MODE>
 __device__ __forceinline__ uint2 block_span(const RadixPass &a, uint32_t blk, uint32_t *sfb, uint32_t *sst,
                                             uint32_t *wsum) {
@@ -146,16 +166,12 @@ __device__ __forceinline__ uint2 block_span(const RadixPass &a, uint32_t blk, ui
         const uint32_t b0 = blk * (uint32_t)TILE_N;
         return make_uint2(b0, min(b0 + (uint32_t)TILE_N, a.n));
     } else {
-        const uint32_t c = (int)threadIdx.x < (1 << a.seg_bits) ? a.seg_totals[threadIdx.x] : 0u;
-        const uint32_t nb = (c + (uint32_t)TILE_N - 1u) / (uint32_t)TILE_N;
-        uint32_t totb, totc;
-        const uint32_t ib = block_inclusive_scan<RX_THREADS>(nb, wsum, &totb);
-        const uint32_t ic = block_inclusive_scan<RX_THREADS>(c, wsum, &totc);
-        sfb[threadIdx.x] = ib - nb;
-        sst[threadIdx.x] = ic - c;
+        (void)wsum;
+        sfb[threadIdx.x] = a.seg_table[threadIdx.x];
+        sst[threadIdx.x] = a.seg_table[RADIX + 1 + threadIdx.x];
         if (threadIdx.x == 0) {
-            sfb[RADIX] = totb;
-            sst[RADIX] = totc;
+            sfb[RADIX] = a.seg_table[RADIX];
+            sst[RADIX] = a.seg_table[2 * RADIX + 1];
         }
         __syncthreads();
         int sg = 0;  // the last segment whose first block is <= blk (sfb is non-decreasing, sfb[0] = 0)
@@ -293,6 +309,8 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         gshift[threadIdx.x] = inc - t + a.hist[(size_t)threadIdx.x * a.NB + blk];
         if constexpr (MODE == RXM_UNPACK) dstart[threadIdx.x] = inc - t;
     }
+    if constexpr (MODE == RXM_PACK)
+        if (blk == 0) write_seg_table<TILE_N>(a, wsum);
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) cnt[k][threadIdx.x] = 0;
     __syncthreads();
@@ -746,6 +764,7 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
         a.dmask = (1u << lo) - 1u;
         a.id_bits = 32 - hi;
         a.totals = at<uint32_t>(binning, B.totals1);
+        a.seg_table = at<uint32_t>(binning, B.seg_table);
         hipError_t e = items == TSORT_ITEMS_BIG ? radix_pass<TSORT_ITEMS_BIG, RXM_PACK>(a, s)
                                                 : radix_pass<TSORT_ITEMS, RXM_PACK>(a, s);
         if (e != hipSuccess) return e;

@@ -149,6 +149,7 @@ struct BinningLayout {
     size_t hist;    // uint32 [RADIX][radix_blocks(I, tsort_items(I)) + RADIX] (+ RADIX: segment-aligned blocks)
     size_t totals;  // uint32 [RADIX]
     size_t totals1; // uint32 [RADIX] the first tile pass's digit totals (the second pass's segments)
+    size_t seg_table; // uint32 [2][RADIX + 1] the second pass's segment table: first block, first item
     size_t bytes;
 };
 __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H) {
@@ -163,6 +164,7 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H)
     L.hist = take((size_t)RADIX * (radix_blocks((int64_t)n, tsort_items((int64_t)n)) + RADIX) * 4);
     L.totals = take((size_t)RADIX * 4);
     L.totals1 = take((size_t)RADIX * 4);
+    L.seg_table = take((size_t)2 * (RADIX + 1) * 4);
     L.bytes = o;
     return L;
 }
