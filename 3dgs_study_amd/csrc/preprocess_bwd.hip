@@ -153,12 +153,14 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
                                        uint32_t cl, const Mat4 &V, const Mat4 &Pm);
 
 // One workgroup = PB_THREADS consecutive Gaussians.  Each thread loads its own
-// inputs first and, at SH degree 3, its own 192-B SH row after them (12 x 16 B
-// into registers, in flight while the geometry backward — cov2D, projection,
-// cov3D — runs), turns the row into dL/dSH in place in registers and stores it
-// (row or coefficient-plane layout).  With no LDS stage the kernel runs 4 waves
-// per SIMD instead of 3 (112 -> 102 us at config C).  Other degrees stage the
-// workgroup's rows through LDS and stream them back out coalesced.
+// inputs first and, at SH degree 3, its own 192-B SH row once the geometry
+// backward — cov2D, projection, cov3D — is done (12 x 16 B into registers; issued
+// before the geometry, the row's 48 registers were held through it: 122 vs 117
+// VGPRs, and 118 vs 114 us at config C on one box), turns the row into dL/dSH in
+// place in registers and stores it (row or coefficient-plane layout).  With no
+// LDS stage the kernel runs 4 waves per SIMD instead of 3 (112 -> 102 us at config
+// C); forcing 5 or 6 spilled (160 us).  Other degrees stage the workgroup's rows
+// through LDS and stream them back out coalesced.
 template <int RWC>
 __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PB_THREADS][3M + 1]
@@ -200,7 +202,7 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const int32_t rad = a.radii[li];
     const uint32_t cl = a.clamped[li];
     float rowv[DIRECT ? 48 : 1];
-    if constexpr (DIRECT) {  // launched only with staged (stage == true), 16-B aligned SH rows
+    auto load_row = [&]() {  // launched only with staged (stage == true), 16-B aligned SH rows
         const float4 *r4 = reinterpret_cast<const float4 *>(in.sh + (size_t)li * 48);
 #pragma unroll
         for (int b = 0; b < 12; b++) {
@@ -210,15 +212,16 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
             rowv[4 * b + 2] = v.z;
             rowv[4 * b + 3] = v.w;
         }
-    } else if (stage) {
-        rows_to_lds<PB_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
-    }
+    };
+    if constexpr (!DIRECT)
+        if (stage) rows_to_lds<PB_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
     // pin the per-Gaussian loads ahead of the rows (the compiler would otherwise
     // sink them into the branch below, behind the rows, and wait for all of them)
     asm volatile("" ::"v"(acc0.x), "v"(acc0.y), "v"(acc0.z), "v"(acc0.w), "v"(acc1.x), "v"(acc1.y), "v"(acc1.z),
                  "v"(acc1.w), "v"(accb), "v"(opac), "v"(rad), "v"(cl));
     ShStage st{};
     if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, opac, rad, cl, V, Pm);
+    if constexpr (DIRECT) load_row();  // after the geometry: its registers are not held through it
     if (stage && !DIRECT) __syncthreads();
     if (live) {
         f3 dmean = st.dmean;
