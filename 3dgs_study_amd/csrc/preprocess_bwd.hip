@@ -221,7 +221,8 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
                  "v"(acc1.w), "v"(accb), "v"(opac), "v"(rad), "v"(cl));
     ShStage st{};
     if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, opac, rad, cl, V, Pm);
-    if constexpr (DIRECT) load_row();  // after the geometry: its registers are not held through it
+    if constexpr (DIRECT)  // after the geometry (its registers are not held through it); culled: zeros
+        if (live && st.vis) load_row();
     if (stage && !DIRECT) __syncthreads();
     if (live) {
         f3 dmean = st.dmean;
