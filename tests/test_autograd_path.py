@@ -102,3 +102,53 @@ def test_autograd_path_config_c(dev, oracle, python_branch):
 
     cam, g = case(1_000_000, 1920, 1080, 3, seed=0, view=0)
     _check(oracle, cam, g, dev, python_branch, mt=True)
+
+
+def test_noncontiguous_inputs_match_contiguous(dev):
+    """Inputs that are strided views (upstream's C++ glue calls .contiguous() on each)
+    give the same image and the same gradients as contiguous copies: the forward's
+    validated inputs, contiguous copies included, are what the backward reuses."""
+    import math
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from helpers import case, random_dL
+
+    cam, g = case(10_000, 256, 256, 3, seed=3, view=2)
+    camd = cam.to(dev)
+    dL = torch.from_numpy(random_dL(256, 256)).to(dev)
+    base = {n: t.detach().to(dev) for n, t in (("xyz", g.get_xyz), ("sh", g.get_features), ("op", g.get_opacity),
+                                              ("sc", g.get_scaling), ("rot", g.get_rotation))}
+    settings = GaussianRasterizationSettings(
+        image_height=256, image_width=256, tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5),
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=camd.world_view_transform,
+        projmatrix=camd.full_proj_transform, sh_degree=3, campos=camd.camera_center, prefiltered=False, debug=False)
+
+    def run(strided):
+        leaves, inputs = {}, {}
+        for n, t in base.items():
+            if strided:  # the same values as a view with a padded last dim (or a transposed layout for sh)
+                if n == "sh":
+                    wide = t.transpose(1, 2).contiguous().requires_grad_(True)
+                    leaves[n], inputs[n] = wide, wide.transpose(1, 2)
+                else:
+                    wide = torch.cat([t, torch.zeros_like(t[:, :1])], 1).requires_grad_(True)
+                    leaves[n], inputs[n] = wide, wide[:, :t.shape[1]]
+            else:
+                leaves[n] = inputs[n] = t.clone().requires_grad_(True)
+            assert inputs[n].is_contiguous() != strided, n
+        means2D = torch.zeros_like(inputs["xyz"], requires_grad=True)
+        img, radii = GaussianRasterizer(settings)(means3D=inputs["xyz"], means2D=means2D, opacities=inputs["op"],
+                                                  shs=inputs["sh"], scales=inputs["sc"], rotations=inputs["rot"])
+        (img * dL).sum().backward()
+        grads = {}
+        for n, t in base.items():
+            gr = leaves[n].grad
+            grads[n] = (gr.transpose(1, 2) if n == "sh" else gr[:, :t.shape[1]]) if strided else gr
+        return img.detach(), radii, grads, means2D.grad
+
+    img0, r0, g0, m0 = run(False)
+    img1, r1, g1, m1 = run(True)
+    assert torch.equal(img0, img1) and torch.equal(r0, r1)
+    for n in g0:  # accumulator atomics reorder sums run to run: rel-L2, not bits
+        assert rel_l2(g1[n].cpu().numpy(), g0[n].cpu().numpy()) <= 1e-5, n
+    assert rel_l2(m1.cpu().numpy(), m0.cpu().numpy()) <= 1e-5
