@@ -62,34 +62,26 @@ __device__ __forceinline__ bool quad_hit(float mx, float my, float ca, float cb,
 
 // power and G = exp(power) of one (pixel, Gaussian), for upstream's
 // `power > 0` skip and alpha = min(0.99, opacity * expf(power)) with its
-// `alpha < 1/255` skip.  The blend loops evaluate power as the quadrant-relative
-// quadratic of the staged record (quad_power, the same instructions in both
-// kernels) and exp in hardware (v_exp_f32 of power * log2 e): both within a few
-// ulp of upstream's float expression and the correctly rounded expf.  Where that could move a skip decision — alpha
-// within 2^-12 relative of 1/255 (the combined error is below 2^-16), or a
-// positive power (the conic is positive definite, so only rounding makes one)
-// — the pair is redone exactly as the CPU restatement does it (blend_fix):
-// upstream's expression in upstream's operation order without contraction,
-// and exp in double rounded once (the correctly rounded expf).  So every skip
-// decision, and with it n_contrib, matches the oracle's.  The loops test the
-// flags of both Gaussians of an iteration with ONE wave-uniform branch
-// (ballot), taken for ~1e-4 of the pairs: a per-lane branch around each
-// Gaussian cost render_fwd 20 % and render_bwd 7 % (exec-mask juggling that
-// broke the two Gaussians' interleaving); this form costs 15 % / 6 % (config C:
-// 132 -> 152 us, 247 -> 261 us; of that the positive-power test is 8 / 3 us and
-// the double-precision call ~0 / 3 us).  Both kernels flag from the same fast
-// power and G, so they re-check the same pairs and share every decision bit for
-// bit (a pair that only one of them re-checked could be skipped by one and
-// blended by the other, corrupting the backward's replay of that pixel).  The
-// positive-power test needs no band: upstream's float expression
-// -0.5 (a dx^2 + c dy^2) - b dx dy has the sign of the exact form (<= 0) unless
-// the conic's condition number exceeds ~2^21 (absolute rounding <= 4 ulp of
-// a dx^2 + c dy^2, the form >= that times 1/(2 kappa)) — a 2-D covariance
-// eigenvalue above ~6e5 px^2 given the 0.3 px^2 low-pass — so short of such a
-// conic a fast power <= 0 never hides an upstream skip.
-__device__ __forceinline__ bool blend_near(float power, float opacity_times_G) {
-    return power > 0.0f || fabsf(opacity_times_G * 255.0f - 1.0f) < 0x1p-12f;
-}
+// `alpha < 1/255` skip.  The blend loops evaluate power with upstream's own
+// expression in upstream's operation order, without contraction (exact_power,
+// the same instructions in both kernels and in the CPU restatement), so every
+// power — and with it every `power > 0` decision — is the oracle's bit for bit.
+// (Rounds 2-3 evaluated it as a quadrant-relative quadratic, five FMAs instead
+// of ten operations; for needle-like Gaussians, whose conic's terms cancel, that
+// differed from upstream's rounding by ~1e-3 and moved the image by 2e-3,
+// tests/test_gpu_parity.py::test_needle_gaussians.)  exp runs in hardware
+// (v_exp_f32 of power * log2 e), a few ulp from the correctly rounded expf; where
+// that could move the alpha decision — alpha within 2^-12 relative of 1/255 —
+// the pair takes the correctly rounded exp (blend_exact_G: exp in double,
+// rounded once), so n_contrib matches the oracle's.  The loops test the flags of
+// both Gaussians of an iteration with ONE wave-uniform branch (ballot), taken
+// for ~1e-4 of the pairs: a per-lane branch around each Gaussian cost render_fwd
+// 20 % and render_bwd 7 % (exec-mask juggling that broke the two Gaussians'
+// interleaving).  Both kernels flag from the same power and G, so they re-check
+// the same pairs and share every decision bit for bit (a pair that only one of
+// them re-checked could be skipped by one and blended by the other, corrupting
+// the backward's replay of that pixel).
+__device__ __forceinline__ bool blend_near(float alpha) { return fabsf(alpha * 255.0f - 1.0f) < 0x1p-12f; }
 // exp(x) for |x| <= 16 in double, Taylor to degree 13 on |r| <= ln2/2
 // (truncation < 2^-55 relative), rounded once to float (equal to the correctly
 // rounded exp for every float in [-16, 1]).  Not inlined: the rarely taken
@@ -116,15 +108,24 @@ __device__ __attribute__((noinline)) float exp_rn_f32(float x) {
     p = __builtin_fma(p, r, 1.0);
     return (float)__builtin_ldexp(p, (int)n);
 }
-// the exact power and G of a flagged pair (conic' = -conic/2 from the splat record).
-// Upstream skips a positive power: G = 0 then gives alpha 0, which both blend
-// loops skip, so their fast paths need no `power > 0` select (every positive fast
-// power is flagged, and a fast power <= 0 stands for upstream's, see above).
-__device__ __forceinline__ void blend_fix(float &power, float &G, float dx, float dy, float ca, float cb, float cc) {
+
+// upstream's power of the staged record r0 = {mean, c'a, c'c}, r1.x = 2 c'b
+// (conic' = -conic/2, exact) at pixel (fx, fy): d = mean - pixel (one rounding
+// each, as upstream subtracts), then -1/2 (a dx dx + c dy dy) - b dx dy, which
+// with the exactly scaled conic' reads (c'a dx) dx + (c'c dy) dy + (2c'b dx) dy:
+// every product and sum rounds exactly as upstream's does (scaling by a power
+// of two commutes with rounding).  The backward reuses d.
+__device__ __forceinline__ float exact_power(const float4 &r0, const float4 &r1, float fx, float fy, float &dx,
+                                             float &dy) {
 #pragma clang fp contract(off)
-    const float cx = -2.0f * ca, cy = -2.0f * cb, cz = -2.0f * cc;  // exact
-    power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-    G = power > 0.0f ? 0.0f : exp_rn_f32(power);
+    dx = r0.x - fx;
+    dy = r0.y - fy;
+    return ((r0.z * dx) * dx + (r0.w * dy) * dy) + (r1.x * dx) * dy;
+}
+// alpha = min(0.99, opacity G), 0 for upstream's `power > 0` skip (both skip
+// tests then read alpha < 1/255)
+__device__ __forceinline__ float blend_alpha(float power, float opacity, float G) {
+    return power > 0.0f ? 0.0f : fminf(0.99f, opacity * G);
 }
 
 // s_waitcnt vmcnt(4) expcnt(7) lgkmcnt(15): everything but the 4 youngest
@@ -135,40 +136,22 @@ __device__ __forceinline__ void wait_vmcnt_4() { __builtin_amdgcn_s_waitcnt(0x0F
 // Per-wave LDS image of a chunk's surviving Gaussians, shared by the forward and
 // the backward (so both evaluate the power with the same instructions on the same
 // values: their fast skip decisions, and with them their exact re-checks, agree bit
-// for bit).  Each record carries the power as a quadratic in the pixel's offset
-// (x, y) in 0..7 from the quadrant's first pixel:
-//   p(x, y) = K6 + K4 x + K5 y + K1 x^2 + K2 x y + K3 y^2
-// (conic' = -conic/2, centre offset (u, v) = mean - quadrant origin: K1 = c'a,
-// K2 = 2 c'b, K3 = c'c, K4 = -2 (c'a u + c'b v), K5 = -2 (c'b u + c'c v),
-// K6 = p(0, 0)) — five FMAs per pixel instead of the eight of d^T conic' d — and
-// the mean itself, for the exact re-check (d = mean - pixel, one rounding, as
-// upstream) and the backward's d.
-//   rec[k][0] = {K6, K4, K5, K1}, rec[k][1] = {K2, K3, opacity, r},
-//   rec[k][2] = {g, b, id bits, tag},  rec[k][3] = {mean.x, mean.y, -, -}
+// for bit):
+//   rec[k][0] = {mean.x, mean.y, c'a, c'c}, rec[k][1] = {2 c'b, -, opacity, r},
+//   rec[k][2] = {g, b, id bits, tag}
 // with tag = the entry's list position + 1 (its n_contrib value) in render_fwd,
 // its lane (chunk offset) in render_bwd.
 // A zero record (opacity 0: alpha 0, never blended) pads an odd survivor count.
 struct QuadChunk {
-    float4 rec[66][4];  // render_fwd: survivors 0..ns-1, zero at ns; render_bwd: zero at 0, survivors 1..ns
+    float4 rec[66][3];  // render_fwd: survivors 0..ns-1, zero at ns; render_bwd: zero at 0, survivors 1..ns
 };
-__device__ __forceinline__ void stage_quad(float4 *rec, const float4 &A, const float4 &B, const float4 &C, float qx0,
-                                           float qy0, int tag) {
-    const float u = A.x - qx0, v = A.y - qy0;  // exact for means near the quadrant
-    const float ca = A.z, cb = A.w, cc = B.x;
-    const float hu = fmaf(ca, u, cb * v), hv = fmaf(cb, u, cc * v);
-    rec[0] = make_float4(fmaf(u, hu, v * hv), -2.0f * hu, -2.0f * hv, ca);
-    rec[1] = make_float4(2.0f * cb, cc, B.y, B.z);
+__device__ __forceinline__ void stage_quad(float4 *rec, const float4 &A, const float4 &B, const float4 &C, int tag) {
+    rec[0] = make_float4(A.x, A.y, A.z, B.x);
+    rec[1] = make_float4(2.0f * A.w, 0.0f, B.y, B.z);
     rec[2] = make_float4(B.w, C.x, C.y, __int_as_float(tag));
-    rec[3] = make_float4(A.x, A.y, 0.0f, 0.0f);
 }
 __device__ __forceinline__ void stage_zero(float4 *rec, int lane) {
-    if (lane < 4) rec[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
-// the fast power of record (r0, r1) at quadrant offset (lx, ly): render_fwd and
-// render_bwd use exactly this sequence
-__device__ __forceinline__ float quad_power(const float4 &r0, const float4 &r1, float lx, float ly) {
-    const float t1 = fmaf(r1.x, ly, fmaf(r0.w, lx, r0.y)), t2 = fmaf(r1.y, ly, r0.z);
-    return fmaf(t2, ly, fmaf(t1, lx, r0.x));
+    if (lane < 3) rec[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 // compacted slot of a surviving lane: first + survivors in lower lanes
 __device__ __forceinline__ int survivor_slot(uint64_t mask, int first) {

@@ -80,11 +80,6 @@ __device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
     const f32x4 v = *p;
     return make_float4(v.x, v.y, v.z, v.w);
 }
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float2 ld2(const volatile char *p) {  // the record's mean: 8 of its last 16 B
-    const f32x2 v = *(__attribute__((address_space(3))) const volatile f32x2 *)p;
-    return make_float2(v.x, v.y);
-}
 
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(6))) render_bwd_kernel(RenderBwdArgs a) {
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
@@ -98,7 +93,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float fx = (float)px, fy = (float)py;
-    const float lx = (float)(lane & 7), ly = (float)(lane >> 3);  // offset in the quadrant (quad_power)
     const uint2 r = a.ranges[tile];
 
     const size_t HW = (size_t)a.W * a.H;
@@ -156,14 +150,15 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     struct Part {
         float g5, dx, dy, t;
     };
-    // One Gaussian of the replay (colour r, records r2, r3, list position k): power, G and alpha as
-    // render_fwd.hip computes them (quad_power, the same instructions on the same
-    // staged values, and the same exact re-check near the skip thresholds, done by
-    // the caller), then upstream's back-to-front step, branch-free: a skipped pixel
-    // sees alpha = 0 (T and D unchanged) and zero gradients.
-    auto replay = [&](float G, float alpha, float cr, const float4 &r2, const float2 &r3, int lim) {
+    // One Gaussian of the replay (colour r, record r2, list position k, d = mean -
+    // pixel): power, G and alpha as render_fwd.hip computes them (exact_power, the
+    // same instructions on the same staged values, and the same exact re-check near
+    // the alpha threshold, done by the caller), then upstream's back-to-front step,
+    // branch-free: a skipped pixel sees alpha = 0 (T and D unchanged) and zero
+    // gradients.
+    auto replay = [&](float G, float alpha, float cr, const float4 &r2, float dx, float dy, int lim) {
         const int k = __float_as_int(r2.w);  // entry lo + k = upstream `contributor`
-        const bool valid = k < lim && !(alpha < 1.0f / 255.0f);  // power > 0 arrives as G = 0 (blend_fix)
+        const bool valid = k < lim && !(alpha < 1.0f / 255.0f);  // power > 0 arrives as alpha 0 (blend_alpha)
         const float av = valid ? alpha : 0.0f;
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
         T = T * inv_1ma;
@@ -180,8 +175,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         // positive-definite conic), so an invalid pixel's zero dL/dalpha zeroes them.
         Part p;
         p.g5 = G * dL_dalpha;
-        p.dx = r3.x - fx;
-        p.dy = r3.y - fy;
+        p.dx = dx;
+        p.dy = dy;
         p.t = av * T;  // dchannel/dcolor
         return p;
     };
@@ -244,7 +239,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     auto replay_chunk = [&](int lo, float4 A, float4 B, float4 C) {
         const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         const uint64_t mask = __ballot(rel);
-        if (rel) stage_quad(st.rec[survivor_slot(mask, 1)], A, B, C, (float)qx0, (float)qy0, lane);
+        if (rel) stage_quad(st.rec[survivor_slot(mask, 1)], A, B, C, lane);
         const int ns = __builtin_popcountll(mask);
         const int lim = last_contrib - lo;  // entry lo + l replays for this pixel iff l < lim
         // byte offset of record b = k - 1 + 1 in a VGPR (asm barrier: keep it there)
@@ -257,29 +252,28 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             // the records into 8-B pieces around the unused fields)
             lds_f32x4 *rb = (lds_f32x4 *)(sbase + boff);
             const float4 b0 = ld4(rb + 0), b1 = ld4(rb + 1), b2 = ld4(rb + 2);
-            const float4 a0 = ld4(rb + 4), a1 = ld4(rb + 5), a2 = ld4(rb + 6);
-            const float2 b3 = ld2(sbase + boff + 48), a3 = ld2(sbase + boff + 112);
+            const float4 a0 = ld4(rb + 3), a1 = ld4(rb + 4), a2 = ld4(rb + 5);
             boff -= 2 * (uint32_t)sizeof(st.rec[0]);
-            float pa = quad_power(a0, a1, lx, ly), pb = quad_power(b0, b1, lx, ly);
+            float dxa, dya, dxb, dyb;
+            const float pa = exact_power(a0, a1, fx, fy, dxa, dya), pb = exact_power(b0, b1, fx, fy, dxb, dyb);
             float Ga = __expf(pa), Gb = __expf(pb);
-            // alpha = min(0.99, opacity G); the clamp cannot move a value into or out
-            // of the re-check band, so the band test takes the clamped value
-            float ala = fminf(0.99f, a1.z * Ga), alb = fminf(0.99f, b1.z * Gb);
-            const bool na = blend_near(pa, ala), nb = blend_near(pb, alb);
-            if (__builtin_expect(__ballot(na || nb) != 0, 0)) {  // rare: exact skip decisions (gsr_blend.hpp)
-                if (na) {
-                    blend_fix(pa, Ga, a3.x - fx, a3.y - fy, a0.w, 0.5f * a1.x, a1.y);
-                    ala = fminf(0.99f, a1.z * Ga);
+            // (the clamp cannot move a value into or out of the re-check band)
+            float ala = blend_alpha(pa, a1.z, Ga), alb = blend_alpha(pb, b1.z, Gb);
+            if (__builtin_expect(__ballot(blend_near(ala) || blend_near(alb)) != 0, 0)) {
+                // rare: the correctly rounded exp near 1/255 (gsr_blend.hpp)
+                if (blend_near(ala)) {
+                    Ga = exp_rn_f32(pa);
+                    ala = blend_alpha(pa, a1.z, Ga);
                 }
-                if (nb) {
-                    blend_fix(pb, Gb, b3.x - fx, b3.y - fy, b0.w, 0.5f * b1.x, b1.y);
-                    alb = fminf(0.99f, b1.z * Gb);
+                if (blend_near(alb)) {
+                    Gb = exp_rn_f32(pb);
+                    alb = blend_alpha(pb, b1.z, Gb);
                 }
             }
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
-            const Part qa = replay(Ga, ala, a1.w, a2, a3, lim);  // back to front: a before b
-            const Part qb = replay(Gb, alb, b1.w, b2, b3, lim);   // !two: b is the zero record (alpha 0)
+            const Part qa = replay(Ga, ala, a1.w, a2, dxa, dya, lim);  // back to front: a before b
+            const Part qb = replay(Gb, alb, b1.w, b2, dxb, dyb, lim);   // !two: b is the zero record (alpha 0)
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.z));
             const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.z));
             reduce_emit(qa, qb, gida, gidb, two);

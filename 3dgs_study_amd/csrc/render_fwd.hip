@@ -40,12 +40,10 @@ constexpr int FWD_GROUP = GSR_FWD_GROUP;  // Gaussians per blend iteration (zero
 static_assert(FWD_GROUP >= 1 && FWD_GROUP <= 3, "QuadChunk holds 64 survivors + 2 zero records");
 
 // The survivors of a chunk are staged as QuadChunk records (gsr_blend.hpp): the
-// power is a quadratic in the lane's quadrant offset, five FMAs per pixel, the
-// same instructions render_bwd uses.  The zero record after the survivors lets
-// the odd count's second Gaussian blend nothing without a mask (render_fwd
-// 145 -> 142 us at C, 374-379 -> 370 us at E).  It takes 66 VGPRs: 7 waves per
-// SIMD (forced to 8, the compiler spilled 4 VGPRs to scratch, 1-2 us slower and
-// +20 % traffic).  Three or four Gaussians per iteration spilled.
+// power is upstream's expression in upstream's order (exact_power), the same
+// instructions render_bwd uses.  The zero record after the survivors lets the
+// odd count's second Gaussian blend nothing without a mask (render_fwd 145 ->
+// 142 us at C, 374-379 -> 370 us at E).
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(7))) render_fwd_kernel(RenderFwdArgs a) {
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
@@ -54,7 +52,6 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
-    const float lx = (float)(lane & 7), ly = (float)(lane >> 3);  // offset in the quadrant
     const float fpx = (float)px, fpy = (float)py;
     const uint2 r = a.ranges[tile];
     const int n = (int)(r.y - r.x);
@@ -75,7 +72,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
             const uint64_t mask = __ballot(rel);
-            if (rel) stage_quad(st.rec[survivor_slot(mask, 0)], A, B, C, (float)qx0, (float)qy0, pos + lane + 1);
+            if (rel) stage_quad(st.rec[survivor_slot(mask, 0)], A, B, C, pos + lane + 1);
             const int ns = __builtin_popcountll(mask);
             stage_zero(st.rec[ns], lane);
             if (FWD_GROUP > 2) stage_zero(st.rec[ns + 1], lane);
@@ -84,8 +81,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             // independent, so each wave has that much instruction-level parallelism
             // to cover LDS and transcendental latency; only the T recurrence is serial.
             for (int k = 0; k < ns; k += FWD_GROUP) {
-                float pw[FWD_GROUP], al[FWD_GROUP], cr[FWD_GROUP], cg[FWD_GROUP], cb[FWD_GROUP];
-                float G[FWD_GROUP], op[FWD_GROUP];
+                float pw[FWD_GROUP], al[FWD_GROUP], cr[FWD_GROUP], cg[FWD_GROUP], cb[FWD_GROUP], op[FWD_GROUP];
                 int li[FWD_GROUP];
                 bool near = false, all_done = false;
 #pragma unroll
@@ -93,30 +89,23 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                     const int kg = k + g;  // ns itself: the zero record
                     const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r2 = st.rec[kg][2];
                     li[g] = __float_as_int(r2.w);
-                    pw[g] = quad_power(r0, r1, lx, ly);
-                    G[g] = __expf(pw[g]);
+                    float dx, dy;
+                    pw[g] = exact_power(r0, r1, fpx, fpy, dx, dy);
                     op[g] = r1.z;
-                    // the clamp cannot move a value into or out of the re-check band
-                    al[g] = fminf(0.99f, op[g] * G[g]);
-                    near = near || blend_near(pw[g], al[g]);
+                    al[g] = blend_alpha(pw[g], op[g], __expf(pw[g]));
+                    // (the clamp cannot move a value into or out of the re-check band)
+                    near = near || blend_near(al[g]);
                     cr[g] = r1.w;
                     cg[g] = r2.x;
                     cb[g] = r2.y;
                 }
-                if (__builtin_expect(__ballot(near) != 0, 0)) {  // rare: exact skip decisions (gsr_blend.hpp)
+                if (__builtin_expect(__ballot(near) != 0, 0)) {  // rare: the correctly rounded exp (gsr_blend.hpp)
 #pragma unroll
-                    for (int g = 0; g < FWD_GROUP; g++) {
-                        const int kg = k + g;
-                        const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r3 = st.rec[kg][3];
-                        // d = mean - pixel with upstream's single rounding
-                        if (blend_near(pw[g], al[g])) {
-                            blend_fix(pw[g], G[g], r3.x - fpx, r3.y - fpy, r0.w, 0.5f * r1.x, r1.y);
-                            al[g] = fminf(0.99f, op[g] * G[g]);
-                        }
-                    }
+                    for (int g = 0; g < FWD_GROUP; g++)
+                        if (blend_near(al[g])) al[g] = blend_alpha(pw[g], op[g], exp_rn_f32(pw[g]));
                 }
                 // a = the alpha this pixel takes: 0 when upstream would skip the
-                // Gaussian (alpha < 1/255 — a positive power arrives as G = 0 — or
+                // Gaussian (alpha < 1/255 — a positive power arrives as alpha 0 — or
                 // pixel finished: thr = 2); a zero alpha leaves T and C unchanged.
                 // Selects on VGPRs only: the per-Gaussian SALU work of bool masks and
                 // exec juggling, one scalar unit per CU, bounded this loop.
