@@ -122,11 +122,6 @@ __device__ __forceinline__ float exact_power(const float4 &r0, const float4 &r1,
     dy = r0.y - fy;
     return ((r0.z * dx) * dx + (r0.w * dy) * dy) + (r1.x * dx) * dy;
 }
-// alpha = min(0.99, opacity G), 0 for upstream's `power > 0` skip (both skip
-// tests then read alpha < 1/255)
-__device__ __forceinline__ float blend_alpha(float power, float opacity, float G) {
-    return power > 0.0f ? 0.0f : fminf(0.99f, opacity * G);
-}
 
 // s_waitcnt vmcnt(4) expcnt(7) lgkmcnt(15): everything but the 4 youngest
 // vector-memory ops (the chunk prefetch) has completed.  Issued as the builtin so

@@ -156,9 +156,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // the alpha threshold, done by the caller), then upstream's back-to-front step,
     // branch-free: a skipped pixel sees alpha = 0 (T and D unchanged) and zero
     // gradients.
-    auto replay = [&](float G, float alpha, float cr, const float4 &r2, float dx, float dy, int lim) {
+    auto replay = [&](float power, float G, float alpha, float cr, const float4 &r2, float dx, float dy, int lim) {
         const int k = __float_as_int(r2.w);  // entry lo + k = upstream `contributor`
-        const bool valid = k < lim && !(alpha < 1.0f / 255.0f);  // power > 0 arrives as alpha 0 (blend_alpha)
+        const bool valid = k < lim && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
         const float av = valid ? alpha : 0.0f;
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
         T = T * inv_1ma;
@@ -257,23 +257,24 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             float dxa, dya, dxb, dyb;
             const float pa = exact_power(a0, a1, fx, fy, dxa, dya), pb = exact_power(b0, b1, fx, fy, dxb, dyb);
             float Ga = __expf(pa), Gb = __expf(pb);
-            // (the clamp cannot move a value into or out of the re-check band)
-            float ala = blend_alpha(pa, a1.z, Ga), alb = blend_alpha(pb, b1.z, Gb);
+            // alpha before upstream's `power > 0` skip, which the replay applies (the
+            // clamp cannot move a value into or out of the re-check band)
+            float ala = fminf(0.99f, a1.z * Ga), alb = fminf(0.99f, b1.z * Gb);
             if (__builtin_expect(__ballot(blend_near(ala) || blend_near(alb)) != 0, 0)) {
                 // rare: the correctly rounded exp near 1/255 (gsr_blend.hpp)
                 if (blend_near(ala)) {
                     Ga = exp_rn_f32(pa);
-                    ala = blend_alpha(pa, a1.z, Ga);
+                    ala = fminf(0.99f, a1.z * Ga);
                 }
                 if (blend_near(alb)) {
                     Gb = exp_rn_f32(pb);
-                    alb = blend_alpha(pb, b1.z, Gb);
+                    alb = fminf(0.99f, b1.z * Gb);
                 }
             }
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
-            const Part qa = replay(Ga, ala, a1.w, a2, dxa, dya, lim);  // back to front: a before b
-            const Part qb = replay(Gb, alb, b1.w, b2, dxb, dyb, lim);   // !two: b is the zero record (alpha 0)
+            const Part qa = replay(pa, Ga, ala, a1.w, a2, dxa, dya, lim);  // back to front: a before b
+            const Part qb = replay(pb, Gb, alb, b1.w, b2, dxb, dyb, lim);   // !two: b is the zero record (alpha 0)
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.z));
             const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.z));
             reduce_emit(qa, qb, gida, gidb, two);

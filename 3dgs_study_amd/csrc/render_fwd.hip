@@ -92,8 +92,10 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                     float dx, dy;
                     pw[g] = exact_power(r0, r1, fpx, fpy, dx, dy);
                     op[g] = r1.z;
-                    al[g] = blend_alpha(pw[g], op[g], __expf(pw[g]));
-                    // (the clamp cannot move a value into or out of the re-check band)
+                    // alpha before upstream's `power > 0` skip, which the step below
+                    // applies with the alpha skip (the clamp cannot move a value into
+                    // or out of the re-check band)
+                    al[g] = fminf(0.99f, op[g] * __expf(pw[g]));
                     near = near || blend_near(al[g]);
                     cr[g] = r1.w;
                     cg[g] = r2.x;
@@ -102,16 +104,16 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
                 if (__builtin_expect(__ballot(near) != 0, 0)) {  // rare: the correctly rounded exp (gsr_blend.hpp)
 #pragma unroll
                     for (int g = 0; g < FWD_GROUP; g++)
-                        if (blend_near(al[g])) al[g] = blend_alpha(pw[g], op[g], exp_rn_f32(pw[g]));
+                        if (blend_near(al[g])) al[g] = fminf(0.99f, op[g] * exp_rn_f32(pw[g]));
                 }
                 // a = the alpha this pixel takes: 0 when upstream would skip the
-                // Gaussian (alpha < 1/255 — a positive power arrives as alpha 0 — or
-                // pixel finished: thr = 2); a zero alpha leaves T and C unchanged.
+                // Gaussian (power > 0 or alpha < 1/255, or the pixel finished: thr =
+                // 2); a zero alpha leaves T and C unchanged.
                 // Selects on VGPRs only: the per-Gaussian SALU work of bool masks and
                 // exec juggling, one scalar unit per CU, bounded this loop.
                 float av[FWD_GROUP], tt[FWD_GROUP];
 #pragma unroll
-                for (int g = 0; g < FWD_GROUP; g++) av[g] = al[g] < thr ? 0.0f : al[g];
+                for (int g = 0; g < FWD_GROUP; g++) av[g] = (al[g] < thr || pw[g] > 0.0f) ? 0.0f : al[g];
                 // Upstream's stop test: T (1 - a) < 1e-4 means that Gaussian is not
                 // blended and the pixel stops.  All the group's products are formed up
                 // front: T (1 - a0) (1 - a1) ..., rounded step by step, never grows (a
