@@ -132,8 +132,9 @@ __device__ __forceinline__ void wait_vmcnt_4() { __builtin_amdgcn_s_waitcnt(0x0F
 // the backward (so both evaluate the power with the same instructions on the same
 // values: their fast skip decisions, and with them their exact re-checks, agree bit
 // for bit):
-//   rec[k][0] = {mean.x, mean.y, c'a, c'c}, rec[k][1] = {2 c'b, -, opacity, r},
-//   rec[k][2] = {g, b, id bits, tag}
+//   rec[k][0] = {mean.x, mean.y, c'a, c'c}, rec[k][1] = {2 c'b, opacity, r, g},
+//   rec[k][2] = {b, tag, id bits, -}
+// (the forward reads 40 of the 48 B: two ds_read_b128 and a ds_read_b64)
 // with tag = the entry's list position + 1 (its n_contrib value) in render_fwd,
 // its lane (chunk offset) in render_bwd.
 // A zero record (opacity 0: alpha 0, never blended) pads an odd survivor count.
@@ -142,12 +143,28 @@ struct QuadChunk {
 };
 __device__ __forceinline__ void stage_quad(float4 *rec, const float4 &A, const float4 &B, const float4 &C, int tag) {
     rec[0] = make_float4(A.x, A.y, A.z, B.x);
-    rec[1] = make_float4(2.0f * A.w, 0.0f, B.y, B.z);
-    rec[2] = make_float4(B.w, C.x, C.y, __int_as_float(tag));
+    rec[1] = make_float4(2.0f * A.w, B.y, B.z, B.w);
+    rec[2] = make_float4(C.x, __int_as_float(tag), C.y, 0.0f);
 }
 __device__ __forceinline__ void stage_zero(float4 *rec, int lane) {
     if (lane < 3) rec[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
+// Whole-record LDS reads (volatile: the load vectorizer would otherwise split the
+// records around unused fields, or merge two 8-B reads into one ds_read2_b64,
+// which costs twice the LDS cycles of two ds_read_b64).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const volatile f32x4 lds_f32x4;
+typedef __attribute__((address_space(3))) const volatile f32x2 lds_f32x2;
+__device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
+    const f32x4 v = *p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float2 ld2(lds_f32x2 *p) {
+    const f32x2 v = *p;
+    return make_float2(v.x, v.y);
+}
+
 // compacted slot of a surviving lane: first + survivors in lower lanes
 __device__ __forceinline__ int survivor_slot(uint64_t mask, int first) {
     return first + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));

@@ -74,12 +74,6 @@ __device__ __forceinline__ float swz_fold(float c) {
     return c + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, c), 0x1F | (K << 10)));
 }
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) const volatile f32x4 lds_f32x4;
-__device__ __forceinline__ float4 ld4(lds_f32x4 *p) {
-    const f32x4 v = *p;
-    return make_float4(v.x, v.y, v.z, v.w);
-}
 
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(6))) render_bwd_kernel(RenderBwdArgs a) {
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
@@ -150,19 +144,20 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     struct Part {
         float g5, dx, dy, t;
     };
-    // One Gaussian of the replay (colour r, record r2, list position k, d = mean -
+    // One Gaussian of the replay (colour r, g, record r2, list position k, d = mean -
     // pixel): power, G and alpha as render_fwd.hip computes them (exact_power, the
     // same instructions on the same staged values, and the same exact re-check near
     // the alpha threshold, done by the caller), then upstream's back-to-front step,
     // branch-free: a skipped pixel sees alpha = 0 (T and D unchanged) and zero
     // gradients.
-    auto replay = [&](float power, float G, float alpha, float cr, const float4 &r2, float dx, float dy, int lim) {
-        const int k = __float_as_int(r2.w);  // entry lo + k = upstream `contributor`
+    auto replay = [&](float power, float G, float alpha, float cr, float cg, const float4 &r2, float dx, float dy,
+                      int lim) {
+        const int k = __float_as_int(r2.y);  // entry lo + k = upstream `contributor`
         const bool valid = k < lim && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
         const float av = valid ? alpha : 0.0f;
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
         T = T * inv_1ma;
-        const float cd = fmaf(r2.x, dpx1, cr * dpx0) + r2.y * dpx2;  // sum_c colour_c dL/dpix_c
+        const float cd = fmaf(cg, dpx1, cr * dpx0) + r2.x * dpx2;  // sum_c colour_c dL/dpix_c
         const float dot = cd - D;                                      // sum_c (colour_c - accum_rec_c) dL/dpix_c
         D = fmaf(av, dot, D);
         // dL/dalpha (upstream: sum_c (c - accum_rec) dL_dpix_c * T - T_final/(1-alpha) * bg.dL_dpix)
@@ -259,22 +254,22 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             float Ga = __expf(pa), Gb = __expf(pb);
             // alpha before upstream's `power > 0` skip, which the replay applies (the
             // clamp cannot move a value into or out of the re-check band)
-            float ala = fminf(0.99f, a1.z * Ga), alb = fminf(0.99f, b1.z * Gb);
+            float ala = fminf(0.99f, a1.y * Ga), alb = fminf(0.99f, b1.y * Gb);
             if (__builtin_expect(__ballot(blend_near(ala) || blend_near(alb)) != 0, 0)) {
                 // rare: the correctly rounded exp near 1/255 (gsr_blend.hpp)
                 if (blend_near(ala)) {
                     Ga = exp_rn_f32(pa);
-                    ala = fminf(0.99f, a1.z * Ga);
+                    ala = fminf(0.99f, a1.y * Ga);
                 }
                 if (blend_near(alb)) {
                     Gb = exp_rn_f32(pb);
-                    alb = fminf(0.99f, b1.z * Gb);
+                    alb = fminf(0.99f, b1.y * Gb);
                 }
             }
             // (no early-out for pairs without a contributing pixel: 98.6% of the
             // walked pairs have one at config C, the test cost more than it saved)
-            const Part qa = replay(pa, Ga, ala, a1.w, a2, dxa, dya, lim);  // back to front: a before b
-            const Part qb = replay(pb, Gb, alb, b1.w, b2, dxb, dyb, lim);   // !two: b is the zero record (alpha 0)
+            const Part qa = replay(pa, Ga, ala, a1.z, a1.w, a2, dxa, dya, lim);  // back to front: a before b
+            const Part qb = replay(pb, Gb, alb, b1.z, b1.w, b2, dxb, dyb, lim);   // !two: b is the zero record (alpha 0)
             const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.z));
             const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.z));
             reduce_emit(qa, qb, gida, gidb, two);

@@ -87,19 +87,21 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
 #pragma unroll
                 for (int g = 0; g < FWD_GROUP; g++) {
                     const int kg = k + g;  // ns itself: the zero record
-                    const float4 r0 = st.rec[kg][0], r1 = st.rec[kg][1], r2 = st.rec[kg][2];
-                    li[g] = __float_as_int(r2.w);
+                    lds_f32x4 *rp = (lds_f32x4 *)&st.rec[kg][0];
+                    const float4 r0 = ld4(rp), r1 = ld4(rp + 1);
+                    const float2 r2 = ld2((lds_f32x2 *)(rp + 2));  // {b, tag}: 8 of the record's last 16 B
+                    li[g] = __float_as_int(r2.y);
                     float dx, dy;
                     pw[g] = exact_power(r0, r1, fpx, fpy, dx, dy);
-                    op[g] = r1.z;
+                    op[g] = r1.y;
                     // alpha before upstream's `power > 0` skip, which the step below
                     // applies with the alpha skip (the clamp cannot move a value into
                     // or out of the re-check band)
                     al[g] = fminf(0.99f, op[g] * __expf(pw[g]));
                     near = near || blend_near(al[g]);
-                    cr[g] = r1.w;
-                    cg[g] = r2.x;
-                    cb[g] = r2.y;
+                    cr[g] = r1.z;
+                    cg[g] = r1.w;
+                    cb[g] = r2.x;
                 }
                 if (__builtin_expect(__ballot(near) != 0, 0)) {  // rare: the correctly rounded exp (gsr_blend.hpp)
 #pragma unroll
