@@ -222,7 +222,7 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
                          float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
                          float *drgb, float *dscales, float *drot, void *stream, int dsh_planar = 0,
                          int phases = 3, const gsr_leaf_grads *leaf = nullptr) {
-    // phases: bit 0 = accumulator memset + render_bwd (+ the colour gradient into
+    // phases: bit 0 = accumulator zeroing + render_bwd (+ the colour gradient into
     // drgb), bit 1 = preprocess_bwd.  The view-parallel exchange runs them as two
     // calls and starts its all-gather of drgb in between.
     if (int rc = validate(in, false)) return rc;
@@ -247,7 +247,10 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     float *acc = (float *)accum;
     const bool colors = drgb && in->sh && in->M > 0;
     if (phases & 1) {
-        if (int rc = check_hip(hipMemsetAsync(acc, 0, gsr_accum_bytes(in->P), s), "accumulator memset")) return rc;
+        // zeroes the accumulator and files the quadrants for render_bwd's wave order
+        if (int rc = step(launch_bwd_prepare(*in, const_cast<void *>(geom), img, acc, num_rendered > 0, s),
+                          "backward prepare", dbg, s))
+            return rc;
         if (num_rendered > 0) {
             if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, num_rendered, img, dL_dout_color, acc, s); }),
                               "render backward", dbg, s))

@@ -210,14 +210,14 @@ __host__ inline int blend_grid(int tiles) {
     return BLEND_WAVES == 4 ? xcd_grid(tiles) : xcd_grid<4 * XCD_STRIP>(4 * tiles);
 }
 
-// ---- backward wave order (render_fwd.hip fills it, render_bwd.hip reads it)
+// ---- backward wave order (render_fwd.hip buckets it, render_bwd.hip files and reads it)
 // The backward starts each XCD's heaviest quadrants first.  A quadrant keeps the
 // XCD of the forward's strip order (xcd_tile: strips of ORDER_STRIP quadrants
 // dealt round-robin over the 8 XCDs), so each L2 sees the same neighbouring
-// tiles in both passes.  Each forward wave files its quadrant under
-// (XCD, work bucket) with one atomic; backward workgroup 8 r + x (XCD x under
-// round-robin placement: a speed hint only) takes XCD x's r-th entry in
-// bucket order.
+// tiles in both passes.  Each forward wave stores its quadrant's work bucket;
+// the backward's first launch (bwd_prepare_kernel) files the quadrants under
+// (XCD, work bucket); backward workgroup 8 r + x (XCD x under round-robin
+// placement: a speed hint only) takes XCD x's r-th entry in bucket order.
 constexpr int ORDER_STRIP = 4 * XCD_STRIP;  // quadrants per strip
 constexpr int ORDER_NBUCKET = 32;           // work buckets per XCD, heaviest first
 __host__ __device__ inline int quad_xcd(int q) { return (q / ORDER_STRIP) & 7; }

@@ -111,7 +111,7 @@ struct GeomLayout {
     size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, dsort_items(P))]
     size_t dsort_totals;  // uint32 [RADIX]
     size_t emit_sums;     // uint32 [emit_blocks(P)] rank-order instance offsets per emit block
-    size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts (zeroed by preprocess)
+    size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts + 1 "filed" flag (zeroed by preprocess)
     size_t bytes;
 };
 __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
@@ -137,7 +137,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_hist = take((size_t)RADIX * radix_blocks(P, dsort_items(P)) * 4);
     L.dsort_totals = take((size_t)RADIX * 4);
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
-    L.order_cnt = take(8 * 32 * 4);
+    L.order_cnt = take((8 * 32 + 1) * 4);
     L.bytes = o;
     return L;
 }
@@ -172,6 +172,7 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H)
 struct ImgLayout {
     size_t off[GSR_IMG_NFIELDS];
     size_t qlist;   // uint32 [8][32][maxc] quadrants filed by XCD and forward work (gsr_blend.hpp)
+    size_t qbucket; // uint8 [4 * tiles] each quadrant's forward work bucket (render_fwd.hip)
     size_t bytes;
 };
 __host__ __device__ inline ImgLayout img_layout(int W, int H) {
@@ -183,6 +184,7 @@ __host__ __device__ inline ImgLayout img_layout(int W, int H) {
     L.off[GSR_IMG_N_CONTRIB] = take((size_t)W * H * 4);
     // per (XCD, bucket) room for every quadrant of the XCD (the longest list <= T / 2 + 16)
     L.qlist = take((size_t)8 * 32 * ((size_t)g.tiles / 2 + 16) * 4);
+    L.qbucket = take((size_t)g.tiles * 4);
     L.bytes = o;
     return L;
 }

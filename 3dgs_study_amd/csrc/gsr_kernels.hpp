@@ -26,6 +26,8 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
                              float *out_color, hipStream_t s);
 
 // render_bwd.hip
+hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
+                              hipStream_t s);
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
                              const void *img, const float *dL_dpix, float *accum, hipStream_t s);
 

@@ -152,3 +152,37 @@ def test_noncontiguous_inputs_match_contiguous(dev):
     for n in g0:  # accumulator atomics reorder sums run to run: rel-L2, not bits
         assert rel_l2(g1[n].cpu().numpy(), g0[n].cpu().numpy()) <= 1e-5, n
     assert rel_l2(m1.cpu().numpy(), m0.cpu().numpy()) <= 1e-5
+
+
+def test_second_backward_with_retain_graph(dev):
+    """Two backward passes of ONE forward (retain_graph=True) give the same gradients:
+    the backward's first launch files the quadrants for render_bwd's wave order once
+    per forward (bwd_prepare_kernel); the second pass finds them filed and reuses them
+    (filing again would overflow the order lists)."""
+    import math
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from helpers import case, random_dL
+
+    cam, g = case(20_000, 320, 240, 3, seed=4, view=1)
+    camd = cam.to(dev)
+    dL = torch.from_numpy(random_dL(240, 320)).to(dev)
+    leaves = {n: t.detach().to(dev).clone().requires_grad_(True) for n, t in (
+        ("xyz", g.get_xyz), ("sh", g.get_features), ("op", g.get_opacity), ("sc", g.get_scaling),
+        ("rot", g.get_rotation))}
+    settings = GaussianRasterizationSettings(
+        image_height=240, image_width=320, tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5),
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=camd.world_view_transform,
+        projmatrix=camd.full_proj_transform, sh_degree=3, campos=camd.camera_center, prefiltered=False, debug=False)
+    means2D = torch.zeros_like(leaves["xyz"], requires_grad=True)
+    img, _ = GaussianRasterizer(settings)(means3D=leaves["xyz"], means2D=means2D, opacities=leaves["op"],
+                                          shs=leaves["sh"], scales=leaves["sc"], rotations=leaves["rot"])
+    loss = (img * dL).sum()
+    loss.backward(retain_graph=True)
+    first = {n: t.grad.clone() for n, t in leaves.items()}
+    for t in leaves.values():
+        t.grad = None
+    loss.backward()
+    for n, t in leaves.items():
+        assert torch.isfinite(t.grad).all(), n
+        assert rel_l2(t.grad.cpu().numpy(), first[n].cpu().numpy()) <= 1e-5, n
