@@ -65,9 +65,12 @@ template <typename F>
 hipError_t timed(int st, hipStream_t s, F &&launch) {
     if (!(g_timer.mask & (1 << (st & 0xff)))) return launch();
     if (g_timer.used == g_timer.pool.size()) {
+        // timing-only events: no system-scope fence on record (a default event's
+        // cache writeback / invalidate opened a ~6 us idle gap before the next kernel
+        // and cooled its caches); the elapsed time is read after a stream sync
         hipEvent_t a, b;
-        hipError_t e = hipEventCreate(&a);
-        if (e == hipSuccess) e = hipEventCreate(&b);
+        hipError_t e = hipEventCreateWithFlags(&a, hipEventDisableSystemFence);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&b, hipEventDisableSystemFence);
         if (e != hipSuccess) return e;
         g_timer.pool.emplace_back(a, b);
         g_timer.stage.push_back(st);
