@@ -220,7 +220,8 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     // (stores are counted by vmcnt too: issued here, after the geometry, they do not
     // hold up its waits for the per-Gaussian loads)
     for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
-    if (idx <= 8 * ORDER_NBUCKET) a.order_cnt[idx] = 0u;  // the backward wave-order buckets + filed flag (render_bwd.hip)
+    if (idx < 8 * ORDER_NBUCKET) a.order_cnt[idx] = 0u;  // the backward wave-order buckets (render_bwd.hip)
+    if (idx == 0) a.order_cnt[8 * ORDER_NBUCKET] = 0u;     // and the "filed" flag (one block may be all there is)
     // colour stage: the SH rows land in LDS now, after the geometry
     if (use_sh && !DIRECT) __syncthreads();
     if (emit) {

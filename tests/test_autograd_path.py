@@ -186,3 +186,37 @@ def test_second_backward_with_retain_graph(dev):
     for n, t in leaves.items():
         assert torch.isfinite(t.grad).all(), n
         assert rel_l2(t.grad.cpu().numpy(), first[n].cpu().numpy()) <= 1e-5, n
+
+
+def test_repeated_small_scene_backward(dev):
+    """A one-block scene (P <= 256: the preprocess grid is a single workgroup) run
+    forward + backward repeatedly gives the same gradients every time: the
+    preprocess clears the backward's "filed" flag in scratch memory that the caching
+    allocator hands back from the previous iteration (render_bwd sets it)."""
+    import math
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from helpers import case, random_dL
+
+    cam, g = case(200, 64, 64, 3, seed=6, view=0)
+    camd = cam.to(dev)
+    dL = torch.from_numpy(random_dL(64, 64)).to(dev)
+    settings = GaussianRasterizationSettings(
+        image_height=64, image_width=64, tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5),
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=camd.world_view_transform,
+        projmatrix=camd.full_proj_transform, sh_degree=3, campos=camd.camera_center, prefiltered=False, debug=False)
+    runs = []
+    for _ in range(3):
+        leaves = {n: t.detach().to(dev).clone().requires_grad_(True) for n, t in (
+            ("xyz", g.get_xyz), ("sh", g.get_features), ("op", g.get_opacity), ("sc", g.get_scaling),
+            ("rot", g.get_rotation))}
+        means2D = torch.zeros_like(leaves["xyz"], requires_grad=True)
+        img, _ = GaussianRasterizer(settings)(means3D=leaves["xyz"], means2D=means2D, opacities=leaves["op"],
+                                              shs=leaves["sh"], scales=leaves["sc"], rotations=leaves["rot"])
+        (img * dL).sum().backward()
+        runs.append({n: t.grad.cpu().numpy() for n, t in leaves.items()})
+        del img, leaves, means2D
+    assert np.abs(runs[0]["op"]).sum() > 0
+    for r in runs[1:]:
+        for n in r:
+            assert rel_l2(r[n], runs[0][n]) <= 1e-5, n
