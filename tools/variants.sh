@@ -15,8 +15,10 @@ for spec in "$@"; do
   OBJS=""
   for f in $ALL; do
     if [ "$SRC" = all ] || [ "$f" = "$SRC" ]; then
+      extra=""  # the Makefile's per-object flags
+      case $f in render_fwd|render_bwd) extra="-mllvm --amdgpu-sched-strategy=iterative-ilp" ;; esac
       /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -I../../include -munsafe-fp-atomics \
-          -fno-slp-vectorize $flags -c $f.hip -o ../build/var/${f}_$name.o
+          -fno-slp-vectorize $extra $flags -c $f.hip -o ../build/var/${f}_$name.o
       OBJS="$OBJS ../build/var/${f}_$name.o"
     else
       OBJS="$OBJS ../build/$f.o"
