@@ -24,9 +24,21 @@ thread_local std::string g_err;
 // (the call waits for that launch's event before returning, so calls from one
 // thread never share them in flight).
 thread_local uint32_t *g_pinned = nullptr;
-// pinned words: num_rendered lo / hi, prefiltered error, depth-sort pass count
-constexpr int HOST_DSORT_PASSES = 3;
+// pinned words: num_rendered lo / hi, prefiltered error
 thread_local hipEvent_t g_ctrl_ready = nullptr;
+
+// Per host thread and device: the depth sort's own stream (highest priority: its
+// chain of short launches is the longer path) beside the caller's, and the fork /
+// join events (binning.hip: the sort needs only the view depths, so it overlaps
+// preprocess).  Events are reused call after call: a call's record / wait pairs are
+// enqueued in order, so a wait always sees this call's record.
+struct SideStream {
+    int device = -1;
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+constexpr int MAX_DEVICES = 64;
+thread_local SideStream g_side[MAX_DEVICES];
 
 int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -55,8 +67,9 @@ struct StageTimer {
 };
 StageTimer g_timer;  // the ABI is driven from one host thread per process
 
-const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess", "scan",       "depth_sort", "duplicate",
-                                            "tile_sort",  "render_fwd", "render_bwd", "preprocess_bwd"};
+const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess",     "scan",        "depth_sort",           "duplicate",
+                                            "tile_sort",      "render_fwd",  "render_bwd",           "preprocess_bwd",
+                                            "bwd_prepare",    "depth_sort_concurrent"};
 
 // st | TIMED_MORE: more work of a stage already counted once in this step (its
 // time is added, its launch count is not)
@@ -86,6 +99,28 @@ hipError_t timed(int st, hipStream_t s, F &&launch) {
 }
 
 // upstream debug mode: synchronise and check after every kernel
+int side_stream(hipStream_t main, SideStream **out) {
+    int dev = 0;
+    if (int rc = check_hip(hipStreamGetDevice(main, &dev), "hipStreamGetDevice")) return rc;
+    if (dev < 0 || dev >= MAX_DEVICES) return fail(GSR_ERR_ARGS, "device %d out of range", dev);
+    SideStream &x = g_side[dev];
+    if (x.s == nullptr) {
+        int cur = 0;
+        hipError_t e = hipGetDevice(&cur);
+        if (e == hipSuccess && cur != dev) e = hipSetDevice(dev);
+        int least = 0, greatest = 0;
+        if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, greatest);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&x.join, hipEventDisableTiming);
+        if (cur != dev) (void)hipSetDevice(cur);
+        if (int rc = check_hip(e, "depth-sort stream")) return rc;
+        x.device = dev;
+    }
+    *out = &x;
+    return GSR_OK;
+}
+
 int step(hipError_t e, const char *what, bool debug, hipStream_t s) {
     int rc = check_hip(e, what);
     if (rc || !debug) return rc;
@@ -100,6 +135,7 @@ int validate(const gsr_inputs *in, bool forward) {
         return fail(GSR_ERR_CAPACITY, "image too large");
     if (in->footprint != GSR_FOOTPRINT_RECT && in->footprint != GSR_FOOTPRINT_TIGHT)
         return fail(GSR_ERR_ARGS, "footprint must be GSR_FOOTPRINT_RECT or GSR_FOOTPRINT_TIGHT (got %d)", in->footprint);
+    if (in->flags & ~GSR_FLAG_PREPARE_BACKWARD) return fail(GSR_ERR_ARGS, "unknown flags 0x%x", in->flags);
     if (in->P == 0) return GSR_OK;
     if (!in->means3D || !in->viewmatrix || !in->projmatrix || !in->bg || (forward && !in->opacities))
         return fail(GSR_ERR_ARGS, "missing required input (means3D/opacities/viewmatrix/projmatrix/bg)");
@@ -184,20 +220,40 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     const bool dbg = in->debug != 0;
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
+    // The depth sort needs only the view depths: it runs on its own stream beside
+    // preprocess (debug mode: in line, so every kernel is checked on one stream).
+    SideStream *side = nullptr;
+    if (!dbg)
+        if (int rc = side_stream(s, &side)) return rc;
+    hipStream_t ds = side ? side->s : s;
+    if (side) {
+        if (int rc = check_hip(hipEventRecord(side->fork, s), "fork")) return rc;
+        if (int rc = check_hip(hipStreamWaitEvent(ds, side->fork, 0), "fork")) return rc;
+    }
+    if (int rc = step(timed(GSR_STAGE_DSORT_CONCURRENT, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, ds); }), "depth sort", dbg, ds))
+        return rc;
+    if (side)
+        if (int rc = check_hip(hipEventRecord(side->join, ds), "join")) return rc;
     if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s); }), "preprocess", dbg, s)) return rc;
     if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
-    // the depth sort does not depend on num_rendered: it runs while the host waits
-    if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] { return launch_depth_sort(in->P, in->W, in->H, geom, s); }), "depth sort", dbg, s)) return rc;
+    // the sort's exposed part: waiting for its stream, then the rects in rank order
+    // and the emission offsets (queued before the host waits, so the device stays busy)
+    if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] {
+                          if (side) {
+                              hipError_t e = hipStreamWaitEvent(s, side->join, 0);
+                              if (e != hipSuccess) return e;
+                          }
+                          return launch_rank_gather(in->P, in->W, in->H, geom, s);
+                      }),
+                      "rank gather", dbg, s))
+        return rc;
     if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;
     if (g_pinned[CTRL_PREFILTER_ERR])
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     const int64_t I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
     if (I > 0xFFFFFFFFll) return fail(GSR_ERR_CAPACITY, "num_rendered %lld exceeds 32-bit list indexing", (long long)I);
     *num_rendered = I;
-    // the depth sort's fourth pass (wide depth ranges only) and the emission offsets
-    const bool fourth = g_pinned[HOST_DSORT_PASSES] == 4;
-    return step(timed(GSR_STAGE_DUPLICATE | TIMED_MORE, s, [&] { return launch_depth_sort_tail(in->P, in->W, in->H, geom, fourth, s); }),
-                "depth sort", dbg, s);
+    return GSR_OK;
 }
 
 int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
@@ -217,7 +273,30 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
                           "tile sort", dbg, s))
             return rc;
     }  // else every range stays (0, 0) as preprocess left it
-    return step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s); }), "render", dbg, s);
+    // GSR_FLAG_PREPARE_BACKWARD: the backward's accumulator is zeroed on the second
+    // stream beside the blend (which is bound by instruction issue, not bytes) and
+    // the quadrants are filed after it, so the backward starts with render_bwd
+    const bool prep = (in->flags & GSR_FLAG_PREPARE_BACKWARD) != 0;
+    SideStream *side = nullptr;
+    if (prep && !dbg)
+        if (int rc = side_stream(s, &side)) return rc;
+    const GeomLayout G = geom_layout(in->P, in->W, in->H);
+    void *acc = at<void>(geom, G.accum);
+    const size_t acc_bytes = (size_t)in->P * ACCUM_STRIDE * sizeof(float);
+    if (side) {
+        if (int rc = check_hip(hipEventRecord(side->fork, s), "fork")) return rc;
+        if (int rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "fork")) return rc;
+        if (int rc = check_hip(hipMemsetAsync(acc, 0, acc_bytes, side->s), "accumulator")) return rc;
+        if (int rc = check_hip(hipEventRecord(side->join, side->s), "join")) return rc;
+    } else if (prep) {
+        if (int rc = step(hipMemsetAsync(acc, 0, acc_bytes, s), "accumulator", dbg, s)) return rc;
+    }
+    if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s); }), "render", dbg, s))
+        return rc;
+    if (!prep) return GSR_OK;
+    if (side)
+        if (int rc = check_hip(hipStreamWaitEvent(s, side->join, 0), "join")) return rc;
+    return step(launch_bwd_prepare(*in, geom, img, (float *)acc, num_rendered > 0, true, true, s), "backward prepare", dbg, s);
 }
 
 static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
@@ -230,7 +309,7 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     // calls and starts its all-gather of drgb in between.
     if (int rc = validate(in, false)) return rc;
     if (in->P == 0) return GSR_OK;
-    if (!radii || !geom || !img || !accum || !dL_dout_color || (num_rendered > 0 && !binning))
+    if (!radii || !geom || !img || !dL_dout_color || (num_rendered > 0 && !binning))
         return fail(GSR_ERR_ARGS, "backward scratch/inputs are NULL");
     const gsr_leaf_grads L = leaf ? *leaf : gsr_leaf_grads{};
     if (L.dsh_dc && (!in->sh || in->M <= 0 || (in->M > 1 && !L.dsh_rest)))
@@ -239,6 +318,9 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     if (L.drotation && (!L.rotation_norm || !in->rotations))
         return fail(GSR_ERR_ARGS, "leaf drotation: needs rotations and rotation_norm");
     if (L.dopacity && !in->opacities) return fail(GSR_ERR_ARGS, "leaf dopacity: needs opacities");
+    if (drgb && (dsh || L.dsh_dc)) return fail(GSR_ERR_ARGS, "drgb replaces dsh: dsh / leaf dsh must be NULL with it");
+    const bool internal = accum == nullptr;  // geom's accumulator (GSR_FLAG_PREPARE_BACKWARD may have zeroed it)
+    if (internal) accum = at<void>(const_cast<void *>(geom), geom_layout(in->P, in->W, in->H).accum);
     if (!dmeans2D || (!dcolors && in->colors_precomp) || (!dopacity && !L.dopacity) || !dmeans3D ||
         (!dcov3D && in->cov3D_precomp))
         return fail(GSR_ERR_ARGS, "backward outputs are NULL");
@@ -251,7 +333,7 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     const bool colors = drgb && in->sh && in->M > 0;
     if (phases & 1) {
         // zeroes the accumulator and files the quadrants for render_bwd's wave order
-        if (int rc = step(launch_bwd_prepare(*in, const_cast<void *>(geom), img, acc, num_rendered > 0, s),
+        if (int rc = step(timed(GSR_STAGE_BWD_PREPARE, s, [&] { return launch_bwd_prepare(*in, const_cast<void *>(geom), img, acc, num_rendered > 0, internal, false, s); }),
                           "backward prepare", dbg, s))
             return rc;
         if (num_rendered > 0) {
@@ -272,7 +354,6 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     // SH rows for dL/dmean3D's view-direction term but writes no dsh
     BwdOutputs o{dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, colors ? nullptr : dsh, dscales, drot, nullptr,
                  dsh_planar, colors ? 1 : 0, L};
-    if (colors) o.leaf.dsh_dc = o.leaf.dsh_rest = nullptr;  // the exchange owns the SH gradient
     if (L.dsh_dc) o.dsh = nullptr;
     if (L.dscaling) o.dscales = nullptr;
     if (L.drotation) o.drot = nullptr;
@@ -312,6 +393,18 @@ int gsr_backward_colors(const gsr_inputs *in, const int32_t *radii, const void *
     if (in && in->sh && in->D > 3) return fail(GSR_ERR_ARGS, "sh_degree > 3 is not supported");
     return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
                          dopacity, dmeans3D, dcov3D, nullptr, drgb, dscales, drot, stream);
+}
+
+int gsr_backward_phase(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                       const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                       float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
+                       float *drgb, float *dscales, float *drot, const gsr_leaf_grads *leaf, int32_t phases,
+                       void *stream) {
+    if (phases < 1 || phases > 3) return fail(GSR_ERR_ARGS, "phases must be 1, 2 or 3 (got %d)", phases);
+    if (in && in->P > 0 && drgb && in->sh && in->D > 3) return fail(GSR_ERR_ARGS, "sh_degree > 3 is not supported");
+    return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
+                         dopacity, dmeans3D, dcov3D, dsh, drgb, dscales, drot, stream, leaf ? leaf->dsh_planar : 0,
+                         phases, leaf);
 }
 
 static int colors_phase(int phases, const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,

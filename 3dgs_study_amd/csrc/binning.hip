@@ -8,10 +8,15 @@
 // (depth_bits, id).  Here the same order comes from two much cheaper sorts:
 //
 //  1. depth sort  — stable LSD radix sort of the P depth bit patterns with the
-//                   index as value (4 passes over P, not I): order[rank] = id in
-//                   (depth_bits, id) order.  Invisible Gaussians sort anywhere:
-//                   they emit nothing.
-//  2. rank scan   — exclusive scan of tiles_touched gathered in rank order.
+//                   index as value (3 passes over P when the keys span < 2^24,
+//                   else 4; not over I): order[rank] = id in (depth_bits, id)
+//                   order.  It needs only the view depths, so it runs on a second
+//                   stream beside preprocess (depth_keys_kernel computes the keys
+//                   and the first pass's digit counts itself) and preprocess's
+//                   bytes and the sort's launch-bound chain overlap.  Gaussians
+//                   that preprocess culls sort anywhere: they emit nothing.
+//  2. rank scan   — the tile rects gathered in rank order (rank_gather_kernel),
+//                   instances per emit block, an exclusive scan of those.
 //  3. emit        — each Gaussian, in rank order, writes (tile, id) for every
 //                   tile of its rect (row-major, as upstream) at its offset.
 //  4. tile sort   — stable LSD radix sort of the I instances by tile index
@@ -27,8 +32,8 @@
 //  5. ranges      — from the second pass's per-block digit counts (two-pass
 //                   case), else identifyTileRanges on the sorted tile keys.
 //
-// Steps 1-2 run in gsr_forward_preprocess while the host reads num_rendered;
-// 3-5 run in gsr_forward_render once the caller has sized the binning buffer.
+// Steps 1-2 run in gsr_forward_preprocess (step 2 once both streams are done),
+// 3-5 in gsr_forward_render once the caller has sized the binning buffer.
 //
 // One radix pass = upsweep (per-block digit histogram), digit scan (one
 // workgroup per digit over the blocks), downsweep (stable scatter).  Inside a
@@ -80,8 +85,6 @@ struct RadixPass {
     const uint32_t *vin;   // values; nullptr = the item index
     uint32_t *kout;        // nullptr = keys not needed after this pass
     uint32_t *vout;
-    const uint4 *gsrc;     // optional: gdst[pos] = gsrc[value] for every written value
-    uint4 *gdst;
     uint32_t n;
     int shift;
     int nbits;             // significant bits of this pass's digit (<= RADIX_BITS)
@@ -91,7 +94,9 @@ struct RadixPass {
     int NB;
     // depth sort only (nullptr / 0 otherwise): the geom control words and this
     // pass's role when the key range allows three passes instead of four
-    const uint32_t *ctrl;
+    const uint32_t *ctrl;  // GeomLayout::dsort_ctrl
+    uint2 *minmax;         // first depth pass: the candidate key range per block (its digit scan reduces it)
+    uint32_t *ctrl_out;    // ... into these control words
     int role;              // RX_PLAIN, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH
     uint32_t *vout_final;  // RX_DEPTH_THIRD in three-pass mode: the order lands here
     // packed two-pass tile sort (tile_sort_packed): the first pass (RXM_PACK)
@@ -110,16 +115,20 @@ struct RadixPass {
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
 
-// First depth pass: key = depth bits - base, clamped to 24 bits in three-pass
-// mode (only invisible Gaussians, +inf keys, reach the clamp).
+// First depth pass: key = depth bits - base (base = the smallest candidate key
+// with its low byte cleared, so the key's low byte — this pass's digit, which
+// depth_keys_kernel counted before the base was known — is the raw bits' own);
+// in three-pass mode keys beyond 2^24 (only non-candidates, +inf keys, reach it)
+// saturate their top 16 bits and keep that low byte: every pass then sorts by the
+// digits of one and the same key.
 __device__ __forceinline__ uint32_t key_of(const RadixPass &a, uint32_t k) {
     if (a.role != RX_DEPTH_FIRST) return k;
-    const uint32_t d = k - a.ctrl[CTRL_KEY_BASE];
-    return a.ctrl[CTRL_DSORT_PASSES] == 3 ? min(d, 0xffffffu) : d;
+    const uint32_t d = k - a.ctrl[DCTRL_KEY_BASE];
+    return a.ctrl[DCTRL_PASSES] == 3 && d > 0xffffffu ? (0xffff00u | (d & 0xffu)) : d;
 }
 __device__ __forceinline__ uint32_t load_key(const RadixPass &a, uint32_t idx) { return key_of(a, a.kin[idx]); }
 __device__ __forceinline__ bool pass_skipped(const RadixPass &a) {
-    return a.role == RX_DEPTH_FOURTH && a.ctrl[CTRL_DSORT_PASSES] == 3;
+    return a.role == RX_DEPTH_FOURTH && a.ctrl[DCTRL_PASSES] == 3;
 }
 
 // Workgroup -> radix block.  The per-block digit counts live column-major
@@ -261,6 +270,36 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
 constexpr int DSCAN_THREADS = 1024, DSCAN_PER = 16;
 __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPass a) {
     __shared__ uint32_t wsum[DSCAN_THREADS / 64];
+    if (blockIdx.x == RADIX) {  // first depth pass: one more workgroup reduces the candidate key range
+        __shared__ uint32_t wmin[DSCAN_THREADS / 64], wmax[DSCAN_THREADS / 64];
+        uint32_t kmin = 0xffffffffu, kmax = 0u;
+        for (int i = threadIdx.x; i < a.NB; i += DSCAN_THREADS) {
+            const uint2 m = a.minmax[i];
+            kmin = min(kmin, m.x);
+            kmax = max(kmax, m.y);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+            kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            wmin[threadIdx.x >> 6] = kmin;
+            wmax[threadIdx.x >> 6] = kmax;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < DSCAN_THREADS / 64; k++) {
+                kmin = min(kmin, wmin[k]);
+                kmax = max(kmax, wmax[k]);
+            }
+            const bool any = kmin <= kmax;
+            const uint32_t base = any ? (kmin & ~0xffu) : 0u;
+            a.ctrl_out[DCTRL_KEY_BASE] = base;
+            a.ctrl_out[DCTRL_PASSES] = any && kmax - base > 0xffffffu ? 4u : 3u;
+        }
+        return;
+    }
     if (pass_skipped(a)) return;
     const uint32_t tot =
         block_exclusive_scan_inplace<DSCAN_THREADS, DSCAN_PER>(a.hist + (size_t)blockIdx.x * a.NB, a.NB, wsum);
@@ -282,10 +321,9 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     __shared__ uint32_t stage_k[TILE_N], stage_v[MODE == RXM_UNPACK ? 1 : TILE_N];
     if (pass_skipped(a)) return;
     // three-pass depth sort: the third pass is the last one
-    const bool final3 = a.role == RX_DEPTH_THIRD && a.ctrl[CTRL_DSORT_PASSES] == 3;
+    const bool final3 = a.role == RX_DEPTH_THIRD && a.ctrl[DCTRL_PASSES] == 3;
     uint32_t *const kout = final3 ? nullptr : a.kout;
     uint32_t *const vout = final3 ? a.vout_final : a.vout;
-    const bool gather = a.gdst && (a.role != RX_DEPTH_THIRD || final3);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t blk = radix_block(a.NB);
     const uint2 span = block_span<TILE_N, MODE>(a, blk, sfb, sst, wsum);
@@ -382,7 +420,6 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
             const uint32_t v = stage_v[i];
             if (kout) kout[pos] = k;
             vout[pos] = v;
-            if (gather) a.gdst[pos] = a.gsrc[v];
         }
     }
     if constexpr (MODE == RXM_UNPACK) {
@@ -406,10 +443,11 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
 }
 
 template <int ITEMS, int MODE = RXM_KV>
-static hipError_t radix_pass(const RadixPass &a, hipStream_t s) {
+static hipError_t radix_pass(const RadixPass &a, hipStream_t s, bool counted = false) {
     if (a.n == 0) return hipSuccess;
-    hipLaunchKernelGGL((radix_upsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
-    hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(RADIX), dim3(DSCAN_THREADS), 0, s, a);
+    // counted: the digit counts are already in a.hist (depth_keys_kernel)
+    if (!counted) hipLaunchKernelGGL((radix_upsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
+    hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(a.minmax ? RADIX + 1 : RADIX), dim3(DSCAN_THREADS), 0, s, a);
     hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     return hipGetLastError();
 }
@@ -446,19 +484,50 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t lo, uint32_t hi, uint32
     return base;
 }
 
-__global__ void __launch_bounds__(EMIT_BLOCK)
-    rank_sums_kernel(const uint4 *rects_ranked, int P, uint32_t *sums) {
-    __shared__ uint32_t wsum[EMIT_BLOCK / 64];
-    const int r = blockIdx.x * EMIT_BLOCK + threadIdx.x;
-    const uint32_t v = r < P ? rect_count(rects_ranked[r]) : 0u;
-    const uint32_t tot = block_sum<EMIT_BLOCK>(v, wsum);
-    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
-}
-
-constexpr int TOPSCAN_THREADS = 1024;
-__global__ void __launch_bounds__(TOPSCAN_THREADS) exclusive_scan_one_block_kernel(uint32_t *v, int n) {
-    __shared__ uint32_t wsum[TOPSCAN_THREADS / 64];
-    block_exclusive_scan_inplace<TOPSCAN_THREADS, 8>(v, n, wsum);  // config E: 16.8 -> 5.7 us
+// The tile rects in rank (depth) order, and where each emit block's instances
+// start: one random 16-B gather per Gaussian (the depth sort's order meets
+// preprocess's rects here, after both streams), the rest coalesced.  A workgroup
+// covers RG_SUPER emit blocks (4,096 ranks, RG_RANKS per thread with every load
+// issued first) and writes each one's instances before it within the workgroup,
+// and its total; emit_kernel adds the totals of the workgroups before its own —
+// so no scan launch sits between this kernel and the emission.
+__global__ void __launch_bounds__(RG_THREADS)
+    rank_gather_kernel(const uint32_t *order, const uint4 *rects, int P, uint4 *rects_ranked, uint32_t *local,
+                       uint32_t *super) {
+    __shared__ uint32_t wsum[RG_RANKS][RG_THREADS / 64];
+    const int r0 = blockIdx.x * RG_THREADS * RG_RANKS + threadIdx.x;
+    uint32_t id[RG_RANKS];
+#pragma unroll
+    for (int k = 0; k < RG_RANKS; k++) {
+        const int r = r0 + k * RG_THREADS;
+        id[k] = r < P ? order[r] : 0u;
+    }
+    uint4 q[RG_RANKS];
+#pragma unroll
+    for (int k = 0; k < RG_RANKS; k++) q[k] = r0 + k * RG_THREADS < P ? rects[id[k]] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < RG_RANKS; k++) {
+        const int r = r0 + k * RG_THREADS;
+        if (r < P) rects_ranked[r] = q[k];
+        uint32_t c = rect_count(q[k]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+        if ((threadIdx.x & 63) == 0) wsum[k][threadIdx.x >> 6] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // emit block j of the workgroup: round j / 4, threads 256 (j % 4) ...
+        constexpr int WPE = EMIT_BLOCK / 64;                 // waves per emit block
+        constexpr int EPR = RG_THREADS / EMIT_BLOCK;          // emit blocks per round
+        const int j = threadIdx.x;
+        uint32_t v = 0;
+        if (j < RG_SUPER)
+#pragma unroll
+            for (int w = 0; w < WPE; w++) v += wsum[j / EPR][(j % EPR) * WPE + w];
+        const uint32_t inc = wave_inclusive_scan(v);
+        const int e = blockIdx.x * RG_SUPER + j;
+        if (j < RG_SUPER && e < emit_blocks(P)) local[e] = inc - v;
+        if (j == RG_SUPER - 1) super[blockIdx.x] = inc;
+    }
 }
 
 // duplicateWithKeys in rank order: (tile, id) for every tile of the rect.
@@ -479,7 +548,8 @@ struct EmitArgs {
     int packed, lo_bits, id_bits;
     const uint32_t *order;
     const uint4 *rects;
-    const uint32_t *block_prefix;
+    const uint32_t *block_local;  // instances before the block within its rank-gather workgroup
+    const uint32_t *super;        // instances per rank-gather workgroup
     uint32_t *tile_keys;
     uint32_t *ids;
 };
@@ -490,11 +560,17 @@ __device__ __forceinline__ uint32_t div_small(uint32_t pos, uint32_t w) {  // po
     return y;
 }
 __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
-    __shared__ uint32_t wsum[EMIT_BLOCK / 64];
+    __shared__ uint32_t wsum[2 * (EMIT_BLOCK / 64)];
     __shared__ uint32_t loff[EMIT_BLOCK + 1];
     __shared__ uint4 rect[EMIT_BLOCK];  // x0, width, y0, id
     __shared__ uint2 mask[EMIT_BLOCK];  // tile mask; {~0, ~0} = every tile of the rect
     const int r = blockIdx.x * EMIT_BLOCK + threadIdx.x;
+    // the block's first instance: the rank-gather workgroups before its own, summed
+    // here (<= 2 loads per thread up to 2M Gaussians), + its offset within its own
+    uint32_t pre = 0;
+    const int ns = blockIdx.x / RG_SUPER;
+    for (int i = threadIdx.x; i < ns; i += EMIT_BLOCK) pre += a.super[i];
+    const uint32_t loc = a.block_local[blockIdx.x];
     const uint32_t id = r < a.P ? a.order[r] : 0u;
     const uint4 q = r < a.P ? a.rects[r] : make_uint4(0u, 0u, 0u, 0u);  // rects in depth order
     const uint32_t v = rect_count(q);
@@ -506,8 +582,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
         rect[threadIdx.x] = make_uint4(q.x & 0xffffu, (q.x >> 16) - (q.x & 0xffffu), q.y & 0xffffu, id);
         mask[threadIdx.x] = make_uint2(q.z, q.w);
     }
-    __syncthreads();
-    const uint32_t base = a.block_prefix[blockIdx.x];
+    const uint32_t base = block_sum<EMIT_BLOCK>(pre, wsum + EMIT_BLOCK / 64) + loc;  // (its own barriers)
     // a round's EMIT_BLOCK x EMIT_IPT instances go through LDS (thread t's run at
     // stride EMIT_IPT + 1 words: conflict-free) and leave coalesced
     constexpr int RS = EMIT_IPT + 1;
@@ -635,13 +710,84 @@ hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const v
     return hipGetLastError();
 }
 
+// The depth sort's keys and its first pass's digit counts in one launch (the
+// first pass needs no upsweep of its own): per Gaussian the view-space depth as
+// preprocess computes it (xform_point4x3, the same operations, no contraction),
+// key = its bits for a candidate (z > 0.2: not culled by the near plane), +inf
+// bits otherwise; per radix block the histogram of the keys' low byte (the first
+// digit needs no base: key_of keeps it) and the candidates' key range, which the
+// first digit scan reduces into the base and the pass count.
+struct DepthKeyArgs {
+    const float *means3D;
+    const float *viewmatrix;
+    uint32_t n;
+    int NB;
+    uint32_t *keys;
+    uint32_t *hist;   // [RADIX][NB]
+    uint2 *minmax;    // [NB]
+};
+template <int ITEMS>
+__global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) {
+    constexpr int TILE_N = RX_THREADS * ITEMS;
+    __shared__ uint32_t h[RX_WAVES][RADIX];
+    __shared__ uint32_t wmin[RX_WAVES], wmax[RX_WAVES];
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
+    const uint32_t blk = radix_block(a.NB);
+    const Mat4 V = load_mat4(a.viewmatrix);
+    float z[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {  // every load first
+        const uint32_t idx = blk * (uint32_t)TILE_N + (uint32_t)(r * RX_THREADS) + threadIdx.x;
+        const uint32_t li = idx < a.n ? idx : a.n - 1;
+        const f3 p = {a.means3D[3 * (size_t)li], a.means3D[3 * (size_t)li + 1], a.means3D[3 * (size_t)li + 2]};
+        z[r] = xform_point4x3(p, V).z;
+    }
+    __syncthreads();
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const uint32_t idx = blk * (uint32_t)TILE_N + (uint32_t)(r * RX_THREADS) + threadIdx.x;
+        if (idx < a.n) {
+            const bool cand = z[r] > 0.2f;  // preprocess culls z <= 0.2 (and a NaN depth sorts last)
+            const uint32_t key = cand ? __float_as_uint(z[r]) : 0x7f800000u;
+            a.keys[idx] = key;
+            atomicAdd(&h[w][key & (RADIX - 1)], 1u);
+            if (cand) {
+                kmin = min(kmin, key);
+                kmax = max(kmax, key);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wmin[w] = kmin;
+        wmax[w] = kmax;
+    }
+    __syncthreads();
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < RX_WAVES; k++) c += h[k][threadIdx.x];
+    a.hist[(size_t)threadIdx.x * a.NB + blk] = c;
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < RX_WAVES; k++) {
+            kmin = min(kmin, wmin[k]);
+            kmax = max(kmax, wmax[k]);
+        }
+        a.minmax[blk] = make_uint2(kmin, kmax);
+    }
+}
+
 // ------------------------------------------------------------ launchers
-// The depth sort is launched in two parts around the host's one sync.  Passes 1-3
-// go first (they overlap the host wait); the third pass writes the final order
-// itself when every visible key lies within 2^24 of the base (decided on the
-// device from publish_total_kernel's control words).  Once the host has read the
-// pass count, launch_depth_sort_tail adds the fourth pass only when it is needed,
-// then the rank-order block offsets of the emission.
+// The depth sort runs on its own stream beside preprocess (abi.hip forks it):
+// depth_keys_kernel, then passes 1-3 and the fourth pass, whose kernels return at
+// once unless the key range needs it (decided on the device from the first digit
+// scan's control words).  The order lands in GSR_GEOM_DEPTH_ORDER either way.
 static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     const GeomLayout L = geom_layout(P, W, H);
     RadixPass a = {};
@@ -649,17 +795,20 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     a.NB = radix_blocks(P, dsort_items(P));
     a.hist = at<uint32_t>(geom, L.dsort_hist);
     a.totals = at<uint32_t>(geom, L.dsort_totals);
-    const uint32_t *depth_bits = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTHS]);
     uint32_t *ka = at<uint32_t>(geom, L.dsort_keys_a), *kb = at<uint32_t>(geom, L.dsort_keys_b);
     uint32_t *va = at<uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), *vb = at<uint32_t>(geom, L.dsort_vals_b);
     uint32_t *vc = at<uint32_t>(geom, L.dsort_vals_c);
-    // (depth - base, index) -> b -> a -> b -> a(order); values - -> b -> c -> b -> order
-    const uint32_t *kin[4] = {depth_bits, kb, ka, kb};
+    // keys: a (depth_keys_kernel) -> b -> a -> b -> -; values: index -> b -> c -> b -> order
+    const uint32_t *kin[4] = {ka, kb, ka, kb};
     const uint32_t *vin[4] = {nullptr, vb, vc, vb};
     uint32_t *kout[4] = {kb, ka, kb, nullptr};
     uint32_t *vout[4] = {vb, vc, vb, va};
     const int role[4] = {RX_DEPTH_FIRST, RX_PLAIN, RX_DEPTH_THIRD, RX_DEPTH_FOURTH};
-    a.ctrl = at<const uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+    a.ctrl = at<const uint32_t>(geom, L.dsort_ctrl);
+    if (p == 0) {
+        a.minmax = at<uint2>(geom, L.dsort_minmax);
+        a.ctrl_out = at<uint32_t>(geom, L.dsort_ctrl);
+    }
     a.vout_final = va;
     a.kin = kin[p];
     a.vin = vin[p];
@@ -669,44 +818,46 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     a.shift = 8 * p;
     a.nbits = RADIX_BITS;
     a.dmask = RADIX - 1;
-    // the last pass also lays the tile rects out in depth order (one random
-    // gather here instead of one in rank_sums and one in emit)
-    a.gsrc = p >= 2 ? at<const uint4>(geom, L.rects) : nullptr;
-    a.gdst = p >= 2 ? at<uint4>(geom, L.rects_ranked) : nullptr;
     return a;
 }
 
-static hipError_t depth_radix_pass(int P, const RadixPass &a, hipStream_t s) {
-    return dsort_items(P) == DSORT_ITEMS_BIG ? radix_pass<DSORT_ITEMS_BIG>(a, s) : radix_pass<DSORT_ITEMS>(a, s);
-}
-
-static hipError_t launch_rank_offsets(int P, int W, int H, void *geom, hipStream_t s) {
-    // rank-order exclusive offsets of the instances, per EMIT block
+template <int ITEMS>
+static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
+                                   hipStream_t s) {
     const GeomLayout L = geom_layout(P, W, H);
-    const int nb = emit_blocks(P);
-    uint32_t *sums = at<uint32_t>(geom, L.emit_sums);
-    hipLaunchKernelGGL(rank_sums_kernel, dim3(nb), dim3(EMIT_BLOCK), 0, s, at<const uint4>(geom, L.rects_ranked), P,
-                       sums);
-    hipLaunchKernelGGL(exclusive_scan_one_block_kernel, dim3(1), dim3(TOPSCAN_THREADS), 0, s, sums, nb);
+    DepthKeyArgs k;
+    k.means3D = means3D;
+    k.viewmatrix = viewmatrix;
+    k.n = (uint32_t)P;
+    k.NB = radix_blocks(P, ITEMS);
+    k.keys = at<uint32_t>(geom, L.dsort_keys_a);
+    k.hist = at<uint32_t>(geom, L.dsort_hist);
+    k.minmax = at<uint2>(geom, L.dsort_minmax);
+    hipLaunchKernelGGL(depth_keys_kernel<ITEMS>, dim3(k.NB), dim3(RX_THREADS), 0, s, k);
+    for (int p = 0; p < 4; p++) {
+        hipError_t e = radix_pass<ITEMS>(depth_pass(P, W, H, geom, p), s, p == 0);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 
-// Passes 1-3 and the emission offsets are queued before the host waits (they
-// keep the device busy while the host wakes up and launches the rest); in the
-// rare four-pass case the tail redoes the offsets after the fourth pass.
-hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s) {
-    for (int p = 0; p < 3; p++) {
-        hipError_t e = depth_radix_pass(P, depth_pass(P, W, H, geom, p), s);
-        if (e != hipSuccess) return e;
-    }
-    return launch_rank_offsets(P, W, H, geom, s);
+hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
+                             hipStream_t s) {
+    if (P <= 0) return hipSuccess;
+    return dsort_items(P) == DSORT_ITEMS_BIG ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, s)
+                                             : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, s);
 }
 
-hipError_t launch_depth_sort_tail(int P, int W, int H, void *geom, bool fourth_pass, hipStream_t s) {
-    if (!fourth_pass) return hipSuccess;
-    hipError_t e = depth_radix_pass(P, depth_pass(P, W, H, geom, 3), s);
-    if (e != hipSuccess) return e;
-    return launch_rank_offsets(P, W, H, geom, s);
+// After both streams: the rects in rank order and the rank-order instance offsets
+// of the emit blocks.
+hipError_t launch_rank_gather(int P, int W, int H, void *geom, hipStream_t s) {
+    if (P <= 0) return hipSuccess;
+    const GeomLayout L = geom_layout(P, W, H);
+    hipLaunchKernelGGL(rank_gather_kernel, dim3(rg_blocks(P)), dim3(RG_THREADS), 0, s,
+                       at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), at<const uint4>(geom, L.rects), P,
+                       at<uint4>(geom, L.rects_ranked), at<uint32_t>(geom, L.emit_sums),
+                       at<uint32_t>(geom, L.emit_super));
+    return hipGetLastError();
 }
 
 hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
@@ -719,7 +870,8 @@ hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, vo
     a.gx = g.gx;
     a.order = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]);
     a.rects = at<const uint4>(geom, L.rects_ranked);
-    a.block_prefix = at<const uint32_t>(geom, L.emit_sums);
+    a.block_local = at<const uint32_t>(geom, L.emit_sums);
+    a.super = at<const uint32_t>(geom, L.emit_super);
     // emit into the buffer pair that the tile passes will end in KEYS/POINT_LIST
     // (the packed form: emit -> b, first pass -> KEYS, second -> POINT_LIST)
     const bool packed = tile_sort_packed(g.tiles, P);

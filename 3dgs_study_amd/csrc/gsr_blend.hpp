@@ -220,6 +220,7 @@ __host__ inline int blend_grid(int tiles) {
 // placement: a speed hint only) takes XCD x's r-th entry in bucket order.
 constexpr int ORDER_STRIP = 4 * XCD_STRIP;  // quadrants per strip
 constexpr int ORDER_NBUCKET = 32;           // work buckets per XCD, heaviest first
+static_assert(ORDER_FILED == 8 * ORDER_NBUCKET, "the flag words follow the 8 x ORDER_NBUCKET counts");
 __host__ __device__ inline int quad_xcd(int q) { return (q / ORDER_STRIP) & 7; }
 __device__ __forceinline__ int order_bucket(uint32_t work) {  // 16 blended Gaussians per bucket
     return ORDER_NBUCKET - 1 - (int)min(work >> 4, (uint32_t)ORDER_NBUCKET - 1);

@@ -48,6 +48,8 @@ constexpr int TSORT_ITEMS_BIG = 16;
 constexpr int64_t TSORT_BIG_N = 16 << 20;
 __host__ __device__ inline int tsort_items(int64_t n) { return n > TSORT_BIG_N ? TSORT_ITEMS_BIG : TSORT_ITEMS; }
 constexpr int EMIT_BLOCK = 256;  // Gaussians per rank-order emit workgroup
+// rank_gather_kernel (binning.hip): 1024 threads x 4 ranks = RG_SUPER emit blocks
+constexpr int RG_THREADS = 1024, RG_RANKS = 4, RG_SUPER = RG_THREADS * RG_RANKS / EMIT_BLOCK;
 constexpr int PRE_THREADS = 256;          // preprocess block (scan granule)
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -69,6 +71,7 @@ __host__ __device__ inline int radix_blocks(int64_t n, int items) {
     return nb < 1 ? 1 : (int)nb;
 }
 __host__ __device__ inline int emit_blocks(int P) { return (P + EMIT_BLOCK - 1) / EMIT_BLOCK; }
+__host__ __device__ inline int rg_blocks(int P) { return (P + RG_THREADS * RG_RANKS - 1) / (RG_THREADS * RG_RANKS); }
 // LSD passes of the tile sort: enough 8-bit digits to cover tile indices [0, T)
 __host__ __device__ inline int tile_bits(int T) {
     int bits = 0;
@@ -94,14 +97,18 @@ enum CtrlWord {
     CTRL_NUM_RENDERED_LO = 0,
     CTRL_NUM_RENDERED_HI = 1,
     CTRL_PREFILTER_ERR = 2,
-    CTRL_KEY_BASE = 3,      // smallest depth key (bits) of a visible Gaussian
-    CTRL_DSORT_PASSES = 4,  // 3 when every visible key lies within 2^24 of the base, else 4
     CTRL_WORDS = 16
+};
+// the depth sort's own control words (GeomLayout::dsort_ctrl, a line of their own:
+// the sort runs on a second stream beside preprocess, binning.hip)
+enum DsortCtrlWord {
+    DCTRL_KEY_BASE = 0,  // smallest depth key (bits) of a candidate Gaussian, low byte cleared
+    DCTRL_PASSES = 1,    // 3 when every candidate key lies within 2^24 of the base, else 4
 };
 
 struct GeomLayout {
     size_t off[GSR_GEOM_NFIELDS];
-    size_t block_sums;    // uint4 [pre_blocks(P)] per preprocess workgroup: instances | error << 31, key min, max
+    size_t block_sums;    // uint4 [pre_blocks(P)] per preprocess workgroup: instances | error << 31
     size_t rects;         // uint4 [P] tile rect {x0 | x1 << 16, y0 | y1 << 16} + 64-bit tile mask; 0 when not visible
     size_t rects_ranked;  // uint4 [P] the same in depth order (written by the last depth pass)
     size_t dsort_keys_a;  // uint32 [P] depth-sort ping-pong (the order lands in GSR_GEOM_DEPTH_ORDER)
@@ -110,8 +117,12 @@ struct GeomLayout {
     size_t dsort_vals_c;
     size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, dsort_items(P))]
     size_t dsort_totals;  // uint32 [RADIX]
-    size_t emit_sums;     // uint32 [emit_blocks(P)] rank-order instance offsets per emit block
-    size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts + 1 "filed" flag (zeroed by preprocess)
+    size_t dsort_minmax;  // uint2 [radix_blocks(P, dsort_items(P))] candidate key range per first-pass block
+    size_t dsort_ctrl;    // uint32 [16] DsortCtrlWord
+    size_t emit_sums;     // uint32 [emit_blocks(P)] instances before each emit block within its rank-gather block
+    size_t emit_super;    // uint32 [rg_blocks(P)] instances per rank-gather block (RG_SUPER emit blocks)
+    size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts + the ORDER_FLAGS words (zeroed by preprocess)
+    size_t accum;         // float [P][ACCUM_STRIDE] the backward's gradient accumulator (gsr.h GSR_FLAG_PREPARE_BACKWARD)
     size_t bytes;
 };
 __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
@@ -136,8 +147,12 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_vals_c = take((size_t)P * 4);
     L.dsort_hist = take((size_t)RADIX * radix_blocks(P, dsort_items(P)) * 4);
     L.dsort_totals = take((size_t)RADIX * 4);
+    L.dsort_minmax = take((size_t)radix_blocks(P, dsort_items(P)) * 8);
+    L.dsort_ctrl = take(CTRL_WORDS * 4);
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
-    L.order_cnt = take((8 * 32 + 1) * 4);
+    L.emit_super = take((size_t)rg_blocks(P) * 4 + 4);
+    L.order_cnt = take((8 * 32 + 2) * 4);
+    L.accum = take((size_t)(P > 0 ? P : 1) * 16 * 4);
     L.bytes = o;
     return L;
 }
@@ -190,6 +205,11 @@ __host__ __device__ inline ImgLayout img_layout(int W, int H) {
 }
 
 constexpr int ACCUM_STRIDE = 16;  // floats per Gaussian in the backward accumulator (64 B row)
+// flag words after the 8 x 32 wave-order counts in GeomLayout::order_cnt
+enum OrderFlag {
+    ORDER_FILED = 8 * 32,  // the quadrants are filed in img.qlist (by the forward's prepare or a backward)
+    ORDER_FRESH,           // geom's accumulator is zeroed and unused (the forward's prepare; render_bwd clears it)
+};
 enum AccumSlot {
     ACC_MEAN2D_X = 0,
     ACC_MEAN2D_Y,

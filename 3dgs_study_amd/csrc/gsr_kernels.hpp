@@ -13,8 +13,9 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
                                hipStream_t s);
 
 // binning.hip
-hipError_t launch_depth_sort(int P, int W, int H, void *geom, hipStream_t s);
-hipError_t launch_depth_sort_tail(int P, int W, int H, void *geom, bool fourth_pass, hipStream_t s);
+hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
+                             hipStream_t s);
+hipError_t launch_rank_gather(int P, int W, int H, void *geom, hipStream_t s);
 hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
                        hipStream_t s);
 hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, hipStream_t s);
@@ -27,7 +28,7 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
 
 // render_bwd.hip
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
-                              hipStream_t s);
+                              bool internal, bool forward, hipStream_t s);
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
                              const void *img, const float *dL_dpix, float *accum, hipStream_t s);
 

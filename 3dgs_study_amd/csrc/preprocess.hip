@@ -30,7 +30,7 @@ struct PreArgs {
     uint4 *rects;  // tile rect {x0 | x1 << 16, y0 | y1 << 16} + 64-bit tile mask per Gaussian (binning.hip)
     uint2 *ranges;           // [T] zeroed here (empty tiles keep (0, 0); binning.hip fills the rest)
     int tiles;
-    uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, key min, key max, 0}
+    uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, 0, 0, 0}
     int32_t *radii;
     uint32_t *order_cnt;
 };
@@ -106,8 +106,8 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     } else if (use_sh) {
         rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
     }
-    uint32_t touched = 0, key = 0;
-    bool perr = false, key_vis = false;
+    uint32_t touched = 0;
+    bool perr = false;
     // what the colour stage (after the barrier) needs
     bool emit = false;
     float px = 0.f, py = 0.f, conic_x = 0.f, conic_y = 0.f, conic_z = 0.f, qmax = 0.f, depth = 0.f;
@@ -206,13 +206,9 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 rect_out = make_uint4(rc.x0 | (rc.x1 << 16), rc.y0 | (rc.y1 << 16), (uint32_t)m, (uint32_t)(m >> 32));
             }
         }
-        // depth keys of invisible Gaussians: +inf bits, sorted behind every visible one
-        if (radius_out) {
-            key = __float_as_uint(p_view.z);
-            key_vis = true;
-        } else {
-            a.depths[idx] = __uint_as_float(0x7f800000u);
-        }
+        // depths of invisible Gaussians: +inf (the depth sort keys its candidates
+        // itself, binning.hip depth_keys_kernel)
+        if (!radius_out) a.depths[idx] = __uint_as_float(0x7f800000u);
         a.radii[idx] = radius_out;
         a.tiles_touched[idx] = touched;
         a.rects[idx] = rect_out;
@@ -221,7 +217,10 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     // hold up its waits for the per-Gaussian loads)
     for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
     if (idx < 8 * ORDER_NBUCKET) a.order_cnt[idx] = 0u;  // the backward wave-order buckets (render_bwd.hip)
-    if (idx == 0) a.order_cnt[8 * ORDER_NBUCKET] = 0u;     // and the "filed" flag (one block may be all there is)
+    if (idx == 0) {  // and the flag words (one block may be all there is)
+        a.order_cnt[ORDER_FILED] = 0u;
+        a.order_cnt[ORDER_FRESH] = 0u;
+    }
     // colour stage: the SH rows land in LDS now, after the geometry
     if (use_sh && !DIRECT) __syncthreads();
     if (emit) {
@@ -257,29 +256,10 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         a.clamped[idx] = clampbits;
     }
     // num_rendered is only a total (emit works in depth order, binning.hip): each
-    // workgroup stores its sum (bit 31 flags a prefiltered violation) and the
-    // range of its visible depth keys (the depth sort drops constant top bits)
+    // workgroup stores its sum (bit 31 flags a prefiltered violation)
     const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
     const int berr = __syncthreads_or(perr);
-    uint32_t kmin = key_vis ? key : 0xffffffffu, kmax = key_vis ? key : 0u;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
-        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
-    }
-    __shared__ uint32_t wmin[PRE_THREADS / 64], wmax[PRE_THREADS / 64];
-    if ((threadIdx.x & 63) == 0) {
-        wmin[threadIdx.x >> 6] = kmin;
-        wmax[threadIdx.x >> 6] = kmax;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < PRE_THREADS / 64; k++) {
-            kmin = min(kmin, wmin[k]);
-            kmax = max(kmax, wmax[k]);
-        }
-        a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), kmin, kmax, 0u);
-    }
+    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), 0u, 0u, 0u);
 }
 
 // One workgroup totals the block sums and publishes num_rendered and the error
@@ -289,9 +269,9 @@ constexpr int TOTAL_THREADS = 1024;
 __global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint4 *sums, int n, uint32_t *ctrl,
                                                                       uint32_t *host_ctrl) {
     __shared__ unsigned long long part[TOTAL_THREADS / 64];
-    __shared__ uint32_t perr[TOTAL_THREADS / 64], pmin[TOTAL_THREADS / 64], pmax[TOTAL_THREADS / 64];
+    __shared__ uint32_t perr[TOTAL_THREADS / 64];
     unsigned long long t = 0;
-    uint32_t e = 0, kmin = 0xffffffffu, kmax = 0u;
+    uint32_t e = 0;
     // 8 loads in flight per thread (one at a time: 12 us for config E's 19.5k
     // workgroup records, on the host's critical path)
     constexpr int U = 8;
@@ -300,43 +280,32 @@ __global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint
 #pragma unroll
         for (int j = 0; j < U; j++) {
             const int i = i0 + j * TOTAL_THREADS;
-            v[j] = i < n ? sums[i] : make_uint4(0u, 0xffffffffu, 0u, 0u);
+            v[j] = i < n ? sums[i] : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
         for (int j = 0; j < U; j++) {
             t += v[j].x & 0x7fffffffu;
             e |= v[j].x >> 31;
-            kmin = min(kmin, v[j].y);
-            kmax = max(kmax, v[j].z);
         }
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
         t += __shfl_xor(t, o);
         e |= __shfl_xor(e, o);
-        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
-        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
     }
     if ((threadIdx.x & 63) == 0) {
         part[threadIdx.x >> 6] = t;
         perr[threadIdx.x >> 6] = e;
-        pmin[threadIdx.x >> 6] = kmin;
-        pmax[threadIdx.x >> 6] = kmax;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int k = 1; k < TOTAL_THREADS / 64; k++) {
             t += part[k];
             e |= perr[k];
-            kmin = min(kmin, pmin[k]);
-            kmax = max(kmax, pmax[k]);
         }
-        const bool any = kmin <= kmax;
-        ctrl[CTRL_KEY_BASE] = any ? kmin : 0u;
-        ctrl[CTRL_DSORT_PASSES] = any && kmax - kmin > 0xffffffu ? 4u : 3u;
-        const uint32_t w[4] = {(uint32_t)t, (uint32_t)(t >> 32), e, ctrl[CTRL_DSORT_PASSES]};
-        for (int k = 0; k < 4; k++) {
-            if (k < 3) ctrl[k] = w[k];
+        const uint32_t w[3] = {(uint32_t)t, (uint32_t)(t >> 32), e};
+        for (int k = 0; k < 3; k++) {
+            ctrl[k] = w[k];
             __hip_atomic_store(&host_ctrl[k], w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __threadfence_system();

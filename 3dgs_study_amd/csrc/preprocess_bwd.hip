@@ -234,9 +234,16 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
             else
                 for (int k = 0; k < RW; k++) row[k] = 0.f;
         }
-        a.o.dmeans3D[3 * (size_t)idx + 0] = dmean.x;
-        a.o.dmeans3D[3 * (size_t)idx + 1] = dmean.y;
-        a.o.dmeans3D[3 * (size_t)idx + 2] = dmean.z;
+        float *dm = a.o.dmeans3D + 3 * (size_t)idx;
+        if (a.o.leaf.accumulate & 16) {  // AccumulateGrad of the _xyz leaf: grad += new
+            dm[0] += dmean.x;
+            dm[1] += dmean.y;
+            dm[2] += dmean.z;
+        } else {
+            dm[0] = dmean.x;
+            dm[1] = dmean.y;
+            dm[2] = dmean.z;
+        }
     }
     if constexpr (DIRECT) {
         if (live && a.o.dsh) {
@@ -344,10 +351,7 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
     ShStage st{};
     st.vis = rad > 0;
     if (!st.vis) {
-        for (int k = 0; k < 3; k++) {
-            o.dmeans2D[3 * (size_t)idx + k] = 0.f;
-            o.dmeans3D[3 * (size_t)idx + k] = 0.f;
-        }
+        for (int k = 0; k < 3; k++) o.dmeans2D[3 * (size_t)idx + k] = 0.f;
         if (o.dcolors)
             for (int k = 0; k < 3; k++) o.dcolors[3 * (size_t)idx + k] = 0.f;
         if (o.drgb)
@@ -356,7 +360,7 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
             for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = 0.f;
         const float zs[3] = {0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
         write_activation_grads(a, idx, 0.f, opac, zs, zq, gin, has_sr);
-        return st;  // dmeans3D (zero) and the dsh row are written by the caller
+        return st;  // dmeans3D (st.dmean = 0) and the dsh row are written by the caller
     }
     const float dcol[3] = {acc1.z, acc1.w, accb};
     if (o.dcolors) {  // NULL: no precomputed colours to differentiate (the caller discards it)

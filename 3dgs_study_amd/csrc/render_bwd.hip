@@ -31,7 +31,7 @@ namespace gsr {
 struct RenderBwdArgs {
     int W, H, gx, tiles;
     const uint32_t *order_cnt;  // [8][ORDER_NBUCKET] quadrants per (XCD, work bucket)
-    uint32_t *filed;            // order_cnt[8][ORDER_NBUCKET]: set once the lists are in use
+    uint32_t *flags;            // order_cnt + ORDER_FILED: the OrderFlag words
     const uint32_t *qlist;      // [8][ORDER_NBUCKET][maxc]
     int maxc;
     const uint2 *ranges;
@@ -80,7 +80,10 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
     // workgroup 8 r + x: XCD x's r-th quadrant in bucket order (gsr_blend.hpp)
     const int lane = threadIdx.x & 63;
-    if (blockIdx.x == 0 && lane == 0) *a.filed = 1u;  // a second backward of this forward reuses the lists
+    if (blockIdx.x == 0 && lane == 0) {  // a second backward of this forward reuses the lists, and re-zeroes
+        a.flags[0] = 1u;                 // ORDER_FILED
+        a.flags[1] = 0u;                 // ORDER_FRESH
+    }
     const int quad = ordered_quad(a.order_cnt, a.qlist, a.maxc);
     if (quad < 0) return;
     const int tile = (int)(quad >> 2), w = (int)(quad & 3);
@@ -304,27 +307,40 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     }
 }
 
-// The backward's first launch: zeroes the accumulator rows (in place of a memset
+// The backward's preparation: zeroes the accumulator rows (in place of a memset
 // launch) and files every quadrant under (its XCD, the work bucket the forward
 // stored) for render_bwd_kernel's wave order: per wave of 64 quadrants, ONE
 // returning atomic instruction, each distinct (XCD, bucket) cell's lowest lane
 // reserving its peers' slots (a dependent atomic per cell cost ~20 us of latency).
-// A second backward of the same forward (retain_graph) finds the lists filed and
-// only zeroes.
+// In the backward (forward == 0) it is the first launch, and skips what a forward
+// called with GSR_FLAG_PREPARE_BACKWARD did already (the flag words); a second
+// backward of the same forward (retain_graph) finds the lists filed and only
+// zeroes.  In that forward (forward == 1) it files, after render_fwd, and marks
+// the flags (its accumulator was zeroed beside render_fwd, abi.hip).
 struct BwdPrepArgs {
     float4 *accum4;
     size_t n4;
     const uint8_t *qbucket;
-    uint32_t *order_cnt;  // [8][ORDER_NBUCKET] + the filed flag
+    uint32_t *order_cnt;  // [8][ORDER_NBUCKET] + the OrderFlag words
     uint32_t *qlist;
     int nq, maxc;
+    int internal;         // accum4 is geom's accumulator (ORDER_FRESH applies to it)
+    int forward;
 };
 constexpr int PREP_THREADS = 256;
 __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a) {
     const size_t tid = (size_t)blockIdx.x * PREP_THREADS + threadIdx.x;
     const size_t nthreads = (size_t)gridDim.x * PREP_THREADS;
-    for (size_t i = tid; i < a.n4; i += nthreads) a.accum4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.nq <= 0 || a.order_cnt[8 * ORDER_NBUCKET] != 0u) return;  // nothing to file / already filed
+    if (a.forward) {
+        // the next kernel (a backward's first) reads these; no block of this one does
+        if (tid == 0) {
+            a.order_cnt[ORDER_FILED] = 1u;
+            a.order_cnt[ORDER_FRESH] = 1u;
+        }
+    } else if (!(a.internal && a.order_cnt[ORDER_FRESH] != 0u)) {
+        for (size_t i = tid; i < a.n4; i += nthreads) a.accum4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (a.nq <= 0 || (!a.forward && a.order_cnt[ORDER_FILED] != 0u)) return;  // nothing to file / already filed
     const int lane = threadIdx.x & 63;
     for (size_t q0 = tid - (size_t)lane; q0 < (size_t)a.nq; q0 += nthreads) {  // wave-uniform
         const int q = (int)q0 + lane;
@@ -343,15 +359,16 @@ __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a
         uint32_t base = 0;
         if (cell >= 0 && lane == leader) base = atomicAdd(&a.order_cnt[cell], (uint32_t)__builtin_popcountll(peers));
         base = (uint32_t)__shfl((int)base, leader);
-        if (cell >= 0)
-            a.qlist[(size_t)cell * a.maxc + base +
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u))] =
-                (uint32_t)q;
+        // (a cell never holds more than maxc quadrants: the guard only keeps a
+        // mis-sequenced caller — lists filed twice — from writing past the cell)
+        const uint32_t slot =
+            base + __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+        if (cell >= 0 && slot < (uint32_t)a.maxc) a.qlist[(size_t)cell * a.maxc + slot] = (uint32_t)q;
     }
 }
 
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
-                              hipStream_t s) {
+                              bool internal, bool forward, hipStream_t s) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -363,7 +380,9 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
     a.qlist = at<uint32_t>(const_cast<void *>(img), Im.qlist);
     a.nq = file ? 4 * g.tiles : 0;
     a.maxc = order_max_per_xcd(4 * g.tiles);
-    const size_t want = (a.n4 + PREP_THREADS - 1) / PREP_THREADS;
+    a.internal = internal ? 1 : 0;
+    a.forward = forward ? 1 : 0;
+    const size_t want = forward ? ((size_t)a.nq + PREP_THREADS - 1) / PREP_THREADS : (a.n4 + PREP_THREADS - 1) / PREP_THREADS;
     const int blocks = (int)(want < 2048 ? (want > 0 ? want : 1) : 2048);
     hipLaunchKernelGGL(bwd_prepare_kernel, dim3(blocks), dim3(PREP_THREADS), 0, s, a);
     return hipGetLastError();
@@ -388,7 +407,7 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.dL_dpix = dL_dpix;
     a.accum = accum;
     a.order_cnt = at<uint32_t>(geom, G.order_cnt);
-    a.filed = at<uint32_t>(const_cast<void *>(geom), G.order_cnt) + 8 * ORDER_NBUCKET;
+    a.flags = at<uint32_t>(const_cast<void *>(geom), G.order_cnt) + ORDER_FILED;
     a.qlist = at<uint32_t>(img, Im.qlist);
     a.maxc = order_max_per_xcd(4 * g.tiles);
     hipLaunchKernelGGL(render_bwd_kernel, dim3(8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);

@@ -38,7 +38,7 @@ class GsrInputs(ctypes.Structure):
         ("W", ctypes.c_int32), ("H", ctypes.c_int32),
         ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float), ("scale_modifier", ctypes.c_float),
         ("prefiltered", ctypes.c_int32), ("debug", ctypes.c_int32),
-        ("footprint", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("footprint", ctypes.c_int32), ("flags", ctypes.c_int32),
         ("bg", ctypes.c_void_p), ("means3D", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
         ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p), ("rotations", ctypes.c_void_p),
         ("cov3D_precomp", ctypes.c_void_p), ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
@@ -56,7 +56,7 @@ EXPORTED = (
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
-    "gsr_build_id",
+    "gsr_build_id", "gsr_backward_phase",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -101,18 +101,23 @@ class LeafGrads:
     leaf gradients of the caller's activations written by the library itself
     (gsr_backward_leaves, include/gsr.h).  Every tensor is float32, contiguous, on
     the rasterizer's device; ``accumulate`` bits add into an output instead of
-    overwriting it (1 dsh, 2 dscaling, 4 dopacity, 8 drotation).  ``dopacity``
-    needs the backward's ``opacities``; ``drotation`` needs ``rotation_norm`` (the
-    norms torch's F.normalize computed, [P,1])."""
+    overwriting it (1 dsh, 2 dscaling, 4 dopacity, 8 drotation, 16 dmeans3D).
+    ``dopacity`` needs the backward's ``opacities``; ``drotation`` needs
+    ``rotation_norm`` (the norms torch's F.normalize computed, [P,1]).
+    ``dmeans3D`` [P,3]: where the backward writes (or, bit 16, adds) its means3D
+    gradient instead of a fresh tensor (means3D is the _xyz leaf itself: the
+    caller points it at that leaf's gradient, e.g. a slice of an all-reduce
+    bucket); the returned dmeans3D is then None."""
 
     _SHAPES = {"dsh_dc": lambda P, M: (P, 1, 3), "dsh_rest": lambda P, M: (P, M - 1, 3),
                "dscaling": lambda P, M: (P, 3), "dopacity": lambda P, M: (P, 1), "drotation": lambda P, M: (P, 4),
                "rotation_norm": lambda P, M: (P, 1)}
 
     def __init__(self, dsh_dc=None, dsh_rest=None, dscaling=None, dopacity=None, drotation=None,
-                 rotation_norm=None, rotation_eps=1e-12, accumulate=0):
+                 rotation_norm=None, rotation_eps=1e-12, accumulate=0, dmeans3D=None):
         self.dsh_dc, self.dsh_rest, self.dscaling, self.dopacity, self.drotation = (dsh_dc, dsh_rest, dscaling,
                                                                                     dopacity, drotation)
+        self.dmeans3D = dmeans3D
         self.rotation_norm = rotation_norm
         self.rotation_eps, self.accumulate = float(rotation_eps), int(accumulate)
 
@@ -139,7 +144,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib = None
 
@@ -179,6 +184,9 @@ def load_library():
     lib.gsr_backward_planar.restype = ctypes.c_int
     lib.gsr_backward_leaves.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [ctypes.POINTER(GsrLeafGrads), vp]
     lib.gsr_backward_leaves.restype = ctypes.c_int
+    lib.gsr_backward_phase.argtypes = ([pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 9 +
+                                       [ctypes.POINTER(GsrLeafGrads), i32, vp])
+    lib.gsr_backward_phase.restype = ctypes.c_int
     for name in ("gsr_backward_colors", "gsr_backward_colors_render", "gsr_backward_colors_finish"):
         getattr(lib, name).argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
         getattr(lib, name).restype = ctypes.c_int
@@ -247,12 +255,30 @@ def _prep(t, name, device):
     return t if t.is_contiguous() else t.contiguous()
 
 
+# Test hook (tests/test_poisoned_scratch.py): a byte value every output and scratch
+# buffer the entry points allocate is filled with, instead of being left
+# uninitialised (None, the default).  0xFF makes every float a NaN and every integer
+# all ones, so a kernel that reads a word the same call did not write (a stale
+# flag or counter the caching allocator handed back) shows up.
+_poison = None
+
+
+def _alloc(shape, dtype, device):
+    if _poison is None:
+        return torch.empty(shape, dtype=dtype, device=device)
+    n = math.prod(shape) * torch.tensor([], dtype=dtype).element_size()
+    return torch.full((n,), _poison, dtype=torch.uint8, device=device).view(dtype).view(shape)
+
+
 def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+FLAG_PREPARE_BACKWARD = 1  # gsr.h gsr_flags
+
+
 def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
-            tan_fovx, tan_fovy, H, W, sh, degree, campos, prefiltered, debug, footprint=None):
+            tan_fovx, tan_fovy, H, W, sh, degree, campos, prefiltered, debug, footprint=None, flags=0):
     if means3D.ndim != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     device = means3D.device
@@ -269,7 +295,7 @@ def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov
     M = sh_t.size(1) if (sh_t is not None and sh_t.size(0) != 0) else 0
     s = GsrInputs(P=P, D=int(degree), M=M, W=int(W), H=int(H), tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
                   scale_modifier=float(scale_modifier), prefiltered=int(bool(prefiltered)), debug=int(bool(debug)),
-                  footprint=FOOTPRINTS[footprint or _footprint],
+                  footprint=FOOTPRINTS[footprint or _footprint], flags=int(flags),
                   bg=_ptr(keep["background"]), means3D=_ptr(keep["means3D"]), colors_precomp=_ptr(keep["colors"]),
                   opacities=_ptr(keep["opacity"]), scales=_ptr(keep["scales"]), rotations=_ptr(keep["rotations"]),
                   cov3D_precomp=_ptr(keep["cov3D_precomp"]), viewmatrix=_ptr(keep["viewmatrix"]),
@@ -279,19 +305,26 @@ def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, debug, footprint=None):
+                        prefiltered, debug, footprint=None, prepare_backward=None):
     """-> (num_rendered, color [3,H,W], radii [P] int32, geomBuffer, binningBuffer, imgBuffer)
 
     ``footprint`` (keyword, not upstream): "rect" | "tight" for this call; None =
-    the module setting (``set_footprint``, env GSR_FOOTPRINT, default "tight")."""
+    the module setting (``set_footprint``, env GSR_FOOTPRINT, default "tight").
+    ``prepare_backward`` (keyword, not upstream; gsr.h GSR_FLAG_PREPARE_BACKWARD):
+    also zero the backward's accumulator beside the blend; None = when grad mode is
+    on and an input requires grad.  A speed hint only."""
+    if prepare_backward is None:
+        prepare_backward = torch.is_grad_enabled() and any(
+            isinstance(t, torch.Tensor) and t.requires_grad
+            for t in (means3D, colors, opacity, scales, rotations, cov3D_precomp, sh))
     return _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                       viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                      prefiltered, debug, footprint)[:6]
+                      prefiltered, debug, footprint, prepare_backward)[:6]
 
 
 def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
                projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-               footprint=None):
+               footprint=None, prepare_backward=False):
     """rasterize_gaussians plus its validated inputs ``(struct, kept tensors, device,
     M)``, which the autograd Function hands back to the backward (``inputs=``) so the
     same tensors are not re-checked there: the host's backward path is on the
@@ -302,18 +335,17 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
         raise ValueError(f"footprint must be one of {sorted(FOOTPRINTS)} (got {footprint!r})")
     s, keep, device, M = _inputs(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos,
-                                 prefiltered, debug, footprint)
+                                 prefiltered, debug, footprint, FLAG_PREPARE_BACKWARD if prepare_backward else 0)
     P = s.P
-    u8 = dict(dtype=torch.uint8, device=device)
-    out_color = torch.empty((3, H, W), dtype=torch.float32, device=device)
-    radii = torch.empty((P,), dtype=torch.int32, device=device)
-    geom = torch.empty((lib.gsr_geom_bytes(P, W, H),), **u8)
-    img = torch.empty((lib.gsr_img_bytes(W, H),), **u8)
+    out_color = _alloc((3, H, W), torch.float32, device)
+    radii = _alloc((P,), torch.int32, device)
+    geom = _alloc((lib.gsr_geom_bytes(P, W, H),), torch.uint8, device)
+    img = _alloc((lib.gsr_img_bytes(W, H),), torch.uint8, device)
     stream = _stream(device)
     num_rendered = ctypes.c_int64(0)
     _check(lib.gsr_forward_preprocess(ctypes.byref(s), geom.data_ptr(), _ptr(radii), ctypes.byref(num_rendered),
                                       stream), "rasterize_gaussians (preprocess)")
-    binning = torch.empty((lib.gsr_binning_bytes(num_rendered.value, W, H),), **u8)
+    binning = _alloc((lib.gsr_binning_bytes(num_rendered.value, W, H),), torch.uint8, device)
     _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
                                   num_rendered.value, _ptr(radii), out_color.data_ptr(), stream),
            "rasterize_gaussians (render)")
@@ -335,10 +367,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     ``on_drgb`` (with ``drgb_out``) — called once drgb is queued on the stream and
     before the per-Gaussian backward is (gsr_backward_colors_render / _finish), so
     the caller can start exchanging drgb under it.
-    ``leaf`` — a ``LeafGrads`` (diff_gaussian_rasterization.leaf_grads): the library
-    writes the requested leaf gradients of the caller's activations itself
-    (gsr_backward_leaves) and returns None in place of the activation gradients
-    they replace (dsh, dopacity, dscales, drot).
+    ``leaf`` — a ``LeafGrads``: the library writes the requested leaf gradients of
+    the caller's activations itself (gsr_backward_phase) and returns None in place
+    of the activation gradients they replace (dsh, dopacity, dscales, drot, and
+    dmeans3D when ``leaf.dmeans3D`` is given); it combines with ``drgb_out`` (the
+    exchange takes the SH gradient, the library writes the other leaves).
     ``opacities`` — the forward's opacity input [P,1] (upstream's backward reads
     it from the geom buffer; passed here it is read coalesced); required with a
     leaf opacity gradient.
@@ -351,15 +384,19 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                          viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
     s, keep, device, M = inputs
     P = s.P
-    if leaf is not None and drgb_out is not None:
-        raise RuntimeError("rasterize_gaussians_backward: leaf and drgb_out are exclusive")
-    f32 = dict(dtype=torch.float32, device=device)
-    empty = lambda *shape: torch.empty(shape, **f32)  # noqa: E731
+    empty = lambda *shape: _alloc(shape, torch.float32, device)  # noqa: E731
     # on the leaf path the gradients it replaces, and those of absent inputs
     # (upstream's zeros, discarded by the autograd wrapper: 36 B per Gaussian), are
     # neither allocated nor written
     bare = leaf is not None
-    dmeans2D, dmeans3D = empty(P, 3), empty(P, 3)
+    own_xyz = bare and leaf.dmeans3D is not None
+    if own_xyz:
+        t = leaf.dmeans3D
+        if t.dtype != torch.float32 or t.device != device or not t.is_contiguous() or t.numel() != 3 * P:
+            raise RuntimeError(f"leaf gradient dmeans3D: expected a contiguous float32 tensor of shape ({P}, 3) "
+                               f"on {device}")
+    dmeans2D = empty(P, 3)
+    dmeans3D = leaf.dmeans3D if own_xyz else empty(P, 3)
     dcolors = None if bare and keep["colors"] is None else empty(P, 3)
     dcov3D = None if bare and keep["cov3D_precomp"] is None else empty(P, 6)
     dopacity = None if bare and leaf.dopacity is not None else empty(P, 1)
@@ -371,38 +408,36 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         dsh = empty(M, P, 3).permute(1, 0, 2)
     else:
         dsh = empty(P, M, 3)
+    ret = (dmeans2D, dcolors, dopacity, None if own_xyz else dmeans3D, dcov3D, dsh, dscales, drot)
     if P == 0:
-        return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
-    accum = torch.empty((lib.gsr_accum_bytes(P),), dtype=torch.uint8, device=device)
+        return ret
     grad = _prep(dL_dout_color, "dL_dout_color", device)
     if not radii.is_contiguous():
         radii = radii.contiguous()
-    if drgb_out is not None:
-        if (drgb_out.dtype != torch.float32 or drgb_out.device != device or not drgb_out.is_contiguous()
-                or drgb_out.numel() < 3 * P):
-            raise RuntimeError("drgb_out must be a contiguous float32 tensor of >= 3P elements on the input device")
-        fn, last = lib.gsr_backward_colors, drgb_out.data_ptr()
-    elif dsh_planar and dsh is not None and M > 0 and P > 0:
-        fn, last = lib.gsr_backward_planar, dsh.data_ptr()
-    else:
-        fn, last = lib.gsr_backward, _ptr(dsh)
-    if leaf is not None:
-        fn, last = lib.gsr_backward_leaves, _ptr(dsh)
-    head = lambda: (ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),  # noqa: E731
-                    binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
-                    int(R), grad.data_ptr(), accum.data_ptr(), dmeans2D.data_ptr(), _ptr(dcolors),
-                    _ptr(dopacity), dmeans3D.data_ptr(), _ptr(dcov3D), last, _ptr(dscales), _ptr(drot))
-    call = lambda f: f(*head(), _stream(device))  # noqa: E731
-    if leaf is not None:
-        lg = leaf.struct(P, M, device, dsh_planar)
-        _check(lib.gsr_backward_leaves(*head(), ctypes.byref(lg), _stream(device)), "rasterize_gaussians_backward")
-    elif drgb_out is not None and on_drgb is not None:
-        _check(call(lib.gsr_backward_colors_render), "rasterize_gaussians_backward")
+    if drgb_out is not None and (drgb_out.dtype != torch.float32 or drgb_out.device != device
+                                 or not drgb_out.is_contiguous() or drgb_out.numel() < 3 * P):
+        raise RuntimeError("drgb_out must be a contiguous float32 tensor of >= 3P elements on the input device")
+    head = (ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),
+            binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(), int(R),
+            grad.data_ptr(), None, dmeans2D.data_ptr(), _ptr(dcolors), _ptr(dopacity),
+            dmeans3D.data_ptr(), _ptr(dcov3D))
+    stream = _stream(device)
+    if leaf is None and drgb_out is None:
+        fn = lib.gsr_backward_planar if dsh_planar and dsh is not None and M > 0 else lib.gsr_backward
+        _check(fn(*head, _ptr(dsh), _ptr(dscales), _ptr(drot), stream), "rasterize_gaussians_backward")
+        return ret
+    # gsr_backward_phase: the leaf gradients and / or the exchange's colour gradient
+    lg = ctypes.byref(leaf.struct(P, M, device, dsh_planar)) if leaf is not None else None
+    tail = (_ptr(dsh), _ptr(drgb_out), _ptr(dscales), _ptr(drot), lg)
+    if drgb_out is not None and on_drgb is not None:
+        # the colour gradient is queued before the per-Gaussian backward: the
+        # caller starts exchanging it under that
+        _check(lib.gsr_backward_phase(*head, *tail, 1, stream), "rasterize_gaussians_backward")
         on_drgb()
-        _check(call(lib.gsr_backward_colors_finish), "rasterize_gaussians_backward")
+        _check(lib.gsr_backward_phase(*head, *tail, 2, stream), "rasterize_gaussians_backward")
     else:
-        _check(call(fn), "rasterize_gaussians_backward")
-    return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
+        _check(lib.gsr_backward_phase(*head, *tail, 3, stream), "rasterize_gaussians_backward")
+    return ret
 
 
 def sh_record_floats(P: int) -> int:

@@ -17,11 +17,14 @@ Autograd: ``backward`` maps the 8 native gradients onto the 9 inputs
 cov3Ds_precomp, raster_settings)``; ``means2D.grad[:, :2]`` (NDC-scaled screen-space
 gradient) feeds densification at ``scene/gaussian_model.py:576-580``.
 
-View-parallel SH exchange (not upstream; ``3dgs_study_amd/multiview.py``): while a
-sink is installed with ``set_sh_grad_sink``, a backward with SH input hands the
-sink the view's colour gradient instead of returning dsh (the ``sh`` input then
-gets no gradient through autograd; the sink rebuilds the SH leaf gradients summed
-over all ranks' views).  ``set_sh_grad_sink(None)`` restores upstream behaviour.
+View-parallel gradient exchange (not upstream; ``3dgs_study_amd/multiview.py``):
+while an exchange is installed with ``set_grad_exchange`` (alias
+``set_sh_grad_sink``), a backward with SH input may hand it the view's colour
+gradient instead of returning dsh (the ``sh`` input then gets no gradient through
+autograd; the exchange rebuilds the SH leaf gradients summed over all ranks'
+views), and the fused leaf gradients below are written straight into the
+exchange's all-reduce bucket.  ``set_grad_exchange(None)`` restores upstream
+behaviour.
 
 Tile footprint (not upstream; ``set_footprint``, env ``GSR_FOOTPRINT``): "rect"
 bins every tile of upstream's getRect rect, so ``num_rendered`` and the binning
@@ -46,20 +49,38 @@ from . import _C
 from ._C import get_footprint, set_footprint  # noqa: E402
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "set_sh_grad_sink",
-           "set_footprint", "get_footprint", "set_fused_leaf_grads"]
+           "set_grad_exchange", "set_footprint", "get_footprint", "set_fused_leaf_grads"]
 
-_sh_grad_sink = None
-_fused_leaf_grads = os.environ.get("GSR_FUSED_LEAF_GRADS", "1") != "0"
-last_leaf_plan = ()  # the activations whose leaf gradients the last backward wrote itself
+_exchange = None
+# None = automatic (on, except in a multi-rank process group with no exchange of
+# ours installed: DDP's reducer hooks AccumulateGrad nodes from C++, where the plan
+# cannot see them); True / False = forced (env GSR_FUSED_LEAF_GRADS=1 / 0)
+_fused_leaf_grads = {"0": False, "1": True}.get(os.environ.get("GSR_FUSED_LEAF_GRADS", ""))
+last_leaf_plan = ()  # the inputs whose leaf gradients the last backward wrote itself
 
 
-def set_fused_leaf_grads(on: bool) -> bool:
-    """Enable (default; env GSR_FUSED_LEAF_GRADS=0 disables) writing the leaf
-    gradients of the caller's activations from the rasterizer backward (see
-    ``_leaf_plan``); returns the previous setting."""
+def set_fused_leaf_grads(on) -> object:
+    """Writing the leaf gradients of the caller's activations from the rasterizer
+    backward (see ``_leaf_plan``): True / False forces it on / off, None (the
+    default) = on unless torch.distributed runs more than one rank without an
+    exchange of this package installed (a DDP-wrapped model: its reducer's
+    AccumulateGrad hooks are invisible here).  Returns the previous setting."""
     global _fused_leaf_grads
-    prev, _fused_leaf_grads = _fused_leaf_grads, bool(on)
+    prev, _fused_leaf_grads = _fused_leaf_grads, (None if on is None else bool(on))
     return prev
+
+
+def _fusion_on(ex) -> bool:
+    if _fused_leaf_grads is not None:
+        return _fused_leaf_grads
+    if ex is not None:
+        return True
+    try:
+        import torch.distributed as dist
+
+        return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+    except (ImportError, RuntimeError, ValueError):
+        return True
 
 
 # ---------------------------------------------------------------- fused leaf gradients
@@ -74,20 +95,26 @@ def set_fused_leaf_grads(on: bool) -> bool:
 # torch's operation order (bit-identical results), and the Function returns None
 # for that input, so torch skips the activation's backward.  Anything else keeps
 # upstream's path for that input: another graph shape, hooks on the activation or
-# the leaf (tensor hooks, retain_grad, post-accumulate hooks: the view-parallel
-# exchange's all-reduce hooks), create_graph, autograd.grad / backward(inputs=...)
+# the leaf (tensor hooks, retain_grad, post-accumulate hooks other than the
+# installed exchange's own), create_graph, autograd.grad / backward(inputs=...)
 # not accumulating into the leaf, or an existing .grad that is not a dense
 # contiguous float32 tensor.  Hooks registered directly on an AccumulateGrad node
-# are invisible from Python: such callers disable this with set_fused_leaf_grads.
+# are invisible from Python (DDP's): _fusion_on turns the path off by itself in a
+# multi-rank group without our exchange, and set_fused_leaf_grads(False) always.
+# With an exchange that offers an all-reduce bucket (multiview.GradAllReduce at
+# N > 1) the means3D input — the _xyz leaf itself — joins the plan, and every
+# planned gradient is written into the bucket, whose single all-reduce the
+# exchange starts when the backward ends.
 def _acc_leaf(node):
     return node.variable if node is not None and type(node).__name__ == "AccumulateGrad" else None
 
 
-def _leaf_state(leaf, shape, device):
+def _leaf_state(leaf, shape, device, ex=None):
     """-1: not fusable; 0: no .grad yet (write it); 1: add into the existing .grad."""
     if (leaf is None or not leaf.is_leaf or not leaf.requires_grad or leaf.dtype is not torch.float32
-            or leaf.device != device or leaf.shape != shape or not leaf.is_contiguous()
-            or leaf._backward_hooks or getattr(leaf, "_post_accumulate_grad_hooks", None)):
+            or leaf.device != device or leaf.shape != shape or not leaf.is_contiguous() or leaf._backward_hooks):
+        return -1
+    if getattr(leaf, "_post_accumulate_grad_hooks", None) and not (ex is not None and ex.owns_hooks(leaf)):
         return -1
     g = leaf.grad
     if g is None:
@@ -109,14 +136,17 @@ def _will_run(node) -> bool:
         return False
 
 
-def _leaf_plan(sh, colors_precomp, opacities, scales, rotations, needs, sink_takes_sh):
-    """{name: (leaf tensors, state, extras)} for the activations whose leaf gradients
-    the backward may write itself (see above); called inside backward."""
+def _leaf_plan(ctx, needs, sh, colors_precomp, opacities, scales, rotations, means3D, sink_takes_sh, ex):
+    """{name: (leaf tensors, state, extras, bucket views or None)} for the inputs
+    whose leaf gradients the backward may write itself (see above); called inside
+    backward.  ``needs``: needs_input_grad in _RasterizeGaussians' input order;
+    ``ctx.next_functions[0]`` is means3D's."""
     if torch.is_grad_enabled():  # create_graph: the activations' backwards must be recorded
         return {}
     plan = {}
     device = opacities.device
     P = opacities.shape[0]
+    st = lambda leaf, shape: _leaf_state(leaf, shape, device, ex)  # noqa: E731
     try:
         if needs[2] and not sink_takes_sh and sh.numel() and colors_precomp.numel() == 0 and _plain_activation(sh):
             n = sh.grad_fn
@@ -124,7 +154,7 @@ def _leaf_plan(sh, colors_precomp, opacities, scales, rotations, needs, sink_tak
             if len(nf) == 2 and n._saved_dim in (1, -2) and sh.dim() == 3 and sh.shape[2] == 3:
                 M = sh.shape[1]
                 dc, rest = _acc_leaf(nf[0][0]), _acc_leaf(nf[1][0])
-                a, b = _leaf_state(dc, (P, 1, 3), device), _leaf_state(rest, (P, M - 1, 3), device)
+                a, b = st(dc, (P, 1, 3)), st(rest, (P, M - 1, 3))
                 if a >= 0 and a == b and _will_run(nf[0][0]) and _will_run(nf[1][0]):
                     plan["sh"] = ((dc, rest), a, None)
         if needs[5] and scales.numel() and _plain_activation(scales):
@@ -132,17 +162,17 @@ def _leaf_plan(sh, colors_precomp, opacities, scales, rotations, needs, sink_tak
             if type(n).__name__ == "ExpBackward0" and n._saved_result.data_ptr() == scales.data_ptr():
                 acc = n.next_functions[0][0]
                 leaf = _acc_leaf(acc)
-                st = _leaf_state(leaf, (P, 3), device)
-                if st >= 0 and _will_run(acc):
-                    plan["scales"] = ((leaf,), st, None)
+                s_ = st(leaf, (P, 3))
+                if s_ >= 0 and _will_run(acc):
+                    plan["scales"] = ((leaf,), s_, None)
         if needs[4] and opacities.numel() and _plain_activation(opacities):
             n = opacities.grad_fn
             if type(n).__name__ == "SigmoidBackward0" and n._saved_result.data_ptr() == opacities.data_ptr():
                 acc = n.next_functions[0][0]
                 leaf = _acc_leaf(acc)
-                st = _leaf_state(leaf, (P, 1), device)
-                if st >= 0 and _will_run(acc):
-                    plan["opacities"] = ((leaf,), st, None)
+                s_ = st(leaf, (P, 1))
+                if s_ >= 0 and _will_run(acc):
+                    plan["opacities"] = ((leaf,), s_, None)
         if needs[6] and rotations.numel() and _plain_activation(rotations):
             d = rotations.grad_fn
             df = d.next_functions if type(d).__name__ == "DivBackward0" else ()
@@ -154,52 +184,77 @@ def _leaf_plan(sh, colors_precomp, opacities, scales, rotations, needs, sink_tak
                         and tuple(nrm._saved_dim) in ((1,), (-1,)) and nrm._saved_keepdim
                         and nrm.next_functions[0][0] is acc):
                     leaf = _acc_leaf(acc)
-                    st = _leaf_state(leaf, (P, 4), device)
+                    s_ = st(leaf, (P, 4))
                     norm = nrm._saved_result
-                    if (st >= 0 and norm.shape == (P, 1) and norm.dtype == torch.float32 and norm.device == device
+                    if (s_ >= 0 and norm.shape == (P, 1) and norm.dtype == torch.float32 and norm.device == device
                             and d._saved_self.data_ptr() == leaf.data_ptr() and _will_run(acc)):
-                        plan["rotations"] = ((leaf,), st, (norm.contiguous(), float(c._saved_min)))
+                        plan["rotations"] = ((leaf,), s_, (norm.contiguous(), float(c._saved_min)))
+        # means3D is the _xyz leaf itself (scene/gaussian_model.py:114-116): only worth
+        # planning when its gradient can land in the exchange's bucket directly
+        if ex is not None and needs[0] and means3D.is_leaf:
+            acc = ctx.next_functions[0][0]
+            s_ = st(means3D, (P, 3))
+            if s_ >= 0 and _acc_leaf(acc) is means3D and _will_run(acc):
+                plan["means3D"] = ((means3D,), s_, None)
     except (AttributeError, RuntimeError, TypeError):
         return {}
-    return plan
+    views = ex.leaf_bucket({k: v[0] for k, v in plan.items()}) if ex is not None and plan else {}
+    if "means3D" not in views:
+        plan.pop("means3D", None)
+    return {k: (v[0], v[1], v[2], views.get(k)) for k, v in plan.items()}
 
 
 def _leaf_outputs(plan):
-    """The LeafGrads of a plan: the existing .grad where it accumulates, else fresh tensors."""
+    """The LeafGrads of a plan and the (leaf, tensor) pairs to install as .grad: a
+    bucket view of the exchange, else the existing .grad where it accumulates,
+    else a fresh tensor."""
     kw, fresh, acc = {}, [], 0
 
-    def out(leaf, state, bit):
+    def out(leaf, state, bit, view):
         nonlocal acc
         if state == 1:
             acc |= bit
-            return leaf.grad
-        t = torch.empty_like(leaf, memory_format=torch.contiguous_format)
+            return leaf.grad if view is None else view
+        t = torch.empty_like(leaf, memory_format=torch.contiguous_format) if view is None else view
         fresh.append((leaf, t))
         return t
 
     if "sh" in plan:
-        (dc, rest), st, _ = plan["sh"]
-        kw["dsh_dc"], kw["dsh_rest"] = out(dc, st, 1), out(rest, st, 1)
+        (dc, rest), st, _, v = plan["sh"]
+        v = v or (None, None)
+        kw["dsh_dc"], kw["dsh_rest"] = out(dc, st, 1, v[0]), out(rest, st, 1, v[1])
     if "scales" in plan:
-        (leaf,), st, _ = plan["scales"]
-        kw["dscaling"] = out(leaf, st, 2)
+        (leaf,), st, _, v = plan["scales"]
+        kw["dscaling"] = out(leaf, st, 2, v and v[0])
     if "opacities" in plan:
-        (leaf,), st, _ = plan["opacities"]
-        kw["dopacity"] = out(leaf, st, 4)
+        (leaf,), st, _, v = plan["opacities"]
+        kw["dopacity"] = out(leaf, st, 4, v and v[0])
     if "rotations" in plan:
-        (leaf,), st, (norm, eps) = plan["rotations"]
-        kw["drotation"] = out(leaf, st, 8)
+        (leaf,), st, (norm, eps), v = plan["rotations"]
+        kw["drotation"] = out(leaf, st, 8, v and v[0])
         kw["rotation_norm"], kw["rotation_eps"] = norm, eps
+    if "means3D" in plan:
+        (leaf,), st, _, v = plan["means3D"]
+        kw["dmeans3D"] = out(leaf, st, 16, v[0])
     return _C.LeafGrads(accumulate=acc, **kw), fresh
 
 
-def set_sh_grad_sink(sink):
-    """Install (or with None remove) the view-parallel SH-gradient sink.  The sink
-    provides ``accepts(sh, means3D) -> bool``, ``record(P) -> float32 tensor`` of
-    ``_C.sh_record_floats(P)`` elements, and ``push(record, campos, sh_degree)``."""
-    global _sh_grad_sink
-    prev, _sh_grad_sink = _sh_grad_sink, sink
+def set_grad_exchange(ex):
+    """Install (or with None remove) the view-parallel gradient exchange
+    (multiview.GradAllReduce); returns the previous one.  The exchange provides
+    ``accepts(sh, means3D) -> bool`` (True: it takes this backward's SH gradient as
+    the view's colour gradient), ``record(P)`` (a float32 tensor of
+    ``_C.sh_record_floats(P)`` elements) and ``push(record, campos, sh_degree)`` for
+    that; ``owns_hooks(leaf) -> bool`` (the leaf's post-accumulate hooks are its own,
+    so the fused path may write that leaf's gradient) and
+    ``leaf_bucket({name: leaves}) -> {name: views}`` (where the fused leaf gradients
+    go: views of its all-reduce bucket, for the names it can take)."""
+    global _exchange
+    prev, _exchange = _exchange, ex
     return prev
+
+
+set_sh_grad_sink = set_grad_exchange  # the round-1 name
 
 
 def _cpu_snapshot(args):
@@ -218,6 +273,16 @@ def _call_native(fn, args, debug: bool, dump: str, stage: str):
         raise
 
 
+# the forward's validated inputs (_C._rasterize), by name: where each comes from
+_INPUT_SRC = ("background", "means3D", "colors", "opacity", "scales", "rotations", "cov3D_precomp", "viewmatrix",
+              "projmatrix", "sh", "campos")
+
+
+def _input_sources(rs, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh):
+    return dict(zip(_INPUT_SRC, (rs.bg, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                                 rs.viewmatrix, rs.projmatrix, sh, rs.campos)))
+
+
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
@@ -226,56 +291,72 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
                 rs.sh_degree, rs.campos, rs.prefiltered, rs.debug)
-        num_rendered, color, radii, geom, binning, img, ctx.inputs = _call_native(
-            _C._rasterize, args, rs.debug, "snapshot_fw.dump", "forward")
+        # a backward may follow: the forward zeroes its accumulator beside the blend
+        prep = any(ctx.needs_input_grad[:8])
+        num_rendered, color, radii, geom, binning, img, vin = _call_native(
+            lambda *a: _C._rasterize(*a, prepare_backward=prep), args, rs.debug, "snapshot_fw.dump", "forward")
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
+        # The backward reuses the forward's validated inputs (the C struct).  The
+        # tensors it points at stay alive through save_for_backward (the inputs) and
+        # the raster settings (camera, background), as upstream; only contiguous
+        # copies the forward had to make are saved besides, so nothing outlives the
+        # backward (the saved tensors are freed after it unless the graph is
+        # retained), and an in-place change of a saved input raises.
+        copies = {}
+        ctx.inputs = None
+        if vin is not None:
+            s, keep, device, M = vin
+            src = _input_sources(rs, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh)
+            copies = {k: t for k, t in keep.items() if t is not None and t is not src[k]}
+            ctx.inputs = (s, device, M, frozenset(k for k, t in keep.items() if t is not None), tuple(copies))
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom, binning,
-                              img)
-        ctx.opacities = opacities  # an input (no reference cycle): its grad_fn for the fused leaf gradients
+                              img, opacities, *copies.values())
         ctx.mark_non_differentiable(radii)
         return color, radii
 
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii):
         rs = ctx.raster_settings
-        colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom, binning, img = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom, binning, img, opacities = saved[:11]
+        inputs = None
+        if ctx.inputs is not None:
+            s, device, M, present, copy_names = ctx.inputs
+            src = _input_sources(rs, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh)
+            src.update(zip(copy_names, saved[11:]))
+            inputs = (s, {k: (src[k] if k in present else None) for k in _INPUT_SRC}, device, M)
         args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree, rs.campos,
                 geom, ctx.num_rendered, binning, img, rs.debug)
-        sink = _sh_grad_sink
-        sink_takes_sh = sink is not None and sh.numel() > 0 and colors_precomp.numel() == 0 and sink.accepts(sh,
-                                                                                                           means3D)
-        plan = (_leaf_plan(sh, colors_precomp, ctx.opacities, scales, rotations, ctx.needs_input_grad, sink_takes_sh)
-                if _fused_leaf_grads and means3D.size(0) > 0 and not sink_takes_sh else {})
+        ex = _exchange
+        sink_takes_sh = (ex is not None and sh.numel() > 0 and colors_precomp.numel() == 0
+                         and ex.accepts(sh, means3D))
+        plan = (_leaf_plan(ctx, ctx.needs_input_grad, sh, colors_precomp, opacities, scales, rotations, means3D,
+                           sink_takes_sh, ex)
+                if _fusion_on(ex) and means3D.size(0) > 0 else {})
         global last_leaf_plan
         last_leaf_plan = tuple(sorted(plan))
+        kw = dict(opacities=opacities, inputs=inputs)
         if plan:
             leaf, fresh = _leaf_outputs(plan)
-            (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
-                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True, leaf=leaf, opacities=ctx.opacities,
-                                                           inputs=ctx.inputs), args, rs.debug, "snapshot_bw.dump",
-                "backward")
-            for p, g in fresh:
-                p.grad = g
-            return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
+            kw["leaf"] = leaf
         if sink_takes_sh:
-            rec = sink.record(means3D.size(0))
+            rec = ex.record(means3D.size(0))
             # the record's exchange starts as soon as the colour gradient is queued,
             # under the per-Gaussian backward
-            push = lambda: sink.push(rec, rs.campos, rs.sh_degree)  # noqa: E731
-            (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
-                lambda *a: _C.rasterize_gaussians_backward(*a, drgb_out=rec[4:], on_drgb=push,
-                                                           opacities=ctx.opacities, inputs=ctx.inputs), args,
-                rs.debug, "snapshot_bw.dump", "backward")
+            kw["drgb_out"], kw["on_drgb"] = rec[4:], lambda: ex.push(rec, rs.campos, rs.sh_degree)
         else:
-            # dsh as the [P,M,3] view of coefficient planes: the reference's SH cat
-            # backward (get_features) then slices an f_dc gradient that already has
-            # _features_dc's layout, and AccumulateGrad keeps it without a copy
-            (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
-                lambda *a: _C.rasterize_gaussians_backward(*a, dsh_planar=True, opacities=ctx.opacities,
-                                                           inputs=ctx.inputs), args, rs.debug, "snapshot_bw.dump",
-                "backward")
+            # a dsh that autograd receives is the [P,M,3] view of coefficient planes:
+            # the reference's SH cat backward (get_features) then slices an f_dc
+            # gradient that already has _features_dc's layout, and AccumulateGrad
+            # keeps it without a copy
+            kw["dsh_planar"] = True
+        (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
+            lambda *a: _C.rasterize_gaussians_backward(*a, **kw), args, rs.debug, "snapshot_bw.dump", "backward")
+        if plan:
+            for p, g in fresh:
+                p.grad = g
         return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
 
 

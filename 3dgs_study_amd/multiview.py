@@ -23,17 +23,23 @@ equal to the sum of the single-view gradients.  Per GPU and step at 1M Gaussians
 (xyz, opacity, scaling, rotation all-reduced) + 7·12 MB (records received) = 161 MB.
 It also skips the 192 MB dsh write and the SH ``cat`` backward on every rank.
 
-Two modes for the all-reduced gradients:
-  * overlapped (``overlap=True``, default): a post-accumulate-grad hook on every
-    parameter counts the backwards that accumulate into it and, on the step's last
-    one (``views_per_step`` backwards per rank and step), starts that gradient's
-    all-reduce (async, on RCCL's stream) — xyz straight out of the rasterizer's
-    backward, f_dc / f_rest after the SH ``cat`` backward, opacity / scaling /
-    rotation after their activation backwards — so the exchange runs under the
-    remaining backward kernels and no flat copy is made.  ``__call__`` waits.
-  * flat: every gradient whose all-reduce did not start from a hook (no hook on a
-    replaced tensor, gradients assigned by hand, fewer backwards than announced) is
-    packed into ONE fp32 bucket and reduced with one call in ``__call__``.
+One bucket for the all-reduced gradients.  Every gradient the exchange sums
+(xyz, opacity, scaling, rotation — and f_dc / f_rest without the SH exchange) lives
+in ONE flat fp32 bucket per step, reduced by ONE all-reduce:
+  * overlapped (``overlap=True``, default): the rasterizer's fused leaf gradients
+    (diff_gaussian_rasterization, ``_leaf_plan``) are written by its backward
+    kernel straight into bucket views that become the leaves' ``.grad`` — the xyz
+    gradient included — so no activation backward, AccumulateGrad copy or pack
+    copy runs; a post-accumulate-grad hook on every parameter queues a callback at
+    the end of the autograd pass, which (on the step's last backward,
+    ``views_per_step``) copies any gradient that is not in the bucket yet (another
+    graph, an unfusable input) into it and starts the bucket's all-reduce, async
+    on RCCL's stream.  ``__call__`` makes the compute stream wait for it.
+  * flat (``overlap=False``): nothing starts during the backward; ``__call__``
+    packs every gradient into the bucket and reduces it.
+At 1M Gaussians the bucket is 44 MB with the SH exchange (one all-reduce instead of
+four per-parameter ones), and each rank's backward runs no torch kernel after the
+rasterizer's own at any N.
 
 Parameters may be given as a zero-argument callable returning the current tensors
 (and ``sh`` likewise): the reference's densify / prune replaces every parameter with
@@ -43,6 +49,7 @@ returns, so the exchange follows the model instead of going stale.
 """
 from __future__ import annotations
 
+import time
 from typing import Callable, Sequence, Union
 
 import torch
@@ -63,13 +70,15 @@ class GradAllReduce:
     exchanges the SH gradient as per-view colour gradients instead (module
     docstring); it engages when the group has more than one rank, or always with
     ``sh_force=True`` (tests).  ``views_per_step``: backwards each rank runs per step
-    (the overlapped all-reduces start on the last one).  ``rebuild`` replaces the HIP
-    kernel that turns gathered records into the SH gradients (CPU tests only).
-    ``comm_force=True`` runs every collective even in a one-rank group (tests: the
-    RCCL calls on a one-GPU box)."""
+    (the bucket's all-reduce starts at the end of the last one).  ``rebuild``
+    replaces the HIP kernel that turns gathered records into the SH gradients (CPU
+    tests only).  ``comm_force=True`` runs every collective even in a one-rank
+    group (tests and the bench's forced one-rank exchange: the RCCL calls on a
+    one-GPU box).  ``timing=True`` records, per ``__call__``, how long the compute
+    stream waits for the exchange and how long the SH rebuild takes (``stats()``)."""
 
     def __init__(self, params: ParamSource, group=None, overlap: bool = True, sh=None, sh_force: bool = False,
-                 rebuild=None, views_per_step: int = 1, comm_force: bool = False):
+                 rebuild=None, views_per_step: int = 1, comm_force: bool = False, timing: bool = False):
         if views_per_step < 1:
             raise ValueError("views_per_step must be >= 1")
         self._params_src = params
@@ -79,19 +88,26 @@ class GradAllReduce:
         self.views_per_step = views_per_step
         self._comm_force = comm_force  # run the collectives even in a one-rank group (RCCL smoke tests)
         self._rebuild = rebuild
-        self._works = []       # (param, work) of the all-reduces started from hooks
         self._hooks = []
-        self._counts = {}      # id(param) -> backwards accumulated into it this step
         self._gathers = []
         self._sh = None
-        self._prev_sink = None
-        self._sink_installed = False
+        self._bucket = None     # this step's flat fp32 bucket over self._reduced
+        self._views = None      # its per-parameter views
+        self._work = None       # the bucket's async all-reduce
+        self._backwards = 0     # backwards finished this step
+        self._cb_queued = False
+        self.launched_in_backward = False  # the bucket's all-reduce started from the end-of-backward callback
+        self._timing = timing
+        self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0}
+        self._tpending = []
+        self._prev_ex = None
+        self._installed = False
         self._sh_on = sh is not None and (sh_force or self._active())
         self._bind()
-        if self._sh_on:
-            from diff_gaussian_rasterization import set_sh_grad_sink
-            self._prev_sink = set_sh_grad_sink(self)
-            self._sink_installed = True
+        if self._sh_on or (overlap and self._active()):
+            from diff_gaussian_rasterization import set_grad_exchange
+            self._prev_ex = set_grad_exchange(self)
+            self._installed = True
 
     # ---- binding to the current parameter tensors
     def _resolve(self):
@@ -111,13 +127,13 @@ class GradAllReduce:
         self.params, self._sh = self._resolve()
         self.numel = sum(p.numel() for p in self.params)
         self._reduced = [p for p in self.params if self._sh is None or not any(p is q for q in self._sh[1:])]
-        self._counts = {id(p): 0 for p in self._reduced}
-        # hooks only while there is something to exchange: with one rank the
-        # rasterizer may then write the leaves' gradients itself (diff_gaussian_
-        # rasterization's fused leaf gradients skip leaves that carry hooks)
+        self._bucket = self._views = None
+        # hooks only while there is something to exchange: with one rank the leaves
+        # carry none, and the rasterizer's fused leaf gradients apply as without us
         if self.overlap and self._active():
             for p in self._reduced:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._launch))
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_accumulate))
+        self._hook_ids = {h.id for h in self._hooks}
 
     def _stale(self) -> bool:
         params, sh = self._resolve()
@@ -138,14 +154,100 @@ class GradAllReduce:
     def sh_exchange(self) -> bool:
         return self._sh is not None
 
+    @property
+    def pending(self) -> int:
+        """Collectives in flight for this step (the bucket's all-reduce)."""
+        return int(self._work is not None)
+
     def _active(self) -> bool:
         return dist.is_initialized() and (dist.get_world_size(self.group) > 1 or self._comm_force)
 
-    # ---- the rasterizer's SH sink (diff_gaussian_rasterization.set_sh_grad_sink)
+    # ---- the bucket
+    def _ensure_bucket(self):
+        if self._bucket is None:
+            ref = self._reduced[0]
+            self._bucket = torch.empty(sum(p.numel() for p in self._reduced), dtype=torch.float32, device=ref.device)
+            self._views, off = [], 0
+            for p in self._reduced:
+                self._views.append(self._bucket[off:off + p.numel()].view_as(p))
+                off += p.numel()
+        return self._bucket
+
+    @staticmethod
+    def _is_view(g, v) -> bool:
+        return g is not None and g.data_ptr() == v.data_ptr() and g.shape == v.shape and g.dtype == v.dtype
+
+    def _pack(self) -> torch.Tensor:
+        """Every reduced parameter's .grad into its bucket view (zeros where a
+        parameter got none), the views installed as .grad."""
+        self._ensure_bucket()
+        for p, v in zip(self._reduced, self._views):
+            g = p.grad
+            if self._is_view(g, v):
+                continue
+            if g is None:
+                v.zero_()
+            else:
+                v.copy_(g)
+            p.grad = v
+        return self._bucket
+
+    # ---- what the rasterizer asks (diff_gaussian_rasterization.set_grad_exchange)
+    def owns_hooks(self, leaf) -> bool:
+        """True when the leaf's post-accumulate hooks are this exchange's (the fused
+        path may then write its gradient: the hook still fires and the bucket is
+        packed at the end of the backward)."""
+        hooks = getattr(leaf, "_post_accumulate_grad_hooks", None) or {}
+        return bool(self._hooks) and set(hooks) <= self._hook_ids
+
+    def leaf_bucket(self, leaves: dict) -> dict:
+        """Bucket views for the rasterizer's fused leaf gradients: {name: views} for
+        each name whose leaves are all reduced here and have no gradient yet or
+        already hold their bucket view (a later backward of the step accumulates)."""
+        if not (self.overlap and self._active()) or not self._reduced or self._stale():
+            return {}
+        self._ensure_bucket()
+        self._queue_callback()
+        out = {}
+        for name, ls in leaves.items():
+            idx = [next((i for i, p in enumerate(self._reduced) if p is leaf), -1) for leaf in ls]
+            if all(i >= 0 and (ls[j].grad is None or self._is_view(ls[j].grad, self._views[i]))
+                   for j, i in enumerate(idx)):
+                out[name] = tuple(self._views[i] for i in idx)
+        return out
+
+    # ---- the end of each backward: start the bucket's all-reduce on the step's last
+    def _queue_callback(self):
+        if not self._cb_queued:
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._on_backward_end)
+                self._cb_queued = True
+            except RuntimeError:  # not inside a backward: __call__ packs and reduces
+                pass
+
+    def _on_accumulate(self, p: torch.Tensor) -> None:
+        if self._active():
+            self._queue_callback()
+
+    def _on_backward_end(self) -> None:
+        self._cb_queued = False
+        self._backwards += 1
+        if self._backwards > self.views_per_step:
+            raise RuntimeError(f"GradAllReduce: {self._backwards} backwards in one step (views_per_step="
+                               f"{self.views_per_step}); the bucket's all-reduce already started")
+        if self._backwards == self.views_per_step and self._work is None and not self._stale():
+            bucket = self._pack()
+            self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self.launched_in_backward = True
+
+    # ---- the rasterizer's SH sink
     def accepts(self, sh: torch.Tensor, means3D: torch.Tensor) -> bool:
-        """True when this backward's SH input is the bound model's.  With more than
-        one rank a mismatch raises: a silent local dsh would leave this rank's SH
-        gradient out of the exchange and the replicas would drift apart."""
+        """True when this backward's SH input is the bound model's (and the SH
+        exchange is on).  With more than one rank a mismatch raises: a silent local
+        dsh would leave this rank's SH gradient out of the exchange and the replicas
+        would drift apart."""
+        if not self._sh_on:
+            return False
         if self._stale():  # the model's tensors were replaced (densify / prune): follow them
             self._bind()
         xyz, f_dc, f_rest = self._sh
@@ -197,60 +299,88 @@ class GradAllReduce:
             else:
                 p.grad.add_(g)
 
-    def _launch(self, p: torch.Tensor) -> None:
-        k = id(p)
-        if k not in self._counts or not self._active():  # one rank: nothing to exchange
-            return
-        self._counts[k] += 1
-        if self._counts[k] > self.views_per_step:
-            raise RuntimeError(f"GradAllReduce: {self._counts[k]} backwards accumulated into a parameter in one step "
-                               f"(views_per_step={self.views_per_step}); its all-reduce already started")
-        if self._counts[k] == self.views_per_step and self._active():
-            self._works.append((p, dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
-
     def remove_hooks(self) -> None:
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        if self._sink_installed:
-            from diff_gaussian_rasterization import set_sh_grad_sink
-            set_sh_grad_sink(self._prev_sink)
-            self._sink_installed = False
+        self._hook_ids = set()
+        if self._installed:
+            from diff_gaussian_rasterization import set_grad_exchange
+            set_grad_exchange(self._prev_ex)
+            self._installed = False
             self._sh = None
             self._sh_on = False
 
+    # ---- timing (bench.py's N > 1 line)
+    def _mark(self):
+        if not self._timing:
+            return None
+        if self._reduced and self._reduced[0].is_cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def stats(self) -> dict:
+        """Means per __call__ since the last reset: exchange_wait_ms (how long the
+        compute stream waits for the records' all-gather and, after the SH rebuild,
+        for the bucket's all-reduce), sh_rebuild_ms (the SH gradients from the
+        gathered records), and the bytes this rank contributes per step."""
+        for a, b, c, d in self._tpending:
+            if isinstance(a, float):
+                w, r = (b - a + d - c) * 1e3, (c - b) * 1e3
+            else:
+                d.synchronize()
+                w, r = a.elapsed_time(b) + c.elapsed_time(d), b.elapsed_time(c)
+            self._tstats["exchange_wait_ms"] += w
+            self._tstats["sh_rebuild_ms"] += r
+            self._tstats["calls"] += 1
+        self._tpending = []
+        n = max(self._tstats["calls"], 1)
+        return {"exchange_wait_ms": self._tstats["exchange_wait_ms"] / n,
+                "sh_rebuild_ms": self._tstats["sh_rebuild_ms"] / n, "calls": self._tstats["calls"],
+                "bytes_per_rank": self.nbytes}
+
+    def reset_stats(self) -> None:
+        self.stats()
+        self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0}
+
     def __call__(self):
-        """Finish this step's exchange: wait for the overlapped all-reduces, reduce
-        every other gradient as one flat bucket, then rebuild the SH gradients from
-        the gathered colour gradients (SH exchange on).  Returns the flat bucket (or
-        None when every gradient went through a hook)."""
-        done = set()
-        for p, w in self._works:
-            w.wait()
-            done.add(id(p))
-        self._works = []
+        """Finish this step's exchange: the bucket's all-reduce (started at the end
+        of the backward, or packed and reduced here when it was not: flat mode, a
+        parameter swap, fewer backwards than announced), then the SH gradients from
+        the gathered colour gradients (SH exchange on).  Returns the bucket."""
         if self._stale():
             # the model's tensors were replaced since the hooks were bound (densify /
-            # prune): their gradients go through the flat bucket this step, and the
-            # hooks move to them for the next
+            # prune): their gradients go through the bucket here, and the hooks move
+            # to them for the next step
+            self._work = None
             self._bind()
-        rest = [p for p in self._reduced if id(p) not in done]
-        flat = None
-        if rest:
-            grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in rest]
-            flat = torch.cat([g.reshape(-1) for g in grads])
+        if self._work is None:
+            bucket = self._pack()
             if self._active():
-                dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-            off = 0
-            for p in rest:
-                n = p.numel()
-                p.grad = flat[off:off + n].view_as(p)
-                off += n
+                self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        bucket = self._bucket
+        # the SH rebuild needs only the gathered records: it runs while the bucket's
+        # all-reduce is still in flight, and the compute stream waits for the bucket last
+        t0 = self._mark()
+        for _, _, w in self._gathers:
+            if w is not None:
+                w.wait()
+        t1 = self._mark()
         if self._sh is not None:
             self._finish_sh()
-        for k in self._counts:
-            self._counts[k] = 0
-        return flat
+        t2 = self._mark()
+        if self._work is not None:
+            self._work.wait()
+        t3 = self._mark()
+        if t0 is not None:
+            self._tpending.append((t0, t1, t2, t3))
+        self._work = None
+        self._bucket = self._views = None  # the grads keep the storage; next step gets a fresh bucket
+        self._backwards = 0
+        self.launched_in_backward = False
+        return bucket
 
 
 @torch.no_grad()

@@ -68,6 +68,26 @@ def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, M: int) -> flo
     }.get(stage, 0.0)
 
 
+def iter_bytes(P: int, I: int, W: int, H: int, M: int, backward: bool = True) -> float:
+    """SURVEY.md §8(d)'s algorithmic bytes of one unit: forward P(147 + 12M) + I·84 +
+    HW·20 + T·16, backward P(283 + 24M) + I·40 + HW·20 + T·8."""
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    fwd = P * (147 + 12 * M) + I * 84 + W * H * 20 + T * 16
+    bwd = P * (283 + 24 * M) + I * 40 + W * H * 20 + T * 8
+    return float(fwd + (bwd if backward else 0))
+
+
+RASTER_STAGES = ("preprocess", "depth_sort", "duplicate", "tile_sort", "render_fwd", "bwd_prepare", "render_bwd",
+                 "preprocess_bwd")
+
+
+def raster_ms(per_stage: dict) -> float:
+    """The rasterizer's own device time per step: the sum of its stages' mean launch
+    times (HIP events on the launch stream; the caller's torch kernels excluded)."""
+    return round(sum(per_stage[k][0] if isinstance(per_stage[k], tuple) else per_stage[k]
+                     for k in RASTER_STAGES if k in per_stage), 4)
+
+
 def pmc_stage(stage: str) -> dict:
     """profiles/pmc_summary.json's record of a stage (tools/pmc.sh): HBM bytes per
     launch and the VALU issue utilisation, measured by rocprofv3 --pmc passes."""
@@ -206,6 +226,9 @@ def main():
                          "the same K steps right before the timed region, whose steps carry events only around the "
                          "dominant stage (its live launch time = the roofline); all: events on every stage inside "
                          "the timed region (they cost ~5%% of the step); none: no events")
+    ap.add_argument("--exchange-steps", type=int, default=100,
+                    help="N=1: timed steps with the view-parallel exchange forced on in a one-rank RCCL group "
+                         "(every collective runs; reported beside the plain step); 0 = skip")
     ap.add_argument("--render-steps", type=int, default=20,
                     help="timed forward-only renders of config E (5M, 4K) reported beside the C line; 0 = skip")
     args = ap.parse_args()
@@ -246,7 +269,8 @@ def main():
     bg = torch.zeros(3, device=dev)
     params = g.params()
     sh = (params[0], params[1], params[2]) if args.grad_exchange == "sh-colour" else None
-    reducer = GradAllReduce(params, sh=sh)  # exchange engages only when world > 1
+    # the exchange engages only when world > 1 (timing: its wait / SH rebuild per step)
+    reducer = GradAllReduce(params, sh=sh, timing=world > 1)
 
     def one_step():
         for p in params:
@@ -275,6 +299,7 @@ def main():
     _C.timing_enable({"split": [dom], "all": True, "none": False}[args.stage_events])
     torch.cuda.synchronize()
     if world > 1:
+        reducer.reset_stats()
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -286,10 +311,18 @@ def main():
     stages = _C.timing_read()
     _C.timing_enable(False)
     elapsed = t1 - t0
+    exchange = None
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        ex = reducer.stats()
+        t = torch.tensor([elapsed, ex["exchange_wait_ms"], ex["sh_rebuild_ms"]], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
+        import diff_gaussian_rasterization as dgr
+        # per rank, max over the ranks: how long the compute stream waited for the
+        # bucket's all-reduce + the records' all-gather, and the SH rebuild
+        exchange = {"exchange_wait_ms": round(float(t[1].item()), 4), "sh_rebuild_ms": round(float(t[2].item()), 4),
+                    "bytes_per_rank": ex["bytes_per_rank"], "calls": ex["calls"],
+                    "fused_leaves": list(dgr.last_leaf_plan), "stat": "max over ranks of the per-step mean"}
     if args.stage_events == "all":
         per_stage = {k: (ms / n if n else 0.0, n) for k, (ms, n) in stages.items() if n}
         dom = max(per_stage, key=lambda k: per_stage[k][0] * per_stage[k][1]) if per_stage else "render_bwd"
@@ -333,6 +366,11 @@ def main():
             "mpix_per_s": round(value * W * H / 1e6, 2),
             "stages_ms": {k: round(v[0], 4) for k, v in per_stage.items()},
             "stages_source": STAGES_SOURCE[args.stage_events],
+            # the rasterizer's own stages per step, and §8(d)'s bytes per unit at the
+            # measured I against 8 TB/s (the north_star's iteration-level roofline)
+            "raster_ms": raster_ms(per_stage),
+            "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
+            "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * value / world / 1e9 / HBM_PEAK_GBS, 4),
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -356,10 +394,14 @@ def main():
         if world == 1 and args.full_steps > 0:
             line["full_step"] = full_step_rates(cam, P, deg, target, bg, args.full_steps)
         if world == 1 and args.render_steps > 0:
-            del out
+            out = None
             line["config_E_render"] = render_rates("E", dev, args.render_steps, 3)
             if _C.get_footprint() != "rect":  # upstream's instance set (I ~ 110M): the tile sort's stress case
                 line["config_E_render_rect"] = render_rates("E", dev, args.render_steps, 3, footprint="rect")
+        if world == 1 and args.exchange_steps > 0:
+            del out
+            line["exchange_1rank"] = exchange_one_rank_rates(cam, P, deg, target, bg, args.exchange_steps, args.warmup,
+                                                             line["ms_per_step"])
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
@@ -414,9 +456,69 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
         dt = time.perf_counter() - t0
     finally:
         set_footprint(prev)
+    P, W, H, M = g.xyz.shape[0], cam.image_width, cam.image_height, g.features_rest.shape[1] + 1
     return {"footprint": mode, "value": round(steps / dt, 3), "unit": "train-iters/s",
             "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps, "num_rendered": I,
-            "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "stages_source": STAGES_SOURCE["split"]}
+            "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "stages_source": STAGES_SOURCE["split"],
+            "raster_ms": raster_ms(per), "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
+            "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * steps / dt / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmup: int, plain_ms: float) -> dict:
+    """The headline unit with the N > 1 exchange forced on in a one-rank RCCL group
+    ("nccl" backend, comm_force): the SH gradient leaves the backward as the view's
+    colour-gradient record (all-gathered) and is rebuilt by sh_grad_from_colors, the
+    xyz / opacity / scaling / rotation gradients are written by the rasterizer into
+    the exchange's bucket and all-reduced — every collective of an N-rank step runs,
+    over one rank.  What each rank of the driver's 1->8 run pays besides RCCL's
+    transfers."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    import diff_gaussian_rasterization as dgr
+    import synthetic
+    import train_step
+    from multiview import GradAllReduce
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    dev = bg.device
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        g = synthetic.make_gaussians(P, deg, seed=0).to(dev, requires_grad=True)
+        params = g.params()
+        ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), comm_force=True, timing=True)
+
+        def step():
+            for p in params:
+                p.grad = None
+            train_step.train_step(cam, g, target, bg)
+            ar()
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        ar.reset_stats()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        st = ar.stats()
+        plan = list(dgr.last_leaf_plan)
+        ar.remove_hooks()
+        del g, params
+    finally:
+        dist.destroy_process_group()
+    ms = 1e3 * dt / steps
+    return {"value": round(steps / dt, 3), "unit": "train-iters/s", "ms_per_step": round(ms, 4), "steps": steps,
+            "vs_plain_ms": round(ms / plain_ms, 4) if plain_ms else None, "fused_leaves": plan,
+            "exchange_wait_ms": round(st["exchange_wait_ms"], 4), "sh_rebuild_ms": round(st["sh_rebuild_ms"], 4),
+            "bytes_per_rank": st["bytes_per_rank"], "collective_backend": "RCCL (one rank, every collective forced)"}
 
 
 def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0, footprint=None) -> dict:
@@ -483,6 +585,9 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int) -> dic
                     ("preprocess", "depth_sort", "duplicate", "tile_sort", "render_fwd"))
     res["forward_algorithmic_bytes"] = fwd_bytes
     res["forward_hbm_frac"] = round(fwd_bytes * fps / 1e9 / HBM_PEAK_GBS, 4)
+    res["raster_ms"] = raster_ms(per)
+    res["iter_algorithmic_bytes"] = iter_bytes(P, I, W, H, M, backward=False)  # §8(d)'s forward formula
+    res["iter_hbm_frac"] = round(res["iter_algorithmic_bytes"] * fps / 1e9 / HBM_PEAK_GBS, 4)
     del g
     torch.cuda.empty_cache()
     return res

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 6
+#define GSR_ABI_VERSION 7
 
 enum gsr_status {
     GSR_OK = 0,
@@ -69,6 +69,15 @@ enum gsr_status {
  * package defaults to TIGHT (of upstream's outputs only num_rendered differs). */
 enum gsr_footprint { GSR_FOOTPRINT_RECT = 0, GSR_FOOTPRINT_TIGHT = 1 };
 
+/* gsr_inputs.flags.  GSR_FLAG_PREPARE_BACKWARD (forward calls; not upstream):
+ * a backward will follow, so gsr_forward_render also zeroes the backward's
+ * gradient accumulator (inside the geom buffer) on the library's second stream
+ * while the blend runs, and files the quadrants for the backward's wave order —
+ * work the backward then skips (its accum argument NULL: the geom buffer's
+ * accumulator; a second backward of the same forward zeroes it again itself).
+ * Only a speed hint: every backward is correct with or without it. */
+enum gsr_flags { GSR_FLAG_PREPARE_BACKWARD = 1 };
+
 /* Inputs shared by forward and backward.  Mirrors the argument list of
  * _C.rasterize_gaussians (rasterize_points.cu RasterizeGaussiansCUDA). */
 typedef struct gsr_inputs {
@@ -81,7 +90,7 @@ typedef struct gsr_inputs {
     int32_t prefiltered;        /* bool */
     int32_t debug;              /* bool: synchronise + check after every kernel */
     int32_t footprint;          /* enum gsr_footprint: which (tile, Gaussian) pairs are binned */
-    int32_t reserved;           /* 0 */
+    int32_t flags;              /* gsr_flags bits (0 = none) */
     const float *bg;            /* [3]   background colour */
     const float *means3D;       /* [P,3] */
     const float *colors_precomp;/* [P,3] or NULL */
@@ -96,19 +105,23 @@ typedef struct gsr_inputs {
 } gsr_inputs;
 
 /* Scratch sizes in bytes (all buffers 256-byte aligned internally).
- * geom:    per-Gaussian state + per-tile counting scratch (upstream GeometryState)
+ * geom:    per-Gaussian state + per-tile counting scratch (upstream GeometryState),
+ *          and the backward's gradient accumulator (64 B per Gaussian)
  * binning: per-instance keys and the sorted point list (upstream BinningState)
  * img:     per-pixel final T / contributor counts (ImageState)
- * accum:   backward per-Gaussian gradient accumulators (64 B per Gaussian) */
+ * accum:   a separate backward accumulator (64 B per Gaussian), for callers that
+ *          pass one to a backward instead of NULL (the geom buffer's) */
 size_t gsr_geom_bytes(int32_t P, int32_t W, int32_t H);
 size_t gsr_binning_bytes(int64_t num_rendered, int32_t W, int32_t H);
 size_t gsr_img_bytes(int32_t W, int32_t H);
 size_t gsr_accum_bytes(int32_t P);
 
 /* Replaces the first half of RasterizeGaussiansCUDA -> Rasterizer::forward
- * (preprocess + InclusiveSum + the num_rendered cudaMemcpy).  While the host
- * waits for num_rendered the device also sorts the P Gaussians by depth (the
- * first half of the binning, see 3dgs_study_amd/csrc/binning.hip).
+ * (preprocess + InclusiveSum + the num_rendered cudaMemcpy).  The device also
+ * sorts the P Gaussians by depth (the first half of the binning, see
+ * 3dgs_study_amd/csrc/binning.hip), on a second stream of the library's own
+ * (one per host thread and device) that forks from and joins back into `stream`
+ * inside this call: the caller sees one stream.
  * Writes radii [P] int32 and *num_rendered (host pointer). */
 int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered, void *stream);
 
@@ -119,6 +132,8 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
                        const int32_t *radii, float *out_color, void *stream);
 
 /* Replaces RasterizeGaussiansBackwardCUDA -> Rasterizer::backward.
+ * accum: NULL = the accumulator inside geom (zeroed by a forward called with
+ * GSR_FLAG_PREPARE_BACKWARD, else here), or a caller buffer of gsr_accum_bytes(P).
  * Every output is fully written (no pre-zeroing needed); dsh may be NULL when
  * in->sh is NULL, dscales/drot may be NULL when in->scales is NULL, dcolors
  * when in->colors_precomp is NULL and dcov3D when in->cov3D_precomp is NULL
@@ -155,7 +170,9 @@ int gsr_backward_planar(const gsr_inputs *in, const int32_t *radii, const void *
  * the corresponding activation gradient is not written (that output pointer
  * may be NULL).  accumulate bit k adds into output k (AccumulateGrad's
  * `grad += new`) instead of overwriting: bit 0 dsh_dc + dsh_rest, bit 1
- * dscaling, bit 2 dopacity, bit 3 drotation.  Inputs by output:
+ * dscaling, bit 2 dopacity, bit 3 drotation, bit 4 the backward's own dmeans3D
+ * output (means3D is itself the leaf GaussianModel._xyz, scene/gaussian_model.py:
+ * 114-116: a caller may point dmeans3D at that leaf's .grad).  Inputs by output:
  *   dsh_dc [P,1,3], dsh_rest [P,M-1,3] (NULL when M == 1): in->sh required;
  *   dscaling [P,3]: in->scales (= exp(_scaling)) required;
  *   dopacity [P,1]: in->opacities (= sigmoid(_opacity)) required;
@@ -182,6 +199,22 @@ int gsr_backward_leaves(const gsr_inputs *in, const int32_t *radii, const void *
                         const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
                         float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
                         float *dscales, float *drot, const gsr_leaf_grads *leaf, void *stream);
+
+/* The general backward, every output form at once (not upstream; the entry points
+ * above and below are special cases of it).  phases: 1 = accumulator zeroing +
+ * render backward (+ drgb, below), 2 = the per-Gaussian backward, 3 = both; a
+ * caller splitting them issues 1 then 2 with the same arguments on the same
+ * stream, and may start exchanging drgb in between.  drgb (instead of dsh, and
+ * instead of leaf dsh_dc / dsh_rest): the clamp-masked colour gradient of the
+ * view-parallel SH exchange (gsr_backward_colors); leaf: as gsr_backward_leaves
+ * (NULL = none) — so one backward can hand the SH gradient to the exchange and
+ * write the scaling / opacity / rotation leaf gradients and dmeans3D straight into
+ * the caller's all-reduce bucket (3dgs_study_amd/multiview.py). */
+int gsr_backward_phase(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
+                       const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
+                       float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
+                       float *drgb, float *dscales, float *drot, const gsr_leaf_grads *leaf, int32_t phases,
+                       void *stream);
 
 /* View-parallel exchange of the SH gradient (3dgs_study_amd/multiview.py;
  * SURVEY.md §8e).  Upstream has no multi-GPU path; these two calls split
@@ -275,6 +308,9 @@ enum gsr_stage {
     GSR_STAGE_RENDER_FWD,     /* FORWARD::renderCUDA */
     GSR_STAGE_RENDER_BWD,     /* BACKWARD::renderCUDA */
     GSR_STAGE_PREPROCESS_BWD, /* BACKWARD::computeCov2DCUDA + preprocessCUDA */
+    GSR_STAGE_BWD_PREPARE,    /* accumulator zeroing + the render backward's wave order (no upstream kernel) */
+    GSR_STAGE_DSORT_CONCURRENT, /* the depth sort on its own stream, concurrent with preprocess; GSR_STAGE_DEPTH_SORT
+                                   is its exposed part on the launch stream (the join + rank-order gather) */
     GSR_STAGE_COUNT
 };
 int gsr_timing_enable(int mask);

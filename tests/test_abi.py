@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 6
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 7
     # 12 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 48 + 11 * 8
     assert _C.GsrInputs.footprint.offset == 40
@@ -120,9 +120,9 @@ def test_sh_exchange_entry_points_validate(lib):
 def test_stage_names(lib):
     from diff_gaussian_rasterization import _C
 
-    names = [lib.gsr_stage_name(i).decode() for i in range(8)]
+    names = [lib.gsr_stage_name(i).decode() for i in range(10)]
     assert names == ["preprocess", "scan", "depth_sort", "duplicate", "tile_sort", "render_fwd", "render_bwd",
-                     "preprocess_bwd"]
+                     "preprocess_bwd", "bwd_prepare", "depth_sort_concurrent"]
     assert lib.gsr_stage_name(99).decode() == ""
     _C.timing_enable(True)
     assert _C.timing_read() == {n: (0.0, 0) for n in names}

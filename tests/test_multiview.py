@@ -68,11 +68,11 @@ def _cpu_overlap_worker(rank, world, port, out):
     torch.manual_seed(0)
     shapes = [(5, 3), (5, 1, 3), (5, 15, 3), (5, 1), (5, 3), (5, 4)]
     params = [torch.randn(s, requires_grad=True) for s in shapes]
-    ar = GradAllReduce(params)  # hooks: each gradient's all-reduce starts inside backward
+    ar = GradAllReduce(params)  # the bucket's all-reduce starts when the backward ends
     w = float(rank + 1)
     loss = sum((w * (i + 1) * p * p).sum() for i, p in enumerate(params))
     loss.backward()
-    pending = len(ar._works)
+    pending = ar.pending
     ar()
     out[rank] = ([p.detach().clone() for p in params], [p.grad.clone() for p in params], pending)
     ar.remove_hooks()
@@ -80,8 +80,9 @@ def _cpu_overlap_worker(rank, world, port, out):
 
 
 def test_grad_all_reduce_overlapped_gloo_world2():
-    """Overlapped mode: the all-reduces launch from post-accumulate-grad hooks during
-    backward; after the wait every rank holds the sum of the ranks' gradients."""
+    """Overlapped mode: the bucket's one all-reduce launches from the end-of-backward
+    callback the parameters' hooks queue; after the wait every rank holds the sum of
+    the ranks' gradients, as views of one flat bucket."""
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
@@ -89,7 +90,7 @@ def test_grad_all_reduce_overlapped_gloo_world2():
         res = dict(out)
     p0, g0, n0 = res[0]
     p1, g1, n1 = res[1]
-    assert n0 == n1 == 6  # one async all-reduce per parameter, launched during backward
+    assert n0 == n1 == 1  # one async all-reduce of the bucket, launched at the end of backward
     for i, (a, b, p) in enumerate(zip(g0, g1, p0)):
         assert torch.equal(a, b)
         # d/dp sum_r (r+1)(i+1) p^2 = 2 p (i+1) (1 + 2)
@@ -199,7 +200,7 @@ def _gpu_worker(rank, world, port, out, sh_exchange=False):
     # overlapped: the all-reduces (and the SH record gather) start inside backward
     reducer = GradAllReduce(params, sh=(params[0], params[1], params[2]) if sh_exchange else None)
     train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
-    assert len(reducer._works) == (4 if sh_exchange else 6)
+    assert reducer.pending == 1 and reducer.launched_in_backward
     assert len(reducer._gathers) == (1 if sh_exchange else 0)
     reducer()
     out[rank] = [p.grad.detach().cpu() for p in g.params()]
@@ -357,7 +358,7 @@ def _views_worker(rank, world, port, out):
     ar = GradAllReduce(params, views_per_step=len(views))
     for v in views:  # two backwards per rank: the all-reduces start on the second
         _loss(params, v).backward()
-    pending = len(ar._works)
+    pending = ar.pending
     ar()
     out[rank] = ([p.grad.clone() for p in params], pending)
     ar.remove_hooks()
@@ -365,8 +366,8 @@ def _views_worker(rank, world, port, out):
 
 
 def test_two_views_per_rank_overlapped_gloo_world2():
-    """with several backwards per step the hooks start each all-reduce on the
-    step's last backward only; every rank ends with the sum over all 4 views."""
+    """with several backwards per step the bucket's all-reduce starts at the
+    end of the step's last backward only; every rank ends with the sum over all 4 views."""
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
@@ -377,7 +378,7 @@ def test_two_views_per_rank_overlapped_gloo_world2():
     for v in range(4):
         _loss(params, v).backward()
     (g0, n0), (g1, n1) = res[0], res[1]
-    assert n0 == n1 == 6
+    assert n0 == n1 == 1
     for a, b, p in zip(g0, g1, params):
         assert torch.equal(a, b)
         torch.testing.assert_close(a, p.grad, rtol=1e-6, atol=1e-6)
@@ -396,7 +397,7 @@ def _rebind_worker(rank, world, port, out):
             model["params"] = [torch.cat([p.detach(), p.detach()[:2] * 0.5]).requires_grad_(True)
                                for p in model["params"]]
         _loss(model["params"], 10 * step + rank).backward()
-        hooked = len(ar._works)
+        hooked = ar.pending
         ar()
         res.append(([p.grad.clone() for p in model["params"]], hooked))
         for p in model["params"]:
@@ -423,7 +424,7 @@ def test_exchange_follows_replaced_parameters_gloo_world2():
         for r in (0, 1):
             _loss(params, 10 * step + r).backward()
         (g0, h0), (g1, h1) = res[0][step], res[1][step]
-        assert h0 == h1 == (0 if step == 1 else 6), (step, h0)  # no hooks on the fresh tensors yet
+        assert h0 == h1 == (0 if step == 1 else 1), (step, h0)  # no hooks on the fresh tensors yet
         for a, b, p in zip(g0, g1, params):
             assert torch.equal(a, b) and a.shape == p.shape
             torch.testing.assert_close(a, p.grad, rtol=1e-6, atol=1e-6)
@@ -695,6 +696,9 @@ def _rccl_worker(rank, world, port, out):
             ar = GradAllReduce(params, sh=(params[0], params[1], params[2]) if mode == "sh_colour" else None,
                                comm_force=True)
         train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
+        import diff_gaussian_rasterization as dgr
+        plan = dgr.last_leaf_plan
+        launched = ar is not None and ar.launched_in_backward
         if ar is not None:
             ar()
             ar.remove_hooks()
@@ -702,7 +706,7 @@ def _rccl_worker(rank, world, port, out):
         red = reduce_densification_stats(*stats, force=True)
         torch.cuda.synchronize()
         res[mode] = ([p.grad.detach().cpu().clone() for p in params],
-                     all(torch.equal(a, b) for a, b in zip(stats, red)))
+                     all(torch.equal(a, b) for a, b in zip(stats, red)), plan, launched)
     out[rank] = res
     dist.destroy_process_group()
 
@@ -721,9 +725,15 @@ def test_rccl_collectives_one_rank(dev):
         mp.spawn(_rccl_worker, args=(1, port, out), nprocs=1, join=True)
         res = dict(out)[0]
     plain = res["plain"][0]
+    assert res["plain"][2] == ("opacities", "rotations", "scales", "sh")
+    # the fused leaf gradients survive the exchange — the rasterizer
+    # writes xyz / opacity / scaling / rotation (and the SH leaves without the SH
+    # exchange) into the bucket, whose one all-reduce starts at the end of backward
+    assert res["sh_colour"][2] == ("means3D", "opacities", "rotations", "scales")
+    assert res["allreduce"][2] == ("means3D", "opacities", "rotations", "scales", "sh")
     for mode in ("allreduce", "sh_colour"):
-        grads, stats_same = res[mode]
-        assert stats_same, mode
+        grads, stats_same, _, launched = res[mode]
+        assert stats_same and launched, mode
         for i, (a, b) in enumerate(zip(grads, plain)):
             rel = (a - b).norm() / b.norm().clamp_min(1e-30)
             assert rel < 1e-5, (mode, i, float(rel))

@@ -1,0 +1,107 @@
+"""No kernel reads scratch it did not write in the same call.
+
+Round 3 had a silent all-zero backward: a control flag living in caller-owned
+scratch (the caching allocator hands back whatever the previous user left) was
+read before this call wrote it.  Here every output and scratch buffer the entry
+points allocate (geom, binning, img, accum, the gradients) is filled with a poison
+byte instead of being left uninitialised (``_C._poison``): 0xFF makes every float
+a NaN and every integer all ones, 0x5A a large finite float and a large count.  The
+image, radii and n_contrib must equal the normal run bit for bit and every gradient
+must match it to the atomics-order noise floor — through the reference-shaped
+``render()`` autograd path (fused leaf gradients, both tile footprints, a retained
+graph's second backward, the SH-exchange sink) and through ``_C`` directly."""
+import numpy as np
+import pytest
+import torch
+
+import diff_gaussian_rasterization as dgr
+from diff_gaussian_rasterization import _C
+from helpers import case, rel_l2
+
+POISONS = (0xFF, 0x5A)
+
+
+def _autograd_run(cam, g, dev, poison, footprint, retain=False, sink=False):
+    import train_step
+    from multiview import GradAllReduce
+
+    gd = g.to(dev, requires_grad=True)
+    prev_fp, prev_poison = dgr.set_footprint(footprint), _C._poison
+    _C._poison = poison
+    ar = None
+    try:
+        if sink:  # the view-parallel SH sink, forced on in a process without a group
+            params = gd.params()
+            ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), sh_force=True)
+        out = train_step.render(cam.to(dev), gd, torch.zeros(3, device=dev))
+        dL = torch.from_numpy(np.random.default_rng(7).standard_normal(out["render"].shape).astype(np.float32))
+        loss = (out["render"] * dL.to(dev)).sum() * 1e-3
+        loss.backward(retain_graph=retain)
+        if retain:
+            loss.backward()
+        if ar is not None:
+            ar()
+        torch.cuda.synchronize()
+        grads = [p.grad.detach().cpu().clone() for p in gd.params()] + [out["viewspace_points"].grad.cpu().clone()]
+        return out["render"].detach().cpu(), out["radii"].cpu(), grads
+    finally:
+        if ar is not None:
+            ar.remove_hooks()
+        _C._poison = prev_poison
+        dgr.set_footprint(prev_fp)
+
+
+CASES = {
+    "A": (10_000, 256, 256, 0),
+    "B": (100_000, 800, 800, 3),
+    "P200": (200, 96, 64, 3),  # one preprocess workgroup: the round-3 stale-flag case
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("footprint", ["rect", "tight"])
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("mode", ["plain", "retain_graph", "sh_sink"])
+def test_poisoned_scratch_autograd(dev, name, footprint, mode):
+    P, W, H, deg = CASES[name]
+    cam, g = case(P, W, H, deg, seed=3, view=2)
+    kw = dict(retain=mode == "retain_graph", sink=mode == "sh_sink" and deg > 0)
+    img0, radii0, g0 = _autograd_run(cam, g, dev, None, footprint, **kw)
+    _, _, g1 = _autograd_run(cam, g, dev, None, footprint, **kw)  # the atomics-order noise floor
+    for poison in POISONS:
+        img, radii, gp = _autograd_run(cam, g, dev, poison, footprint, **kw)
+        assert torch.equal(img, img0), (poison, float((img - img0).abs().max()))
+        assert torch.equal(radii, radii0), poison
+        for i, (a, b, b2) in enumerate(zip(gp, g0, g1)):
+            assert torch.isfinite(a).all(), (poison, i)
+            noise = rel_l2(b2.numpy(), b.numpy())
+            assert rel_l2(a.numpy(), b.numpy()) <= max(1e-6, 4 * noise), (poison, i, noise)
+        assert float(g0[0].abs().max()) > 0  # the xyz gradient is not the silent all-zero one
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("footprint", ["rect", "tight"])
+def test_poisoned_scratch_entry_points(dev, footprint):
+    """_C directly (upstream's entry points, row-layout dsh): the forward's
+    intermediates — n_contrib, final_T, ranges, point_list — equal the normal run's."""
+    from helpers import random_dL, run_hip
+
+    cam, g = case(100_000, 800, 800, 3, seed=4, view=5)
+    dL = random_dL(800, 800)
+    prev = _C._poison
+    try:
+        ref = run_hip(cam, g, dev, dL=dL, footprint=footprint)
+        ref2 = run_hip(cam, g, dev, dL=dL, footprint=footprint)
+        for poison in POISONS:
+            _C._poison = poison
+            got = run_hip(cam, g, dev, dL=dL, footprint=footprint)
+            _C._poison = prev
+            assert got["num_rendered"] == ref["num_rendered"]
+            for k in ("color", "radii", "n_contrib", "final_T", "ranges", "point_list", "depth_order"):
+                np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} poison={poison:#x}")
+            for k, v in got["grads"].items():
+                noise = rel_l2(ref2["grads"][k], ref["grads"][k])
+                assert np.isfinite(v).all(), k
+                assert rel_l2(v, ref["grads"][k]) <= max(1e-6, 4 * noise), (k, poison)
+    finally:
+        _C._poison = prev

@@ -54,7 +54,7 @@ class OracleC:
         return f["num_rendered"], torch.from_numpy(f["color"]), torch.from_numpy(f["radii"]), tag, tag.clone(), \
             tag.clone()
 
-    def _rasterize(self, *args):  # the autograd Function's entry: + its validated inputs (none here)
+    def _rasterize(self, *args, **kw):  # the autograd Function's entry: + its validated inputs (none here)
         return (*self.rasterize_gaussians(*args), None)
 
     def rasterize_gaussians_backward(self, bg, means3D, radii, colors, scales, rotations, scale_modifier,

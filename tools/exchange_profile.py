@@ -1,0 +1,107 @@
+"""Where the view-parallel exchange's per-rank cost goes, on one GPU (config C).
+
+Variants, alternating, each timed over --steps steps:
+  plain    — the N = 1 step (fused leaf gradients, no exchange);
+  local    — the SH colour exchange forced on without a process group (the record
+             is its own gather, no RCCL): the rasterizer-side and rebuild cost;
+  rccl     — a one-rank RCCL group with every collective forced on (the bench's
+             exchange_1rank): + the bucket all-reduce, the record all-gather.
+Per variant: it/s, and the mean host time spent inside the forward's one host sync
+(gsr_forward_preprocess): near zero means the step is host-bound.
+usage (on the box): python tools/exchange_profile.py [--steps 60] [--rounds 2]"""
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "3dgs_study_amd"), ROOT]
+
+import diff_gaussian_rasterization as dgr  # noqa: E402
+import synthetic  # noqa: E402
+import train_step  # noqa: E402
+from diff_gaussian_rasterization import _C  # noqa: E402
+from multiview import GradAllReduce  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--rounds", type=int, default=2)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    cfg = synthetic.CONFIGS["C"]
+    cam = synthetic.make_camera(cfg["W"], cfg["H"], view=0).to(dev)
+    g = synthetic.make_gaussians(cfg["P"], cfg["sh_degree"], seed=0).to(dev, requires_grad=True)
+    target = synthetic.make_target(cfg["W"], cfg["H"], seed=1).to(dev)
+    bg = torch.zeros(3, device=dev)
+    params = g.params()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+
+    lib = _C.load_library()
+    orig = lib.gsr_forward_preprocess
+    sync = {"t": 0.0, "n": 0}
+
+    def wrapped(*a):
+        t0 = time.perf_counter()
+        r = orig(*a)
+        sync["t"] += time.perf_counter() - t0
+        sync["n"] += 1
+        return r
+
+    lib.gsr_forward_preprocess = wrapped
+    res = {}
+    for rnd in range(args.rounds):
+        for name in ("plain", "local", "rccl"):
+            ar = None
+            if name == "local":
+                ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), sh_force=True, timing=True)
+            elif name == "rccl":
+                ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), comm_force=True, timing=True)
+
+            def step():
+                for p in params:
+                    p.grad = None
+                train_step.train_step(cam, g, target, bg)
+                if ar is not None:
+                    ar()
+
+            for _ in range(10):
+                step()
+            torch.cuda.synchronize()
+            if ar is not None:
+                ar.reset_stats()
+            sync["t"], sync["n"] = 0.0, 0
+            t0 = time.perf_counter()
+            host = 0.0
+            for _ in range(args.steps):
+                h0 = time.perf_counter()
+                step()
+                host += time.perf_counter() - h0
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            r = {"it_s": round(args.steps / dt, 1), "ms": round(1e3 * dt / args.steps, 4),
+                 "sync_wait_ms": round(1e3 * sync["t"] / max(sync["n"], 1), 4),
+                 "plan": list(dgr.last_leaf_plan)}
+            if ar is not None:
+                st = ar.stats()
+                r.update(wait_ms=round(st["exchange_wait_ms"], 4), rebuild_ms=round(st["sh_rebuild_ms"], 4))
+                ar.remove_hooks()
+            res.setdefault(name, []).append(r)
+            print(name, rnd, r, flush=True)
+    dist.destroy_process_group()
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
