@@ -540,7 +540,11 @@ __global__ void __launch_bounds__(RG_THREADS)
 // per instance: 8 dependent LDS reads and a k-th-set-bit search each); 16
 // instances per thread left too few threads busy per workgroup at config C
 // (28 -> 50 us), and stores straight from the walk were uncoalesced (58 us).
-constexpr int EMIT_IPT = 4;
+#ifndef GSR_EMIT_IPT
+#define GSR_EMIT_IPT 4
+#endif
+constexpr int EMIT_IPT = GSR_EMIT_IPT;
+constexpr int EMIT_LOG2 = __builtin_ctz(EMIT_BLOCK);
 struct EmitArgs {
     int P, gx;
     // packed two-pass tile sort: tile_keys receives one byte per instance (the
@@ -592,7 +596,7 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
         if (j0 < tot) {
             int g = 0, hi = EMIT_BLOCK;  // largest g with loff[g] <= j0 (it has v > 0)
 #pragma unroll
-            for (int step = 0; step < 8; step++) {
+            for (int step = 0; step < EMIT_LOG2; step++) {
                 const int mid = (g + hi) >> 1;
                 if (loff[mid] <= j0) g = mid; else hi = mid;
             }

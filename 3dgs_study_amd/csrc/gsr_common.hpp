@@ -47,7 +47,11 @@ constexpr int TSORT_ITEMS = GSR_TSORT_ITEMS;
 constexpr int TSORT_ITEMS_BIG = 16;
 constexpr int64_t TSORT_BIG_N = 16 << 20;
 __host__ __device__ inline int tsort_items(int64_t n) { return n > TSORT_BIG_N ? TSORT_ITEMS_BIG : TSORT_ITEMS; }
-constexpr int EMIT_BLOCK = 256;  // Gaussians per rank-order emit workgroup
+#ifndef GSR_EMIT_BLOCK
+#define GSR_EMIT_BLOCK 256
+#endif
+constexpr int EMIT_BLOCK = GSR_EMIT_BLOCK;  // Gaussians per rank-order emit workgroup (a power of two, 64..1024)
+static_assert(EMIT_BLOCK >= 64 && EMIT_BLOCK <= 1024 && (EMIT_BLOCK & (EMIT_BLOCK - 1)) == 0, "EMIT_BLOCK");
 // rank_gather_kernel (binning.hip): 1024 threads x 4 ranks = RG_SUPER emit blocks
 constexpr int RG_THREADS = 1024, RG_RANKS = 4, RG_SUPER = RG_THREADS * RG_RANKS / EMIT_BLOCK;
 constexpr int PRE_THREADS = 256;          // preprocess block (scan granule)
@@ -149,6 +153,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_totals = take((size_t)RADIX * 4);
     L.dsort_minmax = take((size_t)radix_blocks(P, dsort_items(P)) * 8);
     L.dsort_ctrl = take(CTRL_WORDS * 4);
+    L.off[GSR_GEOM_DSORT_CTRL] = L.dsort_ctrl;
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
     L.emit_super = take((size_t)rg_blocks(P) * 4 + 4);
     L.order_cnt = take((8 * 32 + 2) * 4);

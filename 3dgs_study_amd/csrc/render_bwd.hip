@@ -190,6 +190,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // more ds_swizzle stages (xor 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per
     // output register) and one final v_permlane32 self-swap adding the two halves.
     auto reduce_emit = [&](const Part &pa, const Part &pb, uint32_t gida, uint32_t gidb, bool two) {
+#ifdef GSR_BWD_SETPRIO  // experiment: the dependent exchange chain first in the SIMD's arbitration
+        __builtin_amdgcn_s_setprio(GSR_BWD_SETPRIO);
+#endif
         const float k5 = h16 ? pb.g5 : pa.g5, s5 = h16 ? pa.g5 : pb.g5;
         const float kx = h16 ? pb.dx : pa.dx, sx = h16 ? pa.dx : pb.dx;
         const float ky = h16 ? pb.dy : pa.dy, sy = h16 ? pa.dy : pb.dy;
@@ -229,6 +232,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         // compiler's atomic optimizer (a wave-scan loop) out
         if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, v);
         if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
+#ifdef GSR_BWD_SETPRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
     };
 
     // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l),

@@ -528,6 +528,7 @@ def layouts(P, W, H, num_rendered):
     nb = lib.gsr_binning_layout(num_rendered, W, H, b, 16)
     im = (ctypes.c_size_t * 16)()
     ni = lib.gsr_img_layout(W, H, im, 16)
-    geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "ranges", "ctrl", "depth_order")
+    geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "ranges", "ctrl", "depth_order",
+                  "dsort_ctrl")
     return (dict(zip(geom_names, list(g)[:n])), dict(zip(("keys", "point_list"), list(b)[:nb])),
             dict(zip(("final_T", "n_contrib"), list(im)[:ni])))

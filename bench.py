@@ -400,8 +400,11 @@ def main():
                 line["config_E_render_rect"] = render_rates("E", dev, args.render_steps, 3, footprint="rect")
         if world == 1 and args.exchange_steps > 0:
             del out
-            line["exchange_1rank"] = exchange_one_rank_rates(cam, P, deg, target, bg, args.exchange_steps, args.warmup,
-                                                             line["ms_per_step"])
+            try:  # a side measurement: it must never cost the headline line
+                line["exchange_1rank"] = exchange_one_rank_rates(cam, P, deg, target, bg, args.exchange_steps,
+                                                                 args.warmup, line["ms_per_step"])
+            except Exception as e:  # noqa: BLE001
+                line["exchange_1rank"] = {"status": "failed", "error": f"{type(e).__name__}: {e}"[:300]}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)

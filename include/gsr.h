@@ -272,6 +272,7 @@ enum gsr_geom_field {
     GSR_GEOM_RANGES,         /* uint2  [T]  [start,end) of each tile in point_list */
     GSR_GEOM_CTRL,           /* uint32 [16] num_rendered, status flags */
     GSR_GEOM_DEPTH_ORDER,    /* uint32 [P]  Gaussian ids in (depth_bits, id) order */
+    GSR_GEOM_DSORT_CTRL,     /* uint32 [16] the depth sort's key base (low byte clear) and pass count (3 or 4) */
     GSR_GEOM_NFIELDS
 };
 enum gsr_binning_field {

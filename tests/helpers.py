@@ -92,6 +92,7 @@ def read_intermediates(geom, binning, img, P, W, H, I):
     d["ctrl"] = _view(geom, go["ctrl"], 16, torch.int32, np.uint32)
     d["ranges"] = _view(geom, go["ranges"], 2 * T, torch.int32, np.uint32).reshape(T, 2)
     d["depth_order"] = _view(geom, go["depth_order"], P, torch.int32, np.uint32)
+    d["dsort_ctrl"] = _view(geom, go["dsort_ctrl"], 16, torch.int32, np.uint32)
     d["point_list"] = _view(binning, bo["point_list"], I, torch.int32, np.uint32) if I > 0 else np.zeros(0, np.uint32)
     d["final_T"] = _view(img, io["final_T"], W * H, torch.float32, np.float32).reshape(H, W)
     d["n_contrib"] = _view(img, io["n_contrib"], W * H, torch.int32, np.uint32).reshape(H, W)

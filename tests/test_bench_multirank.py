@@ -43,3 +43,17 @@ def test_bench_multirank_line(n, exchange):
     assert d["scaling"] == "weak" and d["steps"] == 3 and d["warmup"] == 1
     assert d["value"] > 0 and d["value"] == pytest.approx(n * 3 / (d["ms_per_step"] * 3e-3), rel=1e-3)
     assert ("all-gather" in d["config"]["parallelism"]) == (exchange == "sh-colour")
+    # where the N > 1 step's time goes: the compute stream's wait for the
+    # collectives and the SH rebuild, max over the ranks, and the bytes each rank sends
+    ex = d["exchange"]
+    assert ex["calls"] == 3 and ex["exchange_wait_ms"] >= 0 and ex["sh_rebuild_ms"] >= 0
+    if exchange == "sh-colour":
+        assert ex["sh_rebuild_ms"] > 0
+    else:  # nothing between the two events
+        assert ex["sh_rebuild_ms"] < 0.05
+    P = d["config"]["gaussians"]
+    floats = (3 + 1 + 3 + 4) if exchange == "sh-colour" else 59
+    record = 4 * (4 + (3 * P + 3) // 4 * 4) if exchange == "sh-colour" else 0
+    assert ex["bytes_per_rank"] == 4 * floats * P + record
+    # the fused leaf gradients survive the exchange: the rasterizer writes them into the bucket
+    assert set(ex["fused_leaves"]) >= {"means3D", "opacities", "rotations", "scales"}

@@ -532,7 +532,8 @@ def test_depth_sort_pass_count(dev, oracle, radius, passes, footprint):
     cam, g = case(20_000, 160, 120, 1, seed=7, radius=radius)
     dL = random_dL(120, 160)
     h = run_hip(cam, g, dev, dL=dL, footprint=footprint)
-    assert int(h["ctrl"][4]) == passes
+    assert int(h["dsort_ctrl"][1]) == passes  # binning.hip DCTRL_PASSES, decided on the device
+    assert int(h["dsort_ctrl"][0]) & 0xFF == 0  # DCTRL_KEY_BASE: the low byte cleared
     r = run_oracle(oracle, cam, g)
     check_forward(h, r)
     check_backward(h, oracle.backward(r, dL))
