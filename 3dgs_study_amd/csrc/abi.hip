@@ -66,21 +66,22 @@ struct StageTimer {
     int64_t launches[GSR_STAGE_COUNT] = {};
 };
 StageTimer g_timer;  // the ABI is driven from one host thread per process
+size_t g_open[GSR_STAGE_COUNT];  // gsr_timing_begin: the pool slot whose end event is pending, + 1
 
 const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess",     "scan",        "depth_sort",           "duplicate",
                                             "tile_sort",      "render_fwd",  "render_bwd",           "preprocess_bwd",
-                                            "bwd_prepare",    "depth_sort_concurrent"};
+                                            "bwd_prepare",    "depth_sort_concurrent", "exchange_wait",
+                                            "sh_rebuild"};
 
 // st | TIMED_MORE: more work of a stage already counted once in this step (its
 // time is added, its launch count is not)
 constexpr int TIMED_MORE = 0x100;
-template <typename F>
-hipError_t timed(int st, hipStream_t s, F &&launch) {
-    if (!(g_timer.mask & (1 << (st & 0xff)))) return launch();
+// The next pool pair for stage st (created on first use).  Timing-only events: no
+// system-scope fence on record (a default event's cache writeback / invalidate
+// opened a ~6 us idle gap before the next kernel and cooled its caches); the
+// elapsed time is read after a stream sync.
+hipError_t take_pair(int st, std::pair<hipEvent_t, hipEvent_t> **out) {
     if (g_timer.used == g_timer.pool.size()) {
-        // timing-only events: no system-scope fence on record (a default event's
-        // cache writeback / invalidate opened a ~6 us idle gap before the next kernel
-        // and cooled its caches); the elapsed time is read after a stream sync
         hipEvent_t a, b;
         hipError_t e = hipEventCreateWithFlags(&a, hipEventDisableSystemFence);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&b, hipEventDisableSystemFence);
@@ -88,14 +89,23 @@ hipError_t timed(int st, hipStream_t s, F &&launch) {
         g_timer.pool.emplace_back(a, b);
         g_timer.stage.push_back(st);
     }
-    auto &ev = g_timer.pool[g_timer.used];
+    *out = &g_timer.pool[g_timer.used];
     g_timer.stage[g_timer.used] = st;
     g_timer.used++;
-    hipError_t e = hipEventRecord(ev.first, s);
+    return hipSuccess;
+}
+
+template <typename F>
+hipError_t timed(int st, hipStream_t s, F &&launch) {
+    if (!(g_timer.mask & (1 << (st & 0xff)))) return launch();
+    std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
+    hipError_t e = take_pair(st, &ev);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(ev->first, s);
     if (e != hipSuccess) return e;
     e = launch();
     if (e != hipSuccess) return e;
-    return hipEventRecord(ev.second, s);
+    return hipEventRecord(ev->second, s);
 }
 
 // upstream debug mode: synchronise and check after every kernel
@@ -505,6 +515,7 @@ int gsr_knn_mean_dist2(int32_t P, const float *points, float *dist2, void *scrat
 int gsr_timing_enable(int mask) {
     g_timer.mask = mask;
     g_timer.used = 0;
+    for (auto &o : g_open) o = 0;
     for (int k = 0; k < GSR_STAGE_COUNT; k++) {
         g_timer.total_ms[k] = 0;
         g_timer.launches[k] = 0;
@@ -522,6 +533,7 @@ int gsr_timing_read(double *total_ms, int64_t *launches, int cap) {
         g_timer.launches[g_timer.stage[i] & 0xff] += (g_timer.stage[i] & TIMED_MORE) ? 0 : 1;
     }
     g_timer.used = 0;
+    for (auto &o : g_open) o = 0;
     int n = 0;
     for (; n < cap && n < GSR_STAGE_COUNT; n++) {
         if (total_ms) total_ms[n] = g_timer.total_ms[n];
@@ -531,5 +543,26 @@ int gsr_timing_read(double *total_ms, int64_t *launches, int cap) {
 }
 
 const char *gsr_stage_name(int stage) { return (stage >= 0 && stage < GSR_STAGE_COUNT) ? kStageNames[stage] : ""; }
+
+int gsr_timing_begin(int stage, void *stream) {
+    if (stage < 0 || stage >= GSR_STAGE_COUNT) return fail(GSR_ERR_ARGS, "timing stage %d out of range", stage);
+    if (!(g_timer.mask & (1 << stage))) return GSR_OK;
+    std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
+    if (int rc = check_hip(take_pair(stage, &ev), "timing begin")) return rc;
+    g_open[stage] = g_timer.used;  // the pair's slot + 1
+    hipStream_t s = (hipStream_t)stream;
+    // the end event is recorded here too (a read before gsr_timing_end then sees an
+    // empty region, not an unrecorded event) and again by gsr_timing_end
+    if (int rc = check_hip(hipEventRecord(ev->first, s), "timing begin")) return rc;
+    return check_hip(hipEventRecord(ev->second, s), "timing begin");
+}
+
+int gsr_timing_end(int stage, void *stream) {
+    if (stage < 0 || stage >= GSR_STAGE_COUNT) return fail(GSR_ERR_ARGS, "timing stage %d out of range", stage);
+    if (!(g_timer.mask & (1 << stage)) || g_open[stage] == 0) return GSR_OK;
+    auto &ev = g_timer.pool[g_open[stage] - 1];
+    g_open[stage] = 0;
+    return check_hip(hipEventRecord(ev.second, (hipStream_t)stream), "timing end");
+}
 
 }  // extern "C"

@@ -56,7 +56,7 @@ EXPORTED = (
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
-    "gsr_build_id", "gsr_backward_phase",
+    "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -209,6 +209,9 @@ def load_library():
     lib.gsr_timing_read.restype = ctypes.c_int
     lib.gsr_stage_name.argtypes = [ctypes.c_int]
     lib.gsr_stage_name.restype = ctypes.c_char_p
+    for name in ("gsr_timing_begin", "gsr_timing_end"):
+        getattr(lib, name).argtypes = [ctypes.c_int, vp]
+        getattr(lib, name).restype = ctypes.c_int
     lib.gsr_l1_ssim_scratch_bytes.argtypes = [i32, i32, i32]
     lib.gsr_l1_ssim_scratch_bytes.restype = sz
     lib.gsr_l1_ssim.argtypes = [vp, vp, i32, i32, i32, ctypes.c_float, vp, vp, vp, vp]
@@ -492,6 +495,32 @@ def timing_enable(on=True):
         for n in on:
             mask |= 1 << names.index(n)
     lib.gsr_timing_enable(mask)
+
+
+_stage_ids = {}
+
+
+def _stage_id(name: str) -> int:
+    if not _stage_ids:
+        lib = load_library()
+        for i in range(32):
+            n = lib.gsr_stage_name(i).decode()
+            if not n:
+                break
+            _stage_ids[n] = i
+    return _stage_ids[name]
+
+
+def timing_begin(name: str, device) -> None:
+    """Open a caller-marked region of stage `name` on the current stream (recorded
+    only while timing_enable has that stage on; fence-free events)."""
+    lib = load_library()
+    _check(lib.gsr_timing_begin(_stage_id(name), _stream(device)), "gsr_timing_begin")
+
+
+def timing_end(name: str, device) -> None:
+    lib = load_library()
+    _check(lib.gsr_timing_end(_stage_id(name), _stream(device)), "gsr_timing_end")
 
 
 def timing_read() -> dict:

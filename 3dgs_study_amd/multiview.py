@@ -99,7 +99,6 @@ class GradAllReduce:
         self.launched_in_backward = False  # the bucket's all-reduce started from the end-of-backward callback
         self._timing = timing
         self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0}
-        self._tpending = []
         self._prev_ex = None
         self._installed = False
         self._sh_on = sh is not None and (sh_force or self._active())
@@ -311,38 +310,37 @@ class GradAllReduce:
             self._sh = None
             self._sh_on = False
 
-    # ---- timing (bench.py's N > 1 line)
-    def _mark(self):
+    # ---- timing (bench.py's N > 1 line): on a GPU the regions are the library's
+    # fence-free stage events (stages "exchange_wait" / "sh_rebuild", recorded while
+    # _C.timing_enable has them on, read with _C.timing_read); on the CPU host clocks
+    def _begin(self, name):
         if not self._timing:
-            return None
+            return
         if self._reduced and self._reduced[0].is_cuda:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            return e
-        return time.perf_counter()
+            from diff_gaussian_rasterization import _C
+            _C.timing_begin(name, self._reduced[0].device)
+        else:
+            self._t0 = time.perf_counter()
+
+    def _end(self, name):
+        if not self._timing:
+            return
+        if self._reduced and self._reduced[0].is_cuda:
+            from diff_gaussian_rasterization import _C
+            _C.timing_end(name, self._reduced[0].device)
+        else:
+            self._tstats[name + "_ms"] += 1e3 * (time.perf_counter() - self._t0)
 
     def stats(self) -> dict:
-        """Means per __call__ since the last reset: exchange_wait_ms (how long the
-        compute stream waits for the records' all-gather and, after the SH rebuild,
-        for the bucket's all-reduce), sh_rebuild_ms (the SH gradients from the
-        gathered records), and the bytes this rank contributes per step."""
-        for a, b, c, d in self._tpending:
-            if isinstance(a, float):
-                w, r = (b - a + d - c) * 1e3, (c - b) * 1e3
-            else:
-                d.synchronize()
-                w, r = a.elapsed_time(b) + c.elapsed_time(d), b.elapsed_time(c)
-            self._tstats["exchange_wait_ms"] += w
-            self._tstats["sh_rebuild_ms"] += r
-            self._tstats["calls"] += 1
-        self._tpending = []
+        """Per-__call__ means since the last reset of the host-clock regions (CPU
+        tensors; on a GPU the regions are library stages, read by the caller with
+        _C.timing_read), the calls, and the bytes this rank contributes per step."""
         n = max(self._tstats["calls"], 1)
         return {"exchange_wait_ms": self._tstats["exchange_wait_ms"] / n,
                 "sh_rebuild_ms": self._tstats["sh_rebuild_ms"] / n, "calls": self._tstats["calls"],
                 "bytes_per_rank": self.nbytes}
 
     def reset_stats(self) -> None:
-        self.stats()
         self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0}
 
     def __call__(self):
@@ -363,19 +361,20 @@ class GradAllReduce:
         bucket = self._bucket
         # the SH rebuild needs only the gathered records: it runs while the bucket's
         # all-reduce is still in flight, and the compute stream waits for the bucket last
-        t0 = self._mark()
+        self._begin("exchange_wait")
         for _, _, w in self._gathers:
             if w is not None:
                 w.wait()
-        t1 = self._mark()
+        self._end("exchange_wait")
         if self._sh is not None:
+            self._begin("sh_rebuild")
             self._finish_sh()
-        t2 = self._mark()
+            self._end("sh_rebuild")
+        self._begin("exchange_wait")
         if self._work is not None:
             self._work.wait()
-        t3 = self._mark()
-        if t0 is not None:
-            self._tpending.append((t0, t1, t2, t3))
+        self._end("exchange_wait")
+        self._tstats["calls"] += 1
         self._work = None
         self._bucket = self._views = None  # the grads keep the storage; next step gets a fresh bucket
         self._backwards = 0

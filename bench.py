@@ -296,7 +296,10 @@ def main():
         per_stage, dom = stage_split(one_step, args.steps)
     # Timed region: K steps; events around the dominant stage give its live
     # average launch time (the roofline).
-    _C.timing_enable({"split": [dom], "all": True, "none": False}[args.stage_events])
+    on = {"split": [dom], "all": True, "none": False}[args.stage_events]
+    if world > 1 and on is not True:
+        on = (on or []) + list(EXCHANGE_STAGES)
+    _C.timing_enable(on)
     torch.cuda.synchronize()
     if world > 1:
         reducer.reset_stats()
@@ -314,7 +317,8 @@ def main():
     exchange = None
     if world > 1:
         ex = reducer.stats()
-        t = torch.tensor([elapsed, ex["exchange_wait_ms"], ex["sh_rebuild_ms"]], device=dev, dtype=torch.float64)
+        wait_ms, rebuild_ms = _exchange_split(stages, ex["calls"])
+        t = torch.tensor([elapsed, wait_ms, rebuild_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0].item())
         import diff_gaussian_rasterization as dgr
@@ -325,7 +329,7 @@ def main():
                     "fused_leaves": list(dgr.last_leaf_plan), "stat": "max over ranks of the per-step mean"}
     if args.stage_events == "all":
         per_stage = {k: (ms / n if n else 0.0, n) for k, (ms, n) in stages.items() if n}
-        dom = max(per_stage, key=lambda k: per_stage[k][0] * per_stage[k][1]) if per_stage else "render_bwd"
+        dom = _dominant(per_stage)
     dom_live = stages.get(dom, (0.0, 0))
 
     if rank == 0:
@@ -434,8 +438,24 @@ def stage_split(step_fn, steps: int):
     stages = _C.timing_read()
     _C.timing_enable(False)
     per = {k: (ms / n, n) for k, (ms, n) in stages.items() if n}
-    dom = max(per, key=lambda k: per[k][0] * per[k][1]) if per else "render_bwd"
-    return per, dom
+    return per, _dominant(per)
+
+
+# stages the caller marks around the exchange (multiview.GradAllReduce): regions of a
+# step, not kernels, so never the roofline's kernel
+EXCHANGE_STAGES = ("exchange_wait", "sh_rebuild")
+
+
+def _dominant(per: dict) -> str:
+    ks = [k for k in per if k not in EXCHANGE_STAGES]
+    return max(ks, key=lambda k: per[k][0] * per[k][1]) if ks else "render_bwd"
+
+
+def _exchange_split(stages: dict, calls: int) -> tuple:
+    """Per-call means (ms) of the exchange's two regions from the library's stage
+    events: the compute stream's wait for the collectives, the SH rebuild."""
+    n = max(calls, 1)
+    return tuple(stages.get(k, (0.0, 0))[0] / n for k in EXCHANGE_STAGES)
 
 
 def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
@@ -483,6 +503,7 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
     import diff_gaussian_rasterization as dgr
     import synthetic
     import train_step
+    from diff_gaussian_rasterization import _C
     from multiview import GradAllReduce
 
     sock = socket.socket()
@@ -506,12 +527,16 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
             step()
         torch.cuda.synchronize()
         ar.reset_stats()
+        _C.timing_enable(list(EXCHANGE_STAGES))
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        stages = _C.timing_read()
+        _C.timing_enable(False)
         st = ar.stats()
+        st["exchange_wait_ms"], st["sh_rebuild_ms"] = _exchange_split(stages, st["calls"])
         plan = list(dgr.last_leaf_plan)
         ar.remove_hooks()
         del g, params

@@ -312,11 +312,18 @@ enum gsr_stage {
     GSR_STAGE_BWD_PREPARE,    /* accumulator zeroing + the render backward's wave order (no upstream kernel) */
     GSR_STAGE_DSORT_CONCURRENT, /* the depth sort on its own stream, concurrent with preprocess; GSR_STAGE_DEPTH_SORT
                                    is its exposed part on the launch stream (the join + rank-order gather) */
+    GSR_STAGE_EXCHANGE_WAIT,  /* caller-marked (gsr_timing_begin/end): the view-parallel exchange's wait for its collectives */
+    GSR_STAGE_SH_REBUILD,     /* caller-marked: the SH gradients rebuilt from the gathered colour records */
     GSR_STAGE_COUNT
 };
 int gsr_timing_enable(int mask);
 int gsr_timing_read(double *total_ms, int64_t *launches, int cap);
 const char *gsr_stage_name(int stage);
+/* A caller-marked region of `stage` on `stream` (the same fence-free events as the
+ * library's own stages; nothing is recorded unless the stage's bit is enabled):
+ * begin and end pair up per stage; each pair counts one launch. */
+int gsr_timing_begin(int stage, void *stream);
+int gsr_timing_end(int stage, void *stream);
 
 /* ---- Training-step ops after the rasterizer (SURVEY.md §8f "next" rows 1-2) ----
  *

@@ -120,9 +120,9 @@ def test_sh_exchange_entry_points_validate(lib):
 def test_stage_names(lib):
     from diff_gaussian_rasterization import _C
 
-    names = [lib.gsr_stage_name(i).decode() for i in range(10)]
+    names = [lib.gsr_stage_name(i).decode() for i in range(12)]
     assert names == ["preprocess", "scan", "depth_sort", "duplicate", "tile_sort", "render_fwd", "render_bwd",
-                     "preprocess_bwd", "bwd_prepare", "depth_sort_concurrent"]
+                     "preprocess_bwd", "bwd_prepare", "depth_sort_concurrent", "exchange_wait", "sh_rebuild"]
     assert lib.gsr_stage_name(99).decode() == ""
     _C.timing_enable(True)
     assert _C.timing_read() == {n: (0.0, 0) for n in names}

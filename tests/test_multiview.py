@@ -737,3 +737,80 @@ def test_rccl_collectives_one_rank(dev):
         for i, (a, b) in enumerate(zip(grads, plain)):
             rel = (a - b).norm() / b.norm().clamp_min(1e-30)
             assert rel < 1e-5, (mode, i, float(rel))
+
+
+# ---------------------------------------------------------------- the bucket protocol with fused writers (CPU)
+class _FusedWriter(torch.autograd.Function):
+    """Stands in for the rasterizer's fused leaf gradients: its backward asks the
+    installed exchange for bucket views of the leaves it writes (xyz and opacity
+    here), writes (or, when the view is already the leaf's .grad, adds) their
+    gradients itself and returns None for them; the other inputs get theirs through
+    autograd, as unfusable ones do."""
+
+    @staticmethod
+    def forward(ctx, xyz, opacity, rest, w):
+        ctx.save_for_backward(xyz, opacity, rest)
+        ctx.w = w
+        return (w * (xyz * xyz).sum() + w * (opacity * opacity).sum() + w * (rest * rest).sum()).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        import diff_gaussian_rasterization as dgr
+
+        xyz, opacity, rest = ctx.saved_tensors
+        ex = dgr._exchange
+        views = ex.leaf_bucket({"xyz": (xyz,), "opacity": (opacity,)}) if ex is not None else {}
+        out = []
+        for name, leaf in (("xyz", xyz), ("opacity", opacity)):
+            v = views.get(name)
+            val = 2 * ctx.w * leaf.detach() * g
+            if v is None:
+                out.append(val)
+                continue
+            if leaf.grad is None:
+                v[0].copy_(val)
+                leaf.grad = v[0]
+            else:
+                v[0].add_(val)
+            out.append(None)
+        return out[0], out[1], 2 * ctx.w * rest.detach() * g, None
+
+
+def _fused_worker(rank, world, port, out, views_per_step):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    xyz, opacity, rest = (torch.randn(s, requires_grad=True) for s in ((7, 3), (7, 1), (7, 4)))
+    ar = GradAllReduce([xyz, rest, opacity], views_per_step=views_per_step)
+    for v in range(views_per_step):
+        w = float(rank + 1) * (v + 1)
+        _FusedWriter.apply(xyz, opacity, rest, w).backward()
+    launched, pending = ar.launched_in_backward, ar.pending
+    flat = ar()
+    grads = [p.grad.clone() for p in (xyz, opacity, rest)]
+    views_ok = all(p.grad.data_ptr() >= flat.data_ptr() and
+                   p.grad.data_ptr() < flat.data_ptr() + flat.numel() * 4 for p in (xyz, opacity, rest))
+    out[rank] = (grads, [p.detach().clone() for p in (xyz, opacity, rest)], launched, pending, views_ok)
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("views_per_step", [1, 2])
+def test_bucket_with_fused_writers_gloo_world2(views_per_step):
+    """leaves whose gradients a fused backward writes straight into the
+    exchange's bucket (the first backward writes, a later one of the step adds) and a
+    leaf that goes through autograd share ONE bucket; its single all-reduce starts at
+    the end of the step's last backward, and every rank ends with the sum of both
+    ranks' views, every .grad a view of the bucket."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_fused_worker, args=(2, port, out, views_per_step), nprocs=2, join=True)
+        res = dict(out)
+    (g0, p, l0, n0, v0), (g1, _, l1, n1, v1) = res[0], res[1]
+    assert l0 and l1 and n0 == n1 == 1 and v0 and v1
+    wsum = sum(float(r + 1) * (v + 1) for r in (0, 1) for v in range(views_per_step))
+    for a, b, x in zip(g0, g1, p):
+        assert torch.equal(a, b)
+        torch.testing.assert_close(a, 2 * wsum * x, rtol=1e-6, atol=1e-6)

@@ -81,6 +81,7 @@ def main():
             torch.cuda.synchronize()
             if ar is not None:
                 ar.reset_stats()
+            _C.timing_enable(["exchange_wait", "sh_rebuild"])
             sync["t"], sync["n"] = 0.0, 0
             t0 = time.perf_counter()
             host = 0.0
@@ -90,12 +91,15 @@ def main():
                 host += time.perf_counter() - h0
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
+            stages = _C.timing_read()
+            _C.timing_enable(False)
             r = {"it_s": round(args.steps / dt, 1), "ms": round(1e3 * dt / args.steps, 4),
                  "sync_wait_ms": round(1e3 * sync["t"] / max(sync["n"], 1), 4),
                  "plan": list(dgr.last_leaf_plan)}
             if ar is not None:
-                st = ar.stats()
-                r.update(wait_ms=round(st["exchange_wait_ms"], 4), rebuild_ms=round(st["sh_rebuild_ms"], 4))
+                n = max(ar.stats()["calls"], 1)
+                r.update(wait_ms=round(stages["exchange_wait"][0] / n, 4),
+                         rebuild_ms=round(stages["sh_rebuild"][0] / n, 4))
                 ar.remove_hooks()
             res.setdefault(name, []).append(r)
             print(name, rnd, r, flush=True)
