@@ -388,6 +388,7 @@ def main():
                 # the blend loops are issue-bound, not byte-bound: PMC VALU issue share
                 "valu_issue_frac": pmc_stage(dom).get("valu_issue_frac"),
             },
+            **({"exchange": exchange} if exchange is not None else {}),
             "cpu_baseline": None,
             # SHA-256 of the sources the loaded libgsr.so was built from (tools/build_id.py)
             "build_id": _C.load_library().gsr_build_id().decode(),

@@ -33,6 +33,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--only", default="plain,local,rccl", help="comma-separated variants to run")
+    ap.add_argument("--no-wrap", action="store_true", help="do not time the forward's host sync")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -59,10 +61,11 @@ def main():
         sync["n"] += 1
         return r
 
-    lib.gsr_forward_preprocess = wrapped
+    if not args.no_wrap:
+        lib.gsr_forward_preprocess = wrapped
     res = {}
     for rnd in range(args.rounds):
-        for name in ("plain", "local", "rccl"):
+        for name in args.only.split(","):
             ar = None
             if name == "local":
                 ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), sh_force=True, timing=True)
