@@ -8,6 +8,7 @@
 // Python side).  The only host synchronisation is the num_rendered read-back
 // in gsr_forward_preprocess, as upstream.
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <utility>
@@ -110,6 +111,19 @@ hipError_t timed(int st, hipStream_t s, F &&launch) {
 
 // upstream debug mode: synchronise and check after every kernel
 int side_stream(hipStream_t main, SideStream **out) {
+    // Off by default (GSR_SIDE_STREAM=1 turns it on): the concurrent depth sort
+    // measured no faster than in line (1,014-1,028 vs 1,020 it/s at C), and once the
+    // process holds an eagerly initialised RCCL communicator (init_process_group with
+    // device_id) any second stream of ours took the whole step from 0.98 to 2.2-2.4 ms
+    // (DESIGN §9, round 4): every kernel ran ~2x longer.
+    static const bool off = [] {
+        const char *e = getenv("GSR_SIDE_STREAM");
+        return !(e && e[0] == '1');
+    }();
+    if (off) {
+        *out = nullptr;
+        return GSR_OK;
+    }
     int dev = 0;
     if (int rc = check_hip(hipStreamGetDevice(main, &dev), "hipStreamGetDevice")) return rc;
     if (dev < 0 || dev >= MAX_DEVICES) return fail(GSR_ERR_ARGS, "device %d out of range", dev);
@@ -120,7 +134,9 @@ int side_stream(hipStream_t main, SideStream **out) {
         if (e == hipSuccess && cur != dev) e = hipSetDevice(dev);
         int least = 0, greatest = 0;
         if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, greatest);
+        const char *pe = getenv("GSR_SIDE_PRIORITY");  // diagnostics: "normal" = the default priority
+        const bool hi = !(pe && pe[0] == 'n');
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, hi ? greatest : least);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&x.join, hipEventDisableTiming);
         if (cur != dev) (void)hipSetDevice(cur);
@@ -230,8 +246,9 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     const bool dbg = in->debug != 0;
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
-    // The depth sort needs only the view depths: it runs on its own stream beside
-    // preprocess (debug mode: in line, so every kernel is checked on one stream).
+    // The depth sort needs only the view depths.  By default it runs in line, before
+    // preprocess; with GSR_SIDE_STREAM=1 on the library's second stream beside
+    // preprocess (debug mode: always in line, every kernel checked on one stream).
     SideStream *side = nullptr;
     if (!dbg)
         if (int rc = side_stream(s, &side)) return rc;
@@ -240,21 +257,20 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
         if (int rc = check_hip(hipEventRecord(side->fork, s), "fork")) return rc;
         if (int rc = check_hip(hipStreamWaitEvent(ds, side->fork, 0), "fork")) return rc;
     }
-    if (int rc = step(timed(GSR_STAGE_DSORT_CONCURRENT, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, ds); }), "depth sort", dbg, ds))
+    const int sort_stage = side ? GSR_STAGE_DSORT_CONCURRENT : GSR_STAGE_DEPTH_SORT;
+    if (int rc = step(timed(sort_stage, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, ds); }), "depth sort", dbg, ds))
         return rc;
     if (side)
         if (int rc = check_hip(hipEventRecord(side->join, ds), "join")) return rc;
     if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s); }), "preprocess", dbg, s)) return rc;
     if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
-    // the sort's exposed part: waiting for its stream, then the rects in rank order
-    // and the emission offsets (queued before the host waits, so the device stays busy)
-    if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] {
-                          if (side) {
-                              hipError_t e = hipStreamWaitEvent(s, side->join, 0);
-                              if (e != hipSuccess) return e;
-                          }
-                          return launch_rank_gather(in->P, in->W, in->H, geom, s);
-                      }),
+    // concurrent mode: the sort's exposed part, the launch stream's wait for its stream
+    if (side)
+        if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] { return hipStreamWaitEvent(s, side->join, 0); }), "join", dbg, s))
+            return rc;
+    // the rects in rank order and the emission offsets (upstream's InclusiveSum of
+    // tiles_touched, in depth order), queued before the host waits: the device stays busy
+    if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, s); }),
                       "rank gather", dbg, s))
         return rc;
     if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;

@@ -77,8 +77,8 @@ def iter_bytes(P: int, I: int, W: int, H: int, M: int, backward: bool = True) ->
     return float(fwd + (bwd if backward else 0))
 
 
-RASTER_STAGES = ("preprocess", "depth_sort", "duplicate", "tile_sort", "render_fwd", "bwd_prepare", "render_bwd",
-                 "preprocess_bwd")
+RASTER_STAGES = ("preprocess", "depth_sort", "scan", "duplicate", "tile_sort", "render_fwd", "bwd_prepare",
+                 "render_bwd", "preprocess_bwd")
 
 
 def raster_ms(per_stage: dict) -> float:

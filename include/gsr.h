@@ -302,16 +302,16 @@ int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap);
  * negative on error).  A stage is one launch_* group of kernels. */
 enum gsr_stage {
     GSR_STAGE_PREPROCESS = 0, /* FORWARD::preprocessCUDA */
-    GSR_STAGE_SCAN,           /* InclusiveSum of tiles_touched */
-    GSR_STAGE_DEPTH_SORT,     /* stable sort of the P depths + rank-order instance offsets */
+    GSR_STAGE_SCAN,           /* InclusiveSum of tiles_touched: the rects in depth order + emission offsets */
+    GSR_STAGE_DEPTH_SORT,     /* stable sort of the P depths (in line; with the side stream: the wait for it) */
     GSR_STAGE_DUPLICATE,      /* duplicateWithKeys in depth order */
     GSR_STAGE_TILE_SORT,      /* stable sort by tile (SortPairs) + identifyTileRanges */
     GSR_STAGE_RENDER_FWD,     /* FORWARD::renderCUDA */
     GSR_STAGE_RENDER_BWD,     /* BACKWARD::renderCUDA */
     GSR_STAGE_PREPROCESS_BWD, /* BACKWARD::computeCov2DCUDA + preprocessCUDA */
     GSR_STAGE_BWD_PREPARE,    /* accumulator zeroing + the render backward's wave order (no upstream kernel) */
-    GSR_STAGE_DSORT_CONCURRENT, /* the depth sort on its own stream, concurrent with preprocess; GSR_STAGE_DEPTH_SORT
-                                   is its exposed part on the launch stream (the join + rank-order gather) */
+    GSR_STAGE_DSORT_CONCURRENT, /* GSR_SIDE_STREAM=1 only: the depth sort on the library's second stream beside
+                                   preprocess; GSR_STAGE_DEPTH_SORT is then its exposed part (the launch stream's wait) */
     GSR_STAGE_EXCHANGE_WAIT,  /* caller-marked (gsr_timing_begin/end): the view-parallel exchange's wait for its collectives */
     GSR_STAGE_SH_REBUILD,     /* caller-marked: the SH gradients rebuilt from the gathered colour records */
     GSR_STAGE_COUNT

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--only", default="plain,local,rccl", help="comma-separated variants to run")
     ap.add_argument("--no-wrap", action="store_true", help="do not time the forward's host sync")
+    ap.add_argument("--pg", default="eager", choices=["eager", "lazy", "none"],
+                    help="process group: RCCL with device_id (eager communicator), without (lazy), or none")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -48,7 +50,9 @@ def main():
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    if args.pg != "none":
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=dev if args.pg == "eager" else None)
 
     lib = _C.load_library()
     orig = lib.gsr_forward_preprocess
@@ -106,7 +110,8 @@ def main():
                 ar.remove_hooks()
             res.setdefault(name, []).append(r)
             print(name, rnd, r, flush=True)
-    dist.destroy_process_group()
+    if args.pg != "none":
+        dist.destroy_process_group()
     print(json.dumps(res))
 
 
