@@ -162,6 +162,8 @@ int validate(const gsr_inputs *in, bool forward) {
     if (in->footprint != GSR_FOOTPRINT_RECT && in->footprint != GSR_FOOTPRINT_TIGHT)
         return fail(GSR_ERR_ARGS, "footprint must be GSR_FOOTPRINT_RECT or GSR_FOOTPRINT_TIGHT (got %d)", in->footprint);
     if (in->flags & ~GSR_FLAG_PREPARE_BACKWARD) return fail(GSR_ERR_ARGS, "unknown flags 0x%x", in->flags);
+    if (in->activations & ~(GSR_ACT_OPACITY | GSR_ACT_SCALE | GSR_ACT_ROTATION))
+        return fail(GSR_ERR_ARGS, "unknown activations 0x%x", in->activations);
     if (in->P == 0) return GSR_OK;
     if (!in->means3D || !in->viewmatrix || !in->projmatrix || !in->bg || (forward && !in->opacities))
         return fail(GSR_ERR_ARGS, "missing required input (means3D/opacities/viewmatrix/projmatrix/bg)");
@@ -178,6 +180,8 @@ int validate(const gsr_inputs *in, bool forward) {
             return fail(GSR_ERR_ARGS, "sh has %d coefficients per channel, degree %d needs %d", in->M, in->D,
                         (in->D + 1) * (in->D + 1));
     }
+    if (in->sh_rest && (!in->sh || in->M < 2))
+        return fail(GSR_ERR_ARGS, "sh_rest needs sh (the DC coefficients) and M >= 2");
     return GSR_OK;
 }
 
@@ -341,8 +345,8 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     if (L.dsh_dc && (!in->sh || in->M <= 0 || (in->M > 1 && !L.dsh_rest)))
         return fail(GSR_ERR_ARGS, "leaf dsh: needs sh and dsh_rest (M > 1)");
     if ((L.dscaling || L.drotation) && !in->scales) return fail(GSR_ERR_ARGS, "leaf dscaling/drotation: needs scales");
-    if (L.drotation && (!L.rotation_norm || !in->rotations))
-        return fail(GSR_ERR_ARGS, "leaf drotation: needs rotations and rotation_norm");
+    if (L.drotation && (!in->rotations || (!L.rotation_norm && !(in->activations & GSR_ACT_ROTATION))))
+        return fail(GSR_ERR_ARGS, "leaf drotation: needs rotations and rotation_norm (or GSR_ACT_ROTATION)");
     if (L.dopacity && !in->opacities) return fail(GSR_ERR_ARGS, "leaf dopacity: needs opacities");
     if (drgb && (dsh || L.dsh_dc)) return fail(GSR_ERR_ARGS, "drgb replaces dsh: dsh / leaf dsh must be NULL with it");
     const bool internal = accum == nullptr;  // geom's accumulator (GSR_FLAG_PREPARE_BACKWARD may have zeroed it)

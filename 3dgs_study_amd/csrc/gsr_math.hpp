@@ -90,6 +90,30 @@ __device__ inline M3 quat_to_rot(float r, float x, float y, float z) {
                    2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
 }
 
+// GaussianModel's activations (scene/gaussian_model.py:107-126) as torch's GPU
+// kernels evaluate them, for inputs given as the stored parameters
+// (gsr_inputs.activations): sigmoid 1 / (1 + exp(-x)) and exp with the accurate
+// expf (torch's std::exp), F.normalize as x / clamp_min(||x||, 1e-12) with the
+// norm's squares summed pairwise, ((x0^2 + x1^2) + (x2^2 + x3^2)) — the order
+// torch's vector-norm reduction uses for four floats (tools/act_probe.py: equal on
+// 1M of 1M rows; sequential sums and fma chains miss 8-17 %).  No contraction.
+__device__ __forceinline__ float act_sigmoid(float x) {
+#pragma clang fp contract(off)
+    return 1.0f / (1.0f + expf(-x));
+}
+__device__ __forceinline__ float act_exp(float x) { return expf(x); }
+// q <- x / max(n, eps) in place; returns n = ||x|| (LinalgVectorNormBackward0's result)
+__device__ __forceinline__ float act_normalize(float q[4]) {
+#pragma clang fp contract(off)
+    const float s0 = q[0] * q[0], s1 = q[1] * q[1], s2 = q[2] * q[2], s3 = q[3] * q[3];
+    const float n = sqrtf((s0 + s1) + (s2 + s3));
+    const float d = n != n ? n : fmaxf(n, 1e-12f);  // clamp_min keeps a NaN
+#pragma unroll
+    for (int k = 0; k < 4; k++) q[k] = q[k] / d;
+    return n;
+}
+constexpr float ACT_ROTATION_EPS = 1e-12f;  // F.normalize's default eps
+
 // forward.cu computeCov3D: Sigma = (S R)^T (S R) in glm terms; q used as given.
 __device__ inline void compute_cov3d(float sx, float sy, float sz, float mod, float qr, float qx, float qy, float qz,
                                      float cov[6]) {

@@ -70,6 +70,35 @@ __device__ inline void rows_to_lds(const float *__restrict__ src, int g0, int n,
     }
 }
 
+// Rows [g0, g0 + n) of a row-major float [*, w] array into columns [c0, c0 + w) of
+// LDS rows of stride S: the SH storage's two leaves (_features_dc, w = 3, and
+// _features_rest, w = 3M - 3; gsr_inputs.sh_rest) staged side by side as one padded
+// row per Gaussian.  All threads of the workgroup must call it.
+template <int THREADS>
+__device__ inline void rows_to_lds_cols(const float *__restrict__ src, int g0, int n, int w, int c0, int S,
+                                        float *lds) {
+    const int total = n * w;
+    const float invw = 1.0f / (float)w;
+    const float *base = src + (size_t)g0 * w;
+    for (int e = threadIdx.x; e < total; e += THREADS) {
+        int r = (int)((float)e * invw);
+        r += ((r + 1) * w <= e) ? 1 : 0;
+        r -= (r * w > e) ? 1 : 0;
+        lds[r * S + c0 + (e - r * w)] = base[e];
+    }
+}
+
+// One Gaussian's degree-3 SH row (48 floats) from the split storage: 3 floats of
+// _features_dc and 45 of _features_rest (180-B rows, 4-byte aligned: the loads are
+// the compiler's to merge).
+__device__ __forceinline__ void load_sh_row_split(const float *__restrict__ dc, const float *__restrict__ rest,
+                                                  size_t li, float r[48]) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) r[k] = dc[3 * li + k];
+#pragma unroll
+    for (int k = 0; k < 45; k++) r[3 + k] = rest[45 * li + k];
+}
+
 // The reverse: LDS rows (stride RW + 1) -> global rows [g0, g0 + n).
 template <int THREADS, int RWC = 0>
 __device__ inline void lds_to_rows(const float *lds, int g0, int n, int RW_, float *__restrict__ dst) {

@@ -62,7 +62,9 @@ __device__ inline float sh_channel(const float *sh, int c, int deg, float x, flo
     return result + 0.5f;
 }
 
-template <int RWC>
+// SPLIT: the SH rows come from GaussianModel's two leaves (gsr_inputs.sh_rest)
+// instead of their cat.
+template <int RWC, bool SPLIT>
 __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) {
     __shared__ uint32_t wsum[PRE_THREADS / 64];
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
@@ -97,14 +99,32 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
 #pragma unroll
         for (int k = 0; k < 4; k++) gin[3 + k] = in.rotations[4 * (size_t)li + k];
     }
-    const float opac = in.opacities[li];
+    const float opac_in = in.opacities[li];
     float4 rowv[DIRECT ? 12 : 1];
-    if constexpr (DIRECT) {  // launched only with SH rows (16-B aligned)
+    if constexpr (DIRECT && SPLIT) {  // _features_dc + _features_rest rows, 4-B aligned
+        float r[48];
+        load_sh_row_split(in.sh, in.sh_rest, (size_t)li, r);
+#pragma unroll
+        for (int b = 0; b < 12; b++) rowv[b] = make_float4(r[4 * b], r[4 * b + 1], r[4 * b + 2], r[4 * b + 3]);
+    } else if constexpr (DIRECT) {  // launched only with SH rows (16-B aligned)
         const float4 *r4 = reinterpret_cast<const float4 *>(in.sh + (size_t)li * 48);
 #pragma unroll
         for (int b = 0; b < 12; b++) rowv[b] = r4[b];
     } else if (use_sh) {
-        rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
+        if constexpr (SPLIT) {
+            rows_to_lds_cols<PRE_THREADS>(in.sh, g0, n, 3, 0, RW + 1, sh_lds);
+            if (RW > 3) rows_to_lds_cols<PRE_THREADS>(in.sh_rest, g0, n, RW - 3, 3, RW + 1, sh_lds);
+        } else {
+            rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
+        }
+    }
+    // the stored parameters' activations (gsr_inputs.activations), as torch computes them
+    const float opac = (in.activations & GSR_ACT_OPACITY) ? act_sigmoid(opac_in) : opac_in;
+    if (!in.cov3D_precomp) {
+        if (in.activations & GSR_ACT_SCALE)
+#pragma unroll
+            for (int k = 0; k < 3; k++) gin[k] = act_exp(gin[k]);
+        if (in.activations & GSR_ACT_ROTATION) (void)act_normalize(gin + 3);
     }
     uint32_t touched = 0;
     bool perr = false;
@@ -343,20 +363,20 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
     a.radii = radii;
     a.order_cnt = at<uint32_t>(geom, L.order_cnt);
     const int nb = pre_blocks(in.P);
-    const bool direct = in.sh && !in.colors_precomp && 3 * in.M == 48 && ((uintptr_t)in.sh & 15u) == 0;
+    const bool split = in.sh_rest != nullptr;
+    // the register prefetch of cat rows reads them as float4: 16-B aligned only
+    const bool direct = in.sh && !in.colors_precomp && 3 * in.M == 48 && (split || ((uintptr_t)in.sh & 15u) == 0);
     const size_t lds = (in.sh && !in.colors_precomp && !direct) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     // SH row width as a compile-time constant for the common degrees (cheap LDS
     // row indexing); any other width takes the run-time path
-    switch (in.sh && !in.colors_precomp ? 3 * in.M : 0) {
-        case 3: hipLaunchKernelGGL(preprocess_fwd_kernel<3>, dim3(nb), dim3(PRE_THREADS), lds, s, a); break;
-        case 48:  // the register prefetch of the rows reads them as float4: 16-B aligned only
-            if (((uintptr_t)in.sh & 15u) == 0) {
-                hipLaunchKernelGGL(preprocess_fwd_kernel<48>, dim3(nb), dim3(PRE_THREADS), lds, s, a);
-                break;
-            }
-            [[fallthrough]];
-        default: hipLaunchKernelGGL(preprocess_fwd_kernel<0>, dim3(nb), dim3(PRE_THREADS), lds, s, a); break;
-    }
+    const int width = in.sh && !in.colors_precomp ? 3 * in.M : 0;
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(nb), dim3(PRE_THREADS), lds, s, a); };
+    if (width == 3)
+        split ? go(preprocess_fwd_kernel<3, true>) : go(preprocess_fwd_kernel<3, false>);
+    else if (width == 48 && direct)
+        split ? go(preprocess_fwd_kernel<48, true>) : go(preprocess_fwd_kernel<48, false>);
+    else
+        split ? go(preprocess_fwd_kernel<0, true>) : go(preprocess_fwd_kernel<0, false>);
     hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint4 *)a.block_sums, nb,
                        at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl);
     return hipGetLastError();

@@ -149,8 +149,8 @@ struct ShStage {
     bool vis;
 };
 __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 mean, const float gin[7],
-                                       const float4 acc0, const float4 acc1, float accb, float opac, int32_t rad,
-                                       uint32_t cl, const Mat4 &V, const Mat4 &Pm);
+                                       const float4 acc0, const float4 acc1, float accb, float opac, float qnorm,
+                                       int32_t rad, uint32_t cl, const Mat4 &V, const Mat4 &Pm);
 
 // One workgroup = PB_THREADS consecutive Gaussians.  Each thread loads its own
 // inputs first and, at SH degree 3, its own 192-B SH row once the geometry
@@ -161,7 +161,8 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
 // LDS stage the kernel runs 4 waves per SIMD instead of 3 (112 -> 102 us at config
 // C); forcing 5 or 6 spilled (160 us).  Other degrees stage the workgroup's rows
 // through LDS and stream them back out coalesced.
-template <int RWC>
+// SPLIT: the SH rows come from GaussianModel's two leaves (gsr_inputs.sh_rest).
+template <int RWC, bool SPLIT>
 __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PB_THREADS][3M + 1]
     const gsr_inputs &in = a.in;
@@ -198,29 +199,51 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const float accb = acc[8];                                       // color b
     // the sums' per-Gaussian opacity factor: the caller's opacities (coalesced), else
     // the forward's splat record (4 B out of every 48)
-    const float opac = in.opacities ? in.opacities[li] : a.splat_f[12 * (size_t)li + 5];
+    const float opac_in = in.opacities ? in.opacities[li] : a.splat_f[12 * (size_t)li + 5];
     const int32_t rad = a.radii[li];
     const uint32_t cl = a.clamped[li];
     float rowv[DIRECT ? 48 : 1];
-    auto load_row = [&]() {  // launched only with staged (stage == true), 16-B aligned SH rows
-        const float4 *r4 = reinterpret_cast<const float4 *>(in.sh + (size_t)li * 48);
+    auto load_row = [&]() {  // launched only with staged (stage == true) SH rows: 16-B aligned cat rows, or split
+        if constexpr (SPLIT) {
+            load_sh_row_split(in.sh, in.sh_rest, (size_t)li, rowv);
+        } else {
+            const float4 *r4 = reinterpret_cast<const float4 *>(in.sh + (size_t)li * 48);
 #pragma unroll
-        for (int b = 0; b < 12; b++) {
-            const float4 v = r4[b];
-            rowv[4 * b] = v.x;
-            rowv[4 * b + 1] = v.y;
-            rowv[4 * b + 2] = v.z;
-            rowv[4 * b + 3] = v.w;
+            for (int b = 0; b < 12; b++) {
+                const float4 v = r4[b];
+                rowv[4 * b] = v.x;
+                rowv[4 * b + 1] = v.y;
+                rowv[4 * b + 2] = v.z;
+                rowv[4 * b + 3] = v.w;
+            }
         }
     };
-    if constexpr (!DIRECT)
-        if (stage) rows_to_lds<PB_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
+    if constexpr (!DIRECT) {
+        if (stage) {
+            if constexpr (SPLIT) {
+                rows_to_lds_cols<PB_THREADS>(in.sh, g0, n, 3, 0, RW + 1, sh_lds);
+                if (RW > 3) rows_to_lds_cols<PB_THREADS>(in.sh_rest, g0, n, RW - 3, 3, RW + 1, sh_lds);
+            } else {
+                rows_to_lds<PB_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
+            }
+        }
+    }
+    // the stored parameters' activations (gsr_inputs.activations), as the forward
+    // applied them; qnorm = the rotation's norm for the normalize backward
+    const float opac = (in.activations & GSR_ACT_OPACITY) && in.opacities ? act_sigmoid(opac_in) : opac_in;
+    float qnorm = 0.f;
+    if (!in.cov3D_precomp) {
+        if (in.activations & GSR_ACT_SCALE)
+#pragma unroll
+            for (int k = 0; k < 3; k++) gin[k] = act_exp(gin[k]);
+        if (in.activations & GSR_ACT_ROTATION) qnorm = act_normalize(gin + 3);
+    }
     // pin the per-Gaussian loads ahead of the rows (the compiler would otherwise
     // sink them into the branch below, behind the rows, and wait for all of them)
     asm volatile("" ::"v"(acc0.x), "v"(acc0.y), "v"(acc0.z), "v"(acc0.w), "v"(acc1.x), "v"(acc1.y), "v"(acc1.z),
                  "v"(acc1.w), "v"(accb), "v"(opac), "v"(rad), "v"(cl));
     ShStage st{};
-    if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, opac, rad, cl, V, Pm);
+    if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, opac, qnorm, rad, cl, V, Pm);
     if constexpr (DIRECT)  // after the geometry (its registers are not held through it); culled: zeros
         if (live && st.vis) load_row();
     if (stage && !DIRECT) __syncthreads();
@@ -305,15 +328,23 @@ __device__ __forceinline__ void normalize_backward(const float g[4], const float
 // The activation gradients of one Gaussian (zeros for a culled one) go either to
 // upstream's outputs or, where the caller asked for them (gsr_leaf_grads), through
 // the activation's backward into its leaf's gradient.
+// With an activation bit (gsr_inputs.activations) the input is the stored parameter:
+// its gradient goes through the activation's backward into the leaf output if
+// given, else into the plain one.
 __device__ __forceinline__ void write_activation_grads(const PreBwdArgs &a, int idx, float dop, float opac,
                                                        const float ds[3], const float dq[4], const float gin[7],
-                                                       bool has_sr) {
+                                                       float qnorm, bool has_sr) {
     const BwdOutputs &o = a.o;
     const gsr_leaf_grads &L = o.leaf;
+    const int act = a.in.activations;
     auto put = [&](float *p, size_t i, float v, int bit) { p[i] = (L.accumulate & bit) ? p[i] + v : v; };
-    if (L.dopacity) {
-        const float sg = opac;  // = in.opacities[idx] (required with the leaf dopacity)
-        put(L.dopacity, idx, (dop * (1.0f - sg)) * sg, 4);  // sigmoid_backward: grad * (1 - y) * y
+    if (L.dopacity || (act & GSR_ACT_OPACITY)) {
+        const float sg = opac;  // sigmoid(x): in.opacities[idx], or the activation of the logit
+        const float v = (dop * (1.0f - sg)) * sg;  // sigmoid_backward: grad * (1 - y) * y
+        if (L.dopacity)
+            put(L.dopacity, idx, v, 4);
+        else if (o.dopacity)
+            o.dopacity[idx] = v;
     } else if (o.dopacity) {
         o.dopacity[idx] = dop;
     }
@@ -329,13 +360,22 @@ __device__ __forceinline__ void write_activation_grads(const PreBwdArgs &a, int 
         for (int k = 0; k < 3; k++) put(L.dscaling, 3 * (size_t)idx + k, ds[k] * gin[k], 2);  // exp: grad * result
     } else if (o.dscales) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) o.dscales[3 * (size_t)idx + k] = ds[k];
+        for (int k = 0; k < 3; k++) o.dscales[3 * (size_t)idx + k] = (act & GSR_ACT_SCALE) ? ds[k] * gin[k] : ds[k];
     }
-    if (L.drotation) {
+    if (L.drotation || (act & GSR_ACT_ROTATION)) {
         float dx[4];
-        normalize_backward(dq, gin + 3, L.rotation_norm[idx], L.rotation_eps, dx);  // gin[3..6] = q
+        const bool own = (act & GSR_ACT_ROTATION) != 0;  // the norm this kernel computed, else torch's
+        normalize_backward(dq, gin + 3, own ? qnorm : L.rotation_norm[idx], own ? ACT_ROTATION_EPS : L.rotation_eps,
+                           dx);  // gin[3..6] = q
+        float *dst = L.drotation ? L.drotation : o.drot;
+        if (dst)
 #pragma unroll
-        for (int k = 0; k < 4; k++) put(L.drotation, 4 * (size_t)idx + k, dx[k], 8);
+            for (int k = 0; k < 4; k++) {
+                if (L.drotation)
+                    put(dst, 4 * (size_t)idx + k, dx[k], 8);
+                else
+                    dst[4 * (size_t)idx + k] = dx[k];
+            }
     } else if (o.drot) {
 #pragma unroll
         for (int k = 0; k < 4; k++) o.drot[4 * (size_t)idx + k] = dq[k];
@@ -343,8 +383,8 @@ __device__ __forceinline__ void write_activation_grads(const PreBwdArgs &a, int 
 }
 
 __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 mean, const float gin[7],
-                                       const float4 acc0, const float4 acc1, float accb, float opac, int32_t rad,
-                                       uint32_t cl, const Mat4 &V, const Mat4 &Pm) {
+                                       const float4 acc0, const float4 acc1, float accb, float opac, float qnorm,
+                                       int32_t rad, uint32_t cl, const Mat4 &V, const Mat4 &Pm) {
     const gsr_inputs &in = a.in;
     const BwdOutputs &o = a.o;
     const bool has_sr = in.scales != nullptr;
@@ -359,7 +399,7 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
         if (o.dcov3D)
             for (int k = 0; k < 6; k++) o.dcov3D[6 * (size_t)idx + k] = 0.f;
         const float zs[3] = {0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
-        write_activation_grads(a, idx, 0.f, opac, zs, zq, gin, has_sr);
+        write_activation_grads(a, idx, 0.f, opac, zs, zq, gin, qnorm, has_sr);
         return st;  // dmeans3D (st.dmean = 0) and the dsh row are written by the caller
     }
     const float dcol[3] = {acc1.z, acc1.w, accb};
@@ -515,7 +555,7 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
                 4 * qz * (D(1, 1) + D(0, 0));
 #undef D
     }
-    write_activation_grads(a, idx, acc1.y, opac, ds, dq, gin, has_sr);
+    write_activation_grads(a, idx, acc1.y, opac, ds, dq, gin, qnorm, has_sr);
     return st;
 }
 
@@ -532,21 +572,20 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     a.accum = accum;
     a.o = o;
     const bool stage = in.sh && (o.dsh || o.drgb || o.sh_dir || o.leaf.dsh_dc) && in.M > 0;
-    const bool direct = stage && 3 * in.M == 48 && ((uintptr_t)in.sh & 15u) == 0 &&
+    const bool split = in.sh_rest != nullptr;
+    const bool direct = stage && 3 * in.M == 48 && (split || ((uintptr_t)in.sh & 15u) == 0) &&
                         (!a.o.dsh || a.o.dsh_planar || ((uintptr_t)a.o.dsh & 15u) == 0) &&
                         (!o.leaf.dsh_dc || ((uintptr_t)o.leaf.dsh_rest & 15u) == 0);
     const size_t lds = stage && !direct ? (size_t)PB_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     const dim3 grid((in.P + PB_THREADS - 1) / PB_THREADS);
-    switch (3 * in.M) {  // see launch_preprocess
-        case 3: hipLaunchKernelGGL(preprocess_bwd_kernel<3>, grid, dim3(PB_THREADS), lds, s, a); break;
-        case 48:  // the direct-row kernel needs staged, 16-B aligned rows; else the run-time width
-            if (direct) {
-                hipLaunchKernelGGL(preprocess_bwd_kernel<48>, grid, dim3(PB_THREADS), lds, s, a);
-                break;
-            }
-            [[fallthrough]];
-        default: hipLaunchKernelGGL(preprocess_bwd_kernel<0>, grid, dim3(PB_THREADS), lds, s, a); break;
-    }
+    // see launch_preprocess; the direct-row kernel needs staged rows (cat rows 16-B aligned)
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(PB_THREADS), lds, s, a); };
+    if (3 * in.M == 3)
+        split ? go(preprocess_bwd_kernel<3, true>) : go(preprocess_bwd_kernel<3, false>);
+    else if (3 * in.M == 48 && direct)
+        split ? go(preprocess_bwd_kernel<48, true>) : go(preprocess_bwd_kernel<48, false>);
+    else
+        split ? go(preprocess_bwd_kernel<0, true>) : go(preprocess_bwd_kernel<0, false>);
     return hipGetLastError();
 }
 

@@ -43,7 +43,14 @@ class GsrInputs(ctypes.Structure):
         ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p), ("rotations", ctypes.c_void_p),
         ("cov3D_precomp", ctypes.c_void_p), ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
         ("sh", ctypes.c_void_p), ("campos", ctypes.c_void_p),
+        ("sh_rest", ctypes.c_void_p), ("activations", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
+
+
+# gsr_activations (include/gsr.h): the inputs are GaussianModel's stored parameters
+# and the library applies sigmoid / exp / F.normalize itself (bit-identical to torch)
+ACT_OPACITY, ACT_SCALE, ACT_ROTATION = 1, 2, 4
+ACT_ALL = ACT_OPACITY | ACT_SCALE | ACT_ROTATION
 
 
 # every symbol include/gsr.h declares (checked by tests/test_abi.py)
@@ -144,7 +151,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lib = None
 
@@ -281,7 +288,8 @@ FLAG_PREPARE_BACKWARD = 1  # gsr.h gsr_flags
 
 
 def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
-            tan_fovx, tan_fovy, H, W, sh, degree, campos, prefiltered, debug, footprint=None, flags=0):
+            tan_fovx, tan_fovy, H, W, sh, degree, campos, prefiltered, debug, footprint=None, flags=0, sh_rest=None,
+            activations=0):
     if means3D.ndim != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     device = means3D.device
@@ -291,18 +299,24 @@ def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov
     keep = {}
     for name, t in (("background", bg), ("means3D", means3D), ("colors", colors), ("opacity", opacity),
                     ("scales", scales), ("rotations", rotations), ("cov3D_precomp", cov3D_precomp),
-                    ("viewmatrix", viewmatrix), ("projmatrix", projmatrix), ("sh", sh), ("campos", campos)):
+                    ("viewmatrix", viewmatrix), ("projmatrix", projmatrix), ("sh", sh), ("campos", campos),
+                    ("sh_rest", sh_rest)):
         keep[name] = _prep(t, name, device)
     P = means3D.size(0)
-    sh_t = keep["sh"]
+    sh_t, rest_t = keep["sh"], keep["sh_rest"]
     M = sh_t.size(1) if (sh_t is not None and sh_t.size(0) != 0) else 0
+    if rest_t is not None:  # GaussianModel's split SH storage: sh = _features_dc [P,1,3]
+        if sh_t is None or sh_t.shape[1:] != (1, 3) or rest_t.dim() != 3 or rest_t.size(0) != P or rest_t.size(2) != 3:
+            raise RuntimeError("sh_rest: expected sh = features_dc [P,1,3] and sh_rest = features_rest [P,M-1,3]")
+        M += rest_t.size(1)
     s = GsrInputs(P=P, D=int(degree), M=M, W=int(W), H=int(H), tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
                   scale_modifier=float(scale_modifier), prefiltered=int(bool(prefiltered)), debug=int(bool(debug)),
                   footprint=FOOTPRINTS[footprint or _footprint], flags=int(flags),
                   bg=_ptr(keep["background"]), means3D=_ptr(keep["means3D"]), colors_precomp=_ptr(keep["colors"]),
                   opacities=_ptr(keep["opacity"]), scales=_ptr(keep["scales"]), rotations=_ptr(keep["rotations"]),
                   cov3D_precomp=_ptr(keep["cov3D_precomp"]), viewmatrix=_ptr(keep["viewmatrix"]),
-                  projmatrix=_ptr(keep["projmatrix"]), sh=_ptr(sh_t), campos=_ptr(keep["campos"]))
+                  projmatrix=_ptr(keep["projmatrix"]), sh=_ptr(sh_t), campos=_ptr(keep["campos"]),
+                  sh_rest=_ptr(rest_t), activations=int(activations))
     return s, keep, device, M
 
 
@@ -327,18 +341,22 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
                projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-               footprint=None, prepare_backward=False):
+               footprint=None, prepare_backward=False, sh_rest=None, activations=0):
     """rasterize_gaussians plus its validated inputs ``(struct, kept tensors, device,
     M)``, which the autograd Function hands back to the backward (``inputs=``) so the
     same tensors are not re-checked there: the host's backward path is on the
-    step's critical path once the GPU work is short."""
+    step's critical path once the GPU work is short.  ``sh_rest`` / ``activations``
+    (not upstream; gsr_inputs): GaussianModel's stored parameters as the inputs —
+    ``sh`` = _features_dc and ``sh_rest`` = _features_rest instead of their cat, and
+    the ACT_* bits of the opacity / scale / rotation inputs the library activates."""
     lib = load_library()
     H, W = int(image_height), int(image_width)
     if footprint is not None and footprint not in FOOTPRINTS:
         raise ValueError(f"footprint must be one of {sorted(FOOTPRINTS)} (got {footprint!r})")
     s, keep, device, M = _inputs(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos,
-                                 prefiltered, debug, footprint, FLAG_PREPARE_BACKWARD if prepare_backward else 0)
+                                 prefiltered, debug, footprint, FLAG_PREPARE_BACKWARD if prepare_backward else 0,
+                                 sh_rest, activations)
     P = s.P
     out_color = _alloc((3, H, W), torch.float32, device)
     radii = _alloc((P,), torch.int32, device)

@@ -48,7 +48,8 @@ from . import _C
 
 from ._C import get_footprint, set_footprint  # noqa: E402
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "set_sh_grad_sink",
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "rasterize_model",
+           "set_sh_grad_sink",
            "set_grad_exchange", "set_footprint", "get_footprint", "set_fused_leaf_grads"]
 
 _exchange = None
@@ -275,12 +276,12 @@ def _call_native(fn, args, debug: bool, dump: str, stage: str):
 
 # the forward's validated inputs (_C._rasterize), by name: where each comes from
 _INPUT_SRC = ("background", "means3D", "colors", "opacity", "scales", "rotations", "cov3D_precomp", "viewmatrix",
-              "projmatrix", "sh", "campos")
+              "projmatrix", "sh", "campos", "sh_rest")
 
 
-def _input_sources(rs, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh):
+def _input_sources(rs, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sh_rest=None):
     return dict(zip(_INPUT_SRC, (rs.bg, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                                 rs.viewmatrix, rs.projmatrix, sh, rs.campos)))
+                                 rs.viewmatrix, rs.projmatrix, sh, rs.campos, sh_rest)))
 
 
 class _RasterizeGaussians(torch.autograd.Function):
@@ -360,6 +361,119 @@ class _RasterizeGaussians(torch.autograd.Function):
         return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
 
 
+class _RasterizeModel(torch.autograd.Function):
+    """The rasterizer over GaussianModel's stored parameters (not upstream; see
+    ``rasterize_model``): the library applies the activations and reads the SH from
+    the two leaves, and its backward writes the stored parameters' gradients."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, features_dc, features_rest, opacity, scaling, rotation, raster_settings):
+        rs = raster_settings
+        empty = _empty_like_device(means3D)
+        rest = features_rest if features_rest.numel() else None
+        args = (rs.bg, means3D, empty, opacity, scaling, rotation, rs.scale_modifier, empty, rs.viewmatrix,
+                rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, features_dc, rs.sh_degree,
+                rs.campos, rs.prefiltered, rs.debug)
+        prep = any(ctx.needs_input_grad[:7])
+        num_rendered, color, radii, geom, binning, img, (s, keep, device, M) = _call_native(
+            lambda *a: _C._rasterize(*a, prepare_backward=prep, sh_rest=rest, activations=_C.ACT_ALL), args, rs.debug,
+            "snapshot_fw.dump", "forward")
+        ctx.raster_settings = rs
+        ctx.num_rendered = num_rendered
+        src = _input_sources(rs, means3D, None, opacity, scaling, rotation, None, features_dc, rest)
+        copies = {k: t for k, t in keep.items() if t is not None and t is not src[k]}
+        ctx.inputs = (s, device, M, frozenset(k for k, t in keep.items() if t is not None), tuple(copies))
+        ctx.save_for_backward(means3D, features_dc, features_rest, opacity, scaling, rotation, radii, geom, binning,
+                              img, *copies.values())
+        ctx.mark_non_differentiable(radii)
+        return color, radii
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _grad_radii):
+        rs = ctx.raster_settings
+        saved = ctx.saved_tensors
+        means3D, f_dc, f_rest, opacity, scaling, rotation, radii, geom, binning, img = saved[:10]
+        s, device, M, present, copy_names = ctx.inputs
+        rest = f_rest if f_rest.numel() else None
+        src = _input_sources(rs, means3D, None, opacity, scaling, rotation, None, f_dc, rest)
+        src.update(zip(copy_names, saved[10:]))
+        inputs = (s, {k: (src[k] if k in present else None) for k in _INPUT_SRC}, device, M)
+        needs = ctx.needs_input_grad
+        ex = _exchange
+        # the view-parallel exchange takes the SH gradient as the view's colour
+        # gradient, and the all-reduced gradients land in its bucket where it offers one
+        sink_takes_sh = (ex is not None and (needs[2] or needs[3])
+                         and ex.accepts((f_dc, f_rest), means3D))
+        views = {}
+        if ex is not None:
+            want = {k: (t,) for k, t, n in (("means3D", means3D, needs[0]), ("opacities", opacity, needs[4]),
+                                            ("scales", scaling, needs[5]), ("rotations", rotation, needs[6]))
+                    if n and t.is_leaf}
+            views = ex.leaf_bucket(want) if want else {}
+        fresh, acc = [], 0
+
+        def out(name, leaf, shape, bit):
+            nonlocal acc
+            v = views.get(name)
+            if v is None:
+                return torch.empty(shape, dtype=torch.float32, device=device)
+            if leaf.grad is not None:  # a later backward of the step: add into the bucket view
+                acc |= bit
+            else:
+                fresh.append((leaf, v[0]))
+            return v[0]
+
+        P = means3D.size(0)
+        kw = {}
+        if not sink_takes_sh and (needs[2] or needs[3]):
+            kw["dsh_dc"] = torch.empty((P, 1, 3), dtype=torch.float32, device=device)
+            kw["dsh_rest"] = torch.empty((P, M - 1, 3), dtype=torch.float32, device=device)
+        kw["dopacity"] = out("opacities", opacity, (P, 1), 4)
+        kw["dscaling"] = out("scales", scaling, (P, 3), 2)
+        kw["drotation"] = out("rotations", rotation, (P, 4), 8)
+        kw["dmeans3D"] = out("means3D", means3D, (P, 3), 16)
+        leaf = _C.LeafGrads(accumulate=acc, **kw)
+        bkw = dict(inputs=inputs, leaf=leaf)
+        if sink_takes_sh:
+            rec = ex.record(P)
+            bkw["drgb_out"], bkw["on_drgb"] = rec[4:], lambda: ex.push(rec, rs.campos, rs.sh_degree)
+        args = (rs.bg, means3D, radii, None, scaling, rotation, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
+                rs.tanfovx, rs.tanfovy, grad_out_color, f_dc, rs.sh_degree, rs.campos, geom, ctx.num_rendered, binning,
+                img, rs.debug)
+        d_means2D = _call_native(lambda *a: _C.rasterize_gaussians_backward(*a, **bkw), args, rs.debug,
+                                 "snapshot_bw.dump", "backward")[0]
+        for p, g in fresh:
+            p.grad = g
+        global last_leaf_plan
+        last_leaf_plan = tuple(sorted(["means3D", "opacities", "rotations", "scales"] +
+                                      ([] if sink_takes_sh else ["sh"])))
+        bucketed = lambda name, g: None if name in views else g  # noqa: E731
+        d_rest = kw.get("dsh_rest") if rest is not None else (
+            torch.zeros_like(f_rest) if "dsh_rest" in kw else None)
+        return (bucketed("means3D", kw["dmeans3D"]), d_means2D, kw.get("dsh_dc"), d_rest,
+                bucketed("opacities", kw["dopacity"]), bucketed("scales", kw["dscaling"]),
+                bucketed("rotations", kw["drotation"]), None)
+
+
+def rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation, raster_settings):
+    """The rasterizer over GaussianModel's stored parameters (not upstream).
+
+    The reference renders with activations of the model's leaves
+    (gaussian_renderer/__init__.py:81-96 -> scene/gaussian_model.py:107-126):
+    ``shs = cat(_features_dc, _features_rest)`` (a 192 MB copy per view at 1M
+    Gaussians, SH3), ``opacities = sigmoid(_opacity)``, ``scales = exp(_scaling)``,
+    ``rotations = F.normalize(_rotation)``.  Here those leaves go in as they are: the
+    library reads the SH rows from both tensors and applies the activations with
+    torch's own operations in torch's order (include/gsr.h gsr_activations), so the
+    image and radii equal ``rasterize_gaussians`` on the activations bit for bit,
+    and the backward writes the leaves' gradients (through the activations'
+    backwards) — the same values the reference's autograd produces, without the cat,
+    the activation kernels, their backwards or the cat's slice copies.
+    ``means2D`` is the screen-space gradient carrier, as upstream."""
+    return _RasterizeModel.apply(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation,
+                                 raster_settings)
+
+
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                         raster_settings):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
@@ -395,6 +509,13 @@ class GaussianRasterizer(nn.Module):
         with torch.no_grad():
             rs = self.raster_settings
             return _C.mark_visible(positions, rs.viewmatrix, rs.projmatrix)
+
+    def forward_model(self, means3D, means2D, features_dc, features_rest, opacity, scaling, rotation):
+        """``rasterize_model`` with these settings: GaussianModel's stored parameters
+        (_xyz, _features_dc, _features_rest, _opacity, _scaling, _rotation) in place of
+        the activations ``forward`` takes."""
+        return rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation,
+                               self.raster_settings)
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
                 cov3D_precomp=None):

@@ -240,9 +240,10 @@ class GradAllReduce:
             self.launched_in_backward = True
 
     # ---- the rasterizer's SH sink
-    def accepts(self, sh: torch.Tensor, means3D: torch.Tensor) -> bool:
+    def accepts(self, sh, means3D: torch.Tensor) -> bool:
         """True when this backward's SH input is the bound model's (and the SH
-        exchange is on).  With more than one rank a mismatch raises: a silent local
+        exchange is on): the cat [P,M,3], or the (f_dc, f_rest) leaves themselves
+        (diff_gaussian_rasterization.rasterize_model).  With more than one rank a mismatch raises: a silent local
         dsh would leave this rank's SH gradient out of the exchange and the replicas
         would drift apart."""
         if not self._sh_on:
@@ -250,8 +251,11 @@ class GradAllReduce:
         if self._stale():  # the model's tensors were replaced (densify / prune): follow them
             self._bind()
         xyz, f_dc, f_rest = self._sh
-        ok = (means3D.data_ptr() == xyz.data_ptr() and sh.size(0) == xyz.size(0)
-              and sh.size(1) == f_dc.size(1) + f_rest.size(1))
+        if isinstance(sh, tuple):  # rasterize_model: GaussianModel's two SH leaves themselves
+            ok = means3D.data_ptr() == xyz.data_ptr() and sh[0] is f_dc and sh[1] is f_rest
+        else:
+            ok = (means3D.data_ptr() == xyz.data_ptr() and sh.size(0) == xyz.size(0)
+                  and sh.size(1) == f_dc.size(1) + f_rest.size(1))
         if not ok and self._active():
             raise RuntimeError("GradAllReduce: the rasterizer's SH input is not the bound model's "
                                f"(means3D {tuple(means3D.shape)} vs xyz {tuple(xyz.shape)}); pass params/sh as "

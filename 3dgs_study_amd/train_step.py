@@ -11,8 +11,16 @@ GPU box).  ``eval_sh`` / ``covariance`` restate utils/sh_utils.py:57-112 and
 utils/general_utils.py:86-128 + scene/gaussian_model.py:27-32 for the
 ``convert_SHs_python`` / ``compute_cov3D_python`` branches.
 
+``render_fused`` is the same render over GaussianModel's stored parameters
+(``diff_gaussian_rasterization.rasterize_model``): no SH cat, no activation
+kernels, the leaves' gradients written by the rasterizer's backward — the same
+image, radii and gradients.
+
 ``train_step`` is the unit bench.py times: one view's render, the loss of
-train.py:102-104 (L1, or L1 + 0.2·(1 - SSIM)), and ``loss.backward()``.
+train.py:102-104 (L1, or L1 + 0.2·(1 - SSIM)), and ``loss.backward()``; with
+``glue="fused"`` through ``render_fused`` and the fused loss kernel
+(``train_ops.l1_ssim_loss``), with ``glue="reference"`` through ``render`` and the
+reference's torch loss.
 """
 from __future__ import annotations
 
@@ -110,6 +118,37 @@ def render(viewpoint_camera, pc, bg_color: torch.Tensor, scaling_modifier: float
             "radii": radii}
 
 
+def stored_parameters(pc):
+    """GaussianModel's leaves (scene/gaussian_model.py:44-49: _xyz, _features_dc,
+    _features_rest, _opacity, _scaling, _rotation), from a reference GaussianModel or
+    a synthetic.SynthGaussians (same tensors without the underscores)."""
+    names = ("xyz", "features_dc", "features_rest", "opacity", "scaling", "rotation")
+    if hasattr(pc, "_xyz"):
+        return tuple(getattr(pc, "_" + n) for n in names)
+    return tuple(getattr(pc, n) for n in names)
+
+
+def render_fused(viewpoint_camera, pc, bg_color: torch.Tensor, scaling_modifier: float = 1.0,
+                 debug: bool = False) -> dict:
+    """``render`` (gaussian_renderer/__init__.py:20-112, SH and scale/rotation
+    branches) over the model's stored parameters: the rasterizer activates them and
+    reads the SH from _features_dc / _features_rest itself (rasterize_model).  The
+    screen-space gradient carrier is a zero leaf (upstream's ``zeros_like + 0`` with
+    ``retain_grad`` carries the same gradient in ``.grad``)."""
+    xyz, f_dc, f_rest, opacity, scaling, rotation = stored_parameters(pc)
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device)
+    raster_settings = GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+        tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5), bg=bg_color,
+        scale_modifier=scaling_modifier, viewmatrix=viewpoint_camera.world_view_transform,
+        projmatrix=viewpoint_camera.full_proj_transform, sh_degree=pc.active_sh_degree,
+        campos=viewpoint_camera.camera_center, prefiltered=False, debug=debug)
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    rendered_image, radii = rasterizer.forward_model(xyz, screenspace_points, f_dc, f_rest, opacity, scaling, rotation)
+    return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
+            "radii": radii}
+
+
 # ---------------------------------------------------------------- losses (utils/loss_utils.py)
 def l1_loss(network_output: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
     return torch.abs(network_output - gt).mean()
@@ -141,14 +180,29 @@ def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11) -> torch
     return ssim_map.mean()
 
 
-def train_step(camera, gaussians, target: torch.Tensor, bg: torch.Tensor, lambda_dssim: float = 0.0) -> dict:
+GLUES = ("fused", "reference")
+
+
+def train_step(camera, gaussians, target: torch.Tensor, bg: torch.Tensor, lambda_dssim: float = 0.0,
+               glue: str = "reference") -> dict:
     """render -> loss -> backward for one view (train.py:98-105). lambda_dssim=0 is the
-    L1-only headline unit; 0.2 is the reference's default loss."""
-    out = render(camera, gaussians, bg)
-    image = out["render"]
-    loss = l1_loss(image, target)
-    if lambda_dssim:
-        loss = (1.0 - lambda_dssim) * loss + lambda_dssim * (1.0 - ssim(image, target))
+    L1-only headline unit; 0.2 is the reference's default loss.
+    glue="reference": the reference's render() and torch loss; "fused": render_fused
+    and the fused loss kernel (same values)."""
+    if glue == "fused":
+        import train_ops
+
+        out = render_fused(camera, gaussians, bg)
+        image = out["render"]
+        loss = train_ops.l1_ssim_loss(image, target, lambda_dssim)
+    elif glue == "reference":
+        out = render(camera, gaussians, bg)
+        image = out["render"]
+        loss = l1_loss(image, target)
+        if lambda_dssim:
+            loss = (1.0 - lambda_dssim) * loss + lambda_dssim * (1.0 - ssim(image, target))
+    else:
+        raise ValueError(f"glue must be one of {GLUES} (got {glue!r})")
     loss.backward()
     out["loss"] = loss
     return out
@@ -240,8 +294,9 @@ def full_train_step(iteration: int, camera, gaussians, state: TrainState, target
                     bg: torch.Tensor, reducer=None) -> torch.Tensor:
     """One iteration of train.py:86-141 without logging, checkpoints and the periodic
     densify/prune/opacity reset: lr schedule, render, L1 + lambda (1 - SSIM), backward,
-    densification statistics, Adam step, zero_grad.  ``state.fused`` selects the HIP
-    loss/Adam/statistics kernels (train_ops.py) over the reference's torch ops.
+    densification statistics, Adam step, zero_grad.  ``state.fused`` selects
+    render_fused and the HIP loss/Adam/statistics kernels (train_ops.py) over the
+    reference's render() glue and torch ops.
 
     View-parallel: ``reducer`` (multiview.GradAllReduce over the
     process group) finishes the gradient exchange started inside the backward before
@@ -250,7 +305,7 @@ def full_train_step(iteration: int, camera, gaussians, state: TrainState, target
     densification statistics stay per rank until a densify step combines them
     (TrainState.reduce_densification_stats)."""
     state.update_learning_rate(iteration)
-    out = render(camera, gaussians, bg)
+    out = render_fused(camera, gaussians, bg) if state.fused else render(camera, gaussians, bg)
     image = out["render"]
     lam = state.opt["lambda_dssim"]
     if state.fused:

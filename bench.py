@@ -231,6 +231,12 @@ def main():
                          "(every collective runs; reported beside the plain step); 0 = skip")
     ap.add_argument("--render-steps", type=int, default=20,
                     help="timed forward-only renders of config E (5M, 4K) reported beside the C line; 0 = skip")
+    ap.add_argument("--glue", default="fused", choices=["fused", "reference"],
+                    help="the render/loss code around the rasterizer (train_step.py): 'fused' renders from "
+                         "GaussianModel's stored parameters (rasterize_model: no SH cat, in-kernel activations) "
+                         "with the fused loss kernel; 'reference' is the reference's render() + torch loss")
+    ap.add_argument("--glue-steps", type=int, default=100,
+                    help="N=1: timed steps of the same unit with the other glue, reported beside; 0 = skip")
     args = ap.parse_args()
 
     import torch
@@ -275,7 +281,7 @@ def main():
     def one_step():
         for p in params:
             p.grad = None
-        out = train_step.train_step(cam, g, target, bg, lambda_dssim=args.lambda_dssim)
+        out = train_step.train_step(cam, g, target, bg, lambda_dssim=args.lambda_dssim, glue=args.glue)
         if world > 1:
             reducer()  # wait for the exchange started inside backward (+ rebuild the SH gradients)
         return out
@@ -360,6 +366,7 @@ def main():
                 "gaussians": P, "width": W, "height": H, "sh_degree": deg,
                 "footprint": _C.get_footprint(), "num_rendered": I, "views_per_step": world,
                 "loss": "L1" if not args.lambda_dssim else f"L1+{args.lambda_dssim}*(1-SSIM)",
+                "glue": GLUE_NOTE[args.glue],
                 "parallelism": f"view-parallel x{world}" + (
                     (f", {coll} all-gather of per-view colour-gradient records + all-reduce of xyz/opacity/scaling/"
                      f"rotation, {reducer.nbytes / 1e6:.0f} MB sent per rank per step"
@@ -396,18 +403,26 @@ def main():
         if world == 1 and args.footprint_steps > 0:
             line["footprint_" + ("tight" if _C.get_footprint() == "rect" else "rect")] = footprint_rates(
                 one_step, cam, g, bg, args.footprint_steps, args.warmup)
+        if world == 1 and args.glue_steps > 0:
+            other = "reference" if args.glue == "fused" else "fused"
+            line[f"{other}_glue"] = glue_rates(cam, g, target, bg, other, args.glue_steps, args.warmup,
+                                               args.lambda_dssim)
         if world == 1 and args.full_steps > 0:
             line["full_step"] = full_step_rates(cam, P, deg, target, bg, args.full_steps)
         if world == 1 and args.render_steps > 0:
             out = None
-            line["config_E_render"] = render_rates("E", dev, args.render_steps, 3)
+            line["config_E_render"] = render_rates("E", dev, args.render_steps, 3, glue=args.glue)
             if _C.get_footprint() != "rect":  # upstream's instance set (I ~ 110M): the tile sort's stress case
-                line["config_E_render_rect"] = render_rates("E", dev, args.render_steps, 3, footprint="rect")
+                line["config_E_render_rect"] = render_rates("E", dev, args.render_steps, 3, footprint="rect",
+                                                            glue=args.glue)
+            if args.glue_steps > 0:
+                other = "reference" if args.glue == "fused" else "fused"
+                line[f"config_E_render_{other}_glue"] = render_rates("E", dev, args.render_steps, 3, glue=other)
         if world == 1 and args.exchange_steps > 0:
             del out
             try:  # a side measurement: it must never cost the headline line
                 line["exchange_1rank"] = exchange_one_rank_rates(cam, P, deg, target, bg, args.exchange_steps,
-                                                                 args.warmup, line["ms_per_step"])
+                                                                 args.warmup, line["ms_per_step"], args.glue)
             except Exception as e:  # noqa: BLE001
                 line["exchange_1rank"] = {"status": "failed", "error": f"{type(e).__name__}: {e}"[:300]}
         if world == 1 and not args.no_cpu_baseline:
@@ -488,7 +503,45 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
             "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * steps / dt / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmup: int, plain_ms: float) -> dict:
+GLUE_NOTE = {
+    "fused": "fused: train_step.render_fused (rasterize_model over GaussianModel's stored parameters: the SH read "
+             "from _features_dc/_features_rest without the cat, sigmoid/exp/normalize in the preprocess kernels, "
+             "the leaves' gradients written by the backward) + the fused L1 kernel; same image, radii and "
+             "gradients as the reference glue",
+    "reference": "reference: train_step.render (gaussian_renderer/__init__.py:20-112 restated: activations, SH cat) "
+                 "+ torch L1 (utils/loss_utils.py)",
+}
+
+
+def glue_rates(cam, g, target, bg, glue: str, steps: int, warmup: int, lambda_dssim: float) -> dict:
+    """The headline unit again with the other glue around the rasterizer."""
+    import torch
+
+    import train_step
+
+    params = g.params()
+
+    def step():
+        for p in params:
+            p.grad = None
+        train_step.train_step(cam, g, target, bg, lambda_dssim=lambda_dssim, glue=glue)
+
+    for _ in range(warmup):
+        step()
+    per, _ = stage_split(step, steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"glue": GLUE_NOTE[glue], "value": round(steps / dt, 3), "unit": "train-iters/s",
+            "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps,
+            "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "raster_ms": raster_ms(per)}
+
+
+def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmup: int, plain_ms: float,
+                            glue: str = "fused") -> dict:
     """The headline unit with the N > 1 exchange forced on in a one-rank RCCL group
     ("nccl" backend, comm_force): the SH gradient leaves the backward as the view's
     colour-gradient record (all-gathered) and is rebuilt by sh_grad_from_colors, the
@@ -521,7 +574,7 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
         def step():
             for p in params:
                 p.grad = None
-            train_step.train_step(cam, g, target, bg)
+            train_step.train_step(cam, g, target, bg, glue=glue)
             ar()
 
         for _ in range(warmup):
@@ -550,7 +603,8 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
             "bytes_per_rank": st["bytes_per_rank"], "collective_backend": "RCCL (one rank, every collective forced)"}
 
 
-def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0, footprint=None) -> dict:
+def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0, footprint=None,
+                 glue: str = "fused") -> dict:
     """Forward-only throughput of reference render() (render.py:37-49 renders under
     torch.no_grad()) at a forward-only config (E: 5M Gaussians, 4K, SH3): frames/s,
     Mpix/s, the per-stage split, and the largest stage's algorithmic bytes ÷ its live
@@ -560,13 +614,13 @@ def render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int = 0, foo
 
     prev = set_footprint(footprint) if footprint else None
     try:
-        return _render_rates(cfg_name, dev, steps, warmup, view)
+        return _render_rates(cfg_name, dev, steps, warmup, view, glue)
     finally:
         if prev is not None:
             set_footprint(prev)
 
 
-def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int) -> dict:
+def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: str = "fused") -> dict:
     import torch
 
     import synthetic
@@ -580,16 +634,17 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int) -> dic
     g = synthetic.make_gaussians(P, deg, seed=0).to(dev)
     bg = torch.zeros(3, device=dev)
     I = _last_num_rendered(cam, g, bg)
+    render = train_step.render_fused if glue == "fused" else train_step.render
     with torch.no_grad():
         for _ in range(warmup):
-            train_step.render(cam, g, bg)
+            render(cam, g, bg)
         # the largest stage by measured time, from a steady-state block of its own
-        per, dom = stage_split(lambda: train_step.render(cam, g, bg), steps)
+        per, dom = stage_split(lambda: render(cam, g, bg), steps)
         _C.timing_enable([dom])  # only the dominant stage inside the timed region
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            train_step.render(cam, g, bg)
+            render(cam, g, bg)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         live = _C.timing_read()[dom]
@@ -602,7 +657,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int) -> dic
         "metric": render_metric(cfg_name), "value": round(fps, 3), "unit": "frames/s", "ms_per_frame": round(1e3 * dt / steps, 4),
         "mpix_per_s": round(fps * W * H / 1e6, 2), "steps": steps, "warmup": warmup,
         "config": {"workload": f"{cfg_name}: {WORKLOADS[cfg_name]}", "gaussians": P, "width": W, "height": H,
-                   "sh_degree": deg, "footprint": _C.get_footprint(), "num_rendered": I},
+                   "sh_degree": deg, "footprint": _C.get_footprint(), "num_rendered": I, "glue": GLUE_NOTE[glue]},
         "stages_ms": {k: round(v[0], 4) for k, v in per.items()},
         "stages_source": STAGES_SOURCE["split"],
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -630,7 +685,7 @@ def render_main(args, dev, world: int, rank: int) -> None:
 
     if world > 1:
         dist.barrier()
-    r = render_rates(args.config, dev, args.steps, args.warmup, view=rank % 8)
+    r = render_rates(args.config, dev, args.steps, args.warmup, view=rank % 8, glue=args.glue)
     elapsed = args.steps / r["value"]
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)

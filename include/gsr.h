@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 7
+#define GSR_ABI_VERSION 8
 
 enum gsr_status {
     GSR_OK = 0,
@@ -78,8 +78,27 @@ enum gsr_footprint { GSR_FOOTPRINT_RECT = 0, GSR_FOOTPRINT_TIGHT = 1 };
  * Only a speed hint: every backward is correct with or without it. */
 enum gsr_flags { GSR_FLAG_PREPARE_BACKWARD = 1 };
 
+/* gsr_inputs.activations (not upstream; 0 = upstream's inputs, used as given).
+ * The reference hands the rasterizer activations of GaussianModel's stored
+ * parameters (scene/gaussian_model.py:107-126, gaussian_renderer/__init__.py:
+ * 81-96): opacities = sigmoid(_opacity), scales = exp(_scaling), rotations =
+ * F.normalize(_rotation).  With a bit set the input IS the stored parameter and
+ * the library applies that activation itself, with torch's GPU operations in
+ * torch's order, so the values equal torch's bit for bit (sigmoid: 1 / (1 +
+ * exp(-x)); exp; normalize: x / max(sqrt((x0^2 + x1^2) + (x2^2 + x3^2)), 1e-12),
+ * tools/act_probe.py measured that order), and every backward output for that
+ * input — the plain one (dopacity / dscales / drot) or the leaf one — is the
+ * gradient of the stored parameter (through the activation's backward, as
+ * gsr_leaf_grads describes; rotation_norm is not needed). */
+enum gsr_activations {
+    GSR_ACT_OPACITY = 1,  /* opacities are logits (_opacity) */
+    GSR_ACT_SCALE = 2,    /* scales are logarithms (_scaling) */
+    GSR_ACT_ROTATION = 4  /* rotations are unnormalised quaternions (_rotation) */
+};
+
 /* Inputs shared by forward and backward.  Mirrors the argument list of
- * _C.rasterize_gaussians (rasterize_points.cu RasterizeGaussiansCUDA). */
+ * _C.rasterize_gaussians (rasterize_points.cu RasterizeGaussiansCUDA); the
+ * fields after campos are not upstream (zero = upstream's behaviour). */
 typedef struct gsr_inputs {
     int32_t P;                  /* number of Gaussians (means3D.size(0)) */
     int32_t D;                  /* active SH degree (sh_degree) */
@@ -102,6 +121,12 @@ typedef struct gsr_inputs {
     const float *projmatrix;    /* [4,4] full_proj_transform (scene/cameras.py:114-118) */
     const float *sh;            /* [P,M,3] or NULL */
     const float *campos;        /* [3]   camera_center (scene/cameras.py:121) */
+    /* GaussianModel's SH storage without the cat (scene/gaussian_model.py:
+     * get_features): with sh_rest non-NULL, sh is _features_dc [P,1,3] and sh_rest
+     * _features_rest [P,M-1,3] (both 4-byte aligned rows); M counts both. */
+    const float *sh_rest;
+    int32_t activations;        /* gsr_activations bits */
+    int32_t reserved;           /* 0 */
 } gsr_inputs;
 
 /* Scratch sizes in bytes (all buffers 256-byte aligned internally).
@@ -178,7 +203,8 @@ int gsr_backward_planar(const gsr_inputs *in, const int32_t *radii, const void *
  *   dopacity [P,1]: in->opacities (= sigmoid(_opacity)) required;
  *   drotation [P,4]: in->rotations (= F.normalize(_rotation), the quotient
  *                    torch computed) and rotation_norm [P] (the row norms
- *                    torch computed, LinalgVectorNormBackward0's result) required.
+ *                    torch computed, LinalgVectorNormBackward0's result) required,
+ *                    or in->rotations = _rotation itself with GSR_ACT_ROTATION.
  * (The backward reads in->opacities whenever it is given; without it the
  * opacity comes from the forward's geom buffer.) */
 typedef struct gsr_leaf_grads {

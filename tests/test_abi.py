@@ -35,11 +35,12 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 7
-    # 12 x 4-byte scalars then 11 pointers (include/gsr.h struct gsr_inputs)
-    assert ctypes.sizeof(_C.GsrInputs) == 48 + 11 * 8
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 8
+    # 12 x 4-byte scalars, 11 pointers, then sh_rest and two int32 (include/gsr.h struct gsr_inputs)
+    assert ctypes.sizeof(_C.GsrInputs) == 48 + 12 * 8 + 8
     assert _C.GsrInputs.footprint.offset == 40
     assert _C.GsrInputs.bg.offset == 48
+    assert _C.GsrInputs.sh_rest.offset == 136 and _C.GsrInputs.activations.offset == 144
     # 6 pointers, then rotation_eps and three int32 (struct gsr_leaf_grads)
     assert ctypes.sizeof(_C.GsrLeafGrads) == 6 * 8 + 16
     assert _C.GsrLeafGrads.rotation_eps.offset == 48 and _C.GsrLeafGrads.dsh_planar.offset == 56
@@ -83,6 +84,9 @@ def _inputs(**kw):
     (dict(P=-1), "num_points, 3"),
     (dict(W=0), "image size"),
     (dict(footprint=2), "footprint must be"),
+    (dict(activations=8), "unknown activations"),
+    (dict(sh_rest=1), "sh_rest needs sh"),
+    (dict(sh_rest=1, sh=None, colors_precomp=1, M=16), "sh_rest needs sh"),
 ])
 def test_argument_validation_mirrors_upstream_errors(lib, kw, msg):
     s = _inputs(**kw)

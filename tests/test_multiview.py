@@ -688,14 +688,15 @@ def _rccl_worker(rank, world, port, out):
     cam = synthetic.make_camera(200, 150, view=2).to(dev)
     target = synthetic.make_target(200, 150).to(dev)
     res = {}
-    for mode in ("plain", "allreduce", "sh_colour"):
+    for mode in ("plain", "allreduce", "sh_colour", "plain_fused", "allreduce_fused", "sh_colour_fused"):
+        glue = "fused" if mode.endswith("_fused") else "reference"
         g = synthetic.make_gaussians(30_000, 3, seed=4).to(dev, requires_grad=True)
         params = g.params()
         ar = None
-        if mode != "plain":
-            ar = GradAllReduce(params, sh=(params[0], params[1], params[2]) if mode == "sh_colour" else None,
+        if not mode.startswith("plain"):
+            ar = GradAllReduce(params, sh=(params[0], params[1], params[2]) if mode.startswith("sh_colour") else None,
                                comm_force=True)
-        train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
+        train_step.train_step(cam, g, target, torch.zeros(3, device=dev), glue=glue)
         import diff_gaussian_rasterization as dgr
         plan = dgr.last_leaf_plan
         launched = ar is not None and ar.launched_in_backward
@@ -734,6 +735,18 @@ def test_rccl_collectives_one_rank(dev):
     for mode in ("allreduce", "sh_colour"):
         grads, stats_same, _, launched = res[mode]
         assert stats_same and launched, mode
+        for i, (a, b) in enumerate(zip(grads, plain)):
+            rel = (a - b).norm() / b.norm().clamp_min(1e-30)
+            assert rel < 1e-5, (mode, i, float(rel))
+    # the model path (rasterize_model: stored parameters in, their gradients out)
+    # under the same exchanges: every leaf the library writes lands in the bucket
+    every = ("means3D", "opacities", "rotations", "scales", "sh")
+    assert res["plain_fused"][2] == every
+    assert res["sh_colour_fused"][2] == ("means3D", "opacities", "rotations", "scales")
+    assert res["allreduce_fused"][2] == every
+    for mode in ("plain_fused", "allreduce_fused", "sh_colour_fused"):
+        grads, stats_same, _, launched = res[mode]
+        assert stats_same and (launched or mode == "plain_fused"), mode
         for i, (a, b) in enumerate(zip(grads, plain)):
             rel = (a - b).norm() / b.norm().clamp_min(1e-30)
             assert rel < 1e-5, (mode, i, float(rel))

@@ -21,7 +21,7 @@ from helpers import case, rel_l2
 POISONS = (0xFF, 0x5A)
 
 
-def _autograd_run(cam, g, dev, poison, footprint, retain=False, sink=False):
+def _autograd_run(cam, g, dev, poison, footprint, retain=False, sink=False, model=False):
     import train_step
     from multiview import GradAllReduce
 
@@ -33,7 +33,8 @@ def _autograd_run(cam, g, dev, poison, footprint, retain=False, sink=False):
         if sink:  # the view-parallel SH sink, forced on in a process without a group
             params = gd.params()
             ar = GradAllReduce(params, sh=(params[0], params[1], params[2]), sh_force=True)
-        out = train_step.render(cam.to(dev), gd, torch.zeros(3, device=dev))
+        render = train_step.render_fused if model else train_step.render  # model: rasterize_model
+        out = render(cam.to(dev), gd, torch.zeros(3, device=dev))
         dL = torch.from_numpy(np.random.default_rng(7).standard_normal(out["render"].shape).astype(np.float32))
         loss = (out["render"] * dL.to(dev)).sum() * 1e-3
         loss.backward(retain_graph=retain)
@@ -61,11 +62,11 @@ CASES = {
 @pytest.mark.gpu
 @pytest.mark.parametrize("footprint", ["rect", "tight"])
 @pytest.mark.parametrize("name", sorted(CASES))
-@pytest.mark.parametrize("mode", ["plain", "retain_graph", "sh_sink"])
+@pytest.mark.parametrize("mode", ["plain", "retain_graph", "sh_sink", "model"])
 def test_poisoned_scratch_autograd(dev, name, footprint, mode):
     P, W, H, deg = CASES[name]
     cam, g = case(P, W, H, deg, seed=3, view=2)
-    kw = dict(retain=mode == "retain_graph", sink=mode == "sh_sink" and deg > 0)
+    kw = dict(retain=mode == "retain_graph", sink=mode == "sh_sink" and deg > 0, model=mode == "model")
     img0, radii0, g0 = _autograd_run(cam, g, dev, None, footprint, **kw)
     _, _, g1 = _autograd_run(cam, g, dev, None, footprint, **kw)  # the atomics-order noise floor
     for poison in POISONS:
