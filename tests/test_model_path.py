@@ -62,6 +62,8 @@ def test_model_path_equals_reference_glue(dev, cfg):
     assert got["plan"] == ("means3D", "opacities", "rotations", "scales", "sh")
     for name, a, b, b2 in zip(NAMES, got["grads"], ref["grads"], ref2["grads"]):
         assert a.shape == b.shape and a.dtype == b.dtype, name
+        if b.numel() == 0:  # degree 0: _features_rest has no coefficients
+            continue
         noise = _rel(b2, b) if float(b.abs().max()) > 0 else 0.0
         assert _rel(a, b) <= max(4e-6, 4 * noise), (name, _rel(a, b), noise)
     assert _rel(got["means2D"], ref["means2D"]) <= 4e-6
