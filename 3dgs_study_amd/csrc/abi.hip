@@ -303,9 +303,9 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
                           "tile sort", dbg, s))
             return rc;
     }  // else every range stays (0, 0) as preprocess left it
-    // GSR_FLAG_PREPARE_BACKWARD: the backward's accumulator is zeroed on the second
-    // stream beside the blend (which is bound by instruction issue, not bytes) and
-    // the quadrants are filed after it, so the backward starts with render_bwd
+    // GSR_FLAG_PREPARE_BACKWARD: the backward's accumulator is zeroed beside the blend
+    // (by render_fwd itself; with GSR_SIDE_STREAM=1 by a memset on the second stream)
+    // and the quadrants are filed after it, so the backward starts with render_bwd
     const bool prep = (in->flags & GSR_FLAG_PREPARE_BACKWARD) != 0;
     SideStream *side = nullptr;
     if (prep && !dbg)
@@ -318,10 +318,10 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
         if (int rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "fork")) return rc;
         if (int rc = check_hip(hipMemsetAsync(acc, 0, acc_bytes, side->s), "accumulator")) return rc;
         if (int rc = check_hip(hipEventRecord(side->join, side->s), "join")) return rc;
-    } else if (prep) {
-        if (int rc = step(hipMemsetAsync(acc, 0, acc_bytes, s), "accumulator", dbg, s)) return rc;
     }
-    if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, s); }), "render", dbg, s))
+    // in line (the default): render_fwd zeroes the accumulator itself, beside its blend
+    float *zero = prep && !side ? (float *)acc : nullptr;
+    if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, zero, acc_bytes, s); }), "render", dbg, s))
         return rc;
     if (!prep) return GSR_OK;
     if (side)
@@ -496,10 +496,18 @@ size_t gsr_l1_ssim_scratch_bytes(int32_t C, int32_t H, int32_t W) {
 int gsr_l1_ssim(const float *img, const float *gt, int32_t C, int32_t H, int32_t W, float lambda_dssim,
                 float *grad_img, void *scratch, float *loss_out, void *stream) {
     if (C <= 0 || H <= 0 || W <= 0) return fail(GSR_ERR_ARGS, "l1_ssim: empty image (%d x %d x %d)", C, H, W);
-    if (!img || !gt || !grad_img || !scratch || !loss_out) return fail(GSR_ERR_ARGS, "l1_ssim: NULL buffer");
+    if (!img || !gt || (!grad_img && lambda_dssim != 0.0f) || !scratch || !loss_out)
+        return fail(GSR_ERR_ARGS, "l1_ssim: NULL buffer");
     return check_hip(launch_l1_ssim(img, gt, C, H, W, lambda_dssim, grad_img, (float *)scratch, loss_out,
                                     (hipStream_t)stream),
                      "l1_ssim");
+}
+
+int gsr_l1_grad(const float *img, const float *gt, int64_t n, const float *dloss, float *grad_img, void *stream) {
+    if (n < 0) return fail(GSR_ERR_ARGS, "l1_grad: negative size");
+    if (n == 0) return GSR_OK;
+    if (!img || !gt || !dloss || !grad_img) return fail(GSR_ERR_ARGS, "l1_grad: NULL buffer");
+    return check_hip(launch_l1_grad(img, gt, (size_t)n, dloss, grad_img, (hipStream_t)stream), "l1_grad");
 }
 
 int gsr_adam_step(const gsr_adam_segment *segs, int32_t nseg, int32_t step, double beta1, double beta2, double eps,

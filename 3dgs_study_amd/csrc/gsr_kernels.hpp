@@ -24,7 +24,7 @@ hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const v
 
 // render_fwd.hip
 hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,
-                             float *out_color, hipStream_t s);
+                             float *out_color, float *acc_zero, size_t acc_bytes, hipStream_t s);
 
 // render_bwd.hip
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
@@ -53,6 +53,7 @@ hipError_t launch_sh_grad_from_colors(int P, int M, int nviews, int64_t view_str
 size_t l1_ssim_scratch_floats(int C, int H, int W);
 hipError_t launch_l1_ssim(const float *x, const float *y, int C, int H, int W, float lambda, float *grad,
                           float *partials, float *out, hipStream_t s);
+hipError_t launch_l1_grad(const float *x, const float *y, size_t n, const float *dloss, float *grad, hipStream_t s);
 hipError_t launch_adam(const gsr_adam_segment *segs, int nseg, int step, double beta1, double beta2, double eps,
                        hipStream_t s);
 hipError_t launch_densify_stats(int P, const int32_t *radii, const float *vgrad, int vstride, float *max_radii,

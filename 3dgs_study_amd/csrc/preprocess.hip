@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     }
     const float opac_in = in.opacities[li];
     float4 rowv[DIRECT ? 12 : 1];
-    if constexpr (DIRECT && SPLIT) {  // _features_dc + _features_rest rows, 4-B aligned
+    if constexpr (DIRECT && SPLIT) {  // _features_dc + _features_rest rows
         float r[48];
         load_sh_row_split(in.sh, in.sh_rest, (size_t)li, r);
 #pragma unroll
@@ -371,8 +371,8 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
     // row indexing); any other width takes the run-time path
     const int width = in.sh && !in.colors_precomp ? 3 * in.M : 0;
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(nb), dim3(PRE_THREADS), lds, s, a); };
-    if (width == 3)
-        split ? go(preprocess_fwd_kernel<3, true>) : go(preprocess_fwd_kernel<3, false>);
+    if (width == 3)  // (M = 1 has no rest coefficients: never split)
+        go(preprocess_fwd_kernel<3, false>);
     else if (width == 48 && direct)
         split ? go(preprocess_fwd_kernel<48, true>) : go(preprocess_fwd_kernel<48, false>);
     else

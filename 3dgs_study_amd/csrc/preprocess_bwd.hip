@@ -580,8 +580,8 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     const dim3 grid((in.P + PB_THREADS - 1) / PB_THREADS);
     // see launch_preprocess; the direct-row kernel needs staged rows (cat rows 16-B aligned)
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(PB_THREADS), lds, s, a); };
-    if (3 * in.M == 3)
-        split ? go(preprocess_bwd_kernel<3, true>) : go(preprocess_bwd_kernel<3, false>);
+    if (3 * in.M == 3)  // (M = 1 has no rest coefficients: never split)
+        go(preprocess_bwd_kernel<3, false>);
     else if (3 * in.M == 48 && direct)
         split ? go(preprocess_bwd_kernel<48, true>) : go(preprocess_bwd_kernel<48, false>);
     else

@@ -29,6 +29,11 @@ struct RenderFwdArgs {
     float *final_T;
     uint32_t *n_contrib;
     uint8_t *qbucket;  // [4 * tiles] (img)
+    // GSR_FLAG_PREPARE_BACKWARD: the backward's accumulator, zeroed here — this
+    // kernel is bound by instruction issue, not bytes, so its 64 B per Gaussian of
+    // stores ride along (a separate memset launch took 10 us at config C)
+    float4 *zero4;
+    size_t zero_n4;
 };
 
 #ifndef GSR_FWD_GROUP
@@ -43,9 +48,19 @@ static_assert(FWD_GROUP >= 1 && FWD_GROUP <= 3, "QuadChunk holds 64 survivors + 
 // odd count's second Gaussian blend nothing without a mask (render_fwd 145 ->
 // 142 us at C, 374-379 -> 370 us at E).
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(7))) render_fwd_kernel(RenderFwdArgs a) {
+    auto zero_slice = [&]() {  // every workgroup its slice of the backward's accumulator
+        if (a.zero4) {
+            const size_t per = (a.zero_n4 + gridDim.x - 1) / gridDim.x, z0 = (size_t)blockIdx.x * per;
+            const size_t z1 = z0 + per < a.zero_n4 ? z0 + per : a.zero_n4;
+            for (size_t i = z0 + threadIdx.x; i < z1; i += BLEND_THREADS) a.zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
-    if (tile < 0) return;
+    if (tile < 0) {
+        zero_slice();
+        return;
+    }
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
@@ -191,10 +206,13 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         a.out_color[HW + pix] = C1 + T * a.bg[1];
         a.out_color[2 * HW + pix] = C2 + T * a.bg[2];
     }
+    // last: the zeroing stores go out behind the outputs, after the last wait (at the
+    // kernel's start they sat in the chunk loop's vmcnt waits: 128-129 vs 126-127 us)
+    zero_slice();
 }
 
 hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,
-                             float *out_color, hipStream_t s) {
+                             float *out_color, float *acc_zero, size_t acc_bytes, hipStream_t s) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -211,6 +229,8 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
     a.final_T = at<float>(img, Im.off[GSR_IMG_FINAL_T]);
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
     a.qbucket = at<uint8_t>(img, Im.qbucket);
+    a.zero4 = reinterpret_cast<float4 *>(acc_zero);
+    a.zero_n4 = acc_zero ? acc_bytes / sizeof(float4) : 0;
     hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }

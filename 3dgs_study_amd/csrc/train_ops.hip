@@ -260,31 +260,24 @@ __global__ void __launch_bounds__(1024) l1_ssim_finish_kernel(const float *parti
 }
 
 // lambda == 0 (the headline unit's loss, train.py:102 with lambda_dssim = 0): only
-// mean |x - y| and its gradient sign(x - y) / N — torch's MeanBackward then
-// AbsBackward, bit for bit — in one streaming pass (16 B of x, y and the gradient
-// per lane per step; the window sums of the SSIM kernel would cost 10x the time for
-// a zero term).  Per workgroup one partial sum for l1_ssim_finish_kernel.
+// mean |x - y| (l1_kernel, one streaming read of x and y; the window sums of the
+// SSIM kernel would cost 10x the time for a zero term), and in the backward its
+// gradient (l1_grad_kernel): torch's MeanBackward then AbsBackward, (dloss / N) *
+// sign(x - y), bit for bit, with the incoming dloss read on the device — no
+// gradient map is written in the forward and scaled again in the backward.
+// Per workgroup one partial sum for l1_ssim_finish_kernel.
 constexpr int L1_THREADS = 256, L1_BLOCKS = 1024;
-__global__ void __launch_bounds__(L1_THREADS) l1_kernel(const float *x, const float *y, float *g, size_t n, float invN,
-                                                        float *partials) {
+__global__ void __launch_bounds__(L1_THREADS) l1_kernel(const float *x, const float *y, size_t n, float *partials) {
     __shared__ float wsum[L1_THREADS / 64];
     const size_t n4 = n >> 2, stride = (size_t)gridDim.x * L1_THREADS;
     const float4 *x4 = reinterpret_cast<const float4 *>(x), *y4 = reinterpret_cast<const float4 *>(y);
-    float4 *g4 = reinterpret_cast<float4 *>(g);
-    auto sg = [&](float d) { return d > 0.f ? invN : (d < 0.f ? -invN : 0.f); };
     float acc = 0.f;
     for (size_t i = (size_t)blockIdx.x * L1_THREADS + threadIdx.x; i < n4; i += stride) {
         const float4 a = x4[i], b = y4[i];
-        const float d0 = a.x - b.x, d1 = a.y - b.y, d2 = a.z - b.z, d3 = a.w - b.w;
-        acc += (fabsf(d0) + fabsf(d1)) + (fabsf(d2) + fabsf(d3));
-        g4[i] = make_float4(sg(d0), sg(d1), sg(d2), sg(d3));
+        acc += (fabsf(a.x - b.x) + fabsf(a.y - b.y)) + (fabsf(a.z - b.z) + fabsf(a.w - b.w));
     }
     if (blockIdx.x == 0)  // the tail of a length that is not a multiple of 4
-        for (size_t i = (n4 << 2) + threadIdx.x; i < n; i += L1_THREADS) {
-            const float d = x[i] - y[i];
-            acc += fabsf(d);
-            g[i] = sg(d);
-        }
+        for (size_t i = (n4 << 2) + threadIdx.x; i < n; i += L1_THREADS) acc += fabsf(x[i] - y[i]);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
@@ -296,6 +289,32 @@ __global__ void __launch_bounds__(L1_THREADS) l1_kernel(const float *x, const fl
         partials[2 * blockIdx.x] = tot;
         partials[2 * blockIdx.x + 1] = 0.f;
     }
+}
+
+__device__ __forceinline__ float sign_f(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
+__global__ void __launch_bounds__(L1_THREADS) l1_grad_kernel(const float *x, const float *y, size_t n, float fN,
+                                                             const float *dloss, float *g) {
+    const float q = dloss[0] / fN;  // MeanBackward: grad / numel
+    const size_t n4 = n >> 2, stride = (size_t)gridDim.x * L1_THREADS;
+    const float4 *x4 = reinterpret_cast<const float4 *>(x), *y4 = reinterpret_cast<const float4 *>(y);
+    float4 *g4 = reinterpret_cast<float4 *>(g);
+    for (size_t i = (size_t)blockIdx.x * L1_THREADS + threadIdx.x; i < n4; i += stride) {
+        const float4 a = x4[i], b = y4[i];  // AbsBackward: grad * sgn(self)
+        g4[i] = make_float4(q * sign_f(a.x - b.x), q * sign_f(a.y - b.y), q * sign_f(a.z - b.z), q * sign_f(a.w - b.w));
+    }
+    if (blockIdx.x == 0)
+        for (size_t i = (n4 << 2) + threadIdx.x; i < n; i += L1_THREADS) g[i] = q * sign_f(x[i] - y[i]);
+}
+
+static int l1_blocks(size_t n) {
+    const size_t want = (n / 4 + L1_THREADS - 1) / L1_THREADS;
+    return (int)(want < (size_t)L1_BLOCKS ? (want > 0 ? want : 1) : L1_BLOCKS);
+}
+
+hipError_t launch_l1_grad(const float *x, const float *y, size_t n, const float *dloss, float *grad, hipStream_t s) {
+    hipLaunchKernelGGL(l1_grad_kernel, dim3(l1_blocks(n)), dim3(L1_THREADS), 0, s, x, y, n, (float)(double)n, dloss,
+                       grad);
+    return hipGetLastError();
 }
 
 size_t l1_ssim_scratch_floats(int C, int H, int W) {
@@ -317,11 +336,10 @@ hipError_t launch_l1_ssim(const float *x, const float *y, int C, int H, int W, f
     a.tiles_y = (H + SS_TY - 1) / SS_TY;
     a.lambda = lambda;
     a.invN = 1.0f / (float)((double)C * H * W);  // torch's MeanBackward: grad / numel in float
-    if (lambda == 0.0f) {
+    if (lambda == 0.0f && grad == nullptr) {  // the loss alone (its gradient: launch_l1_grad)
         const size_t n = (size_t)C * H * W;
-        const size_t want = (n / 4 + L1_THREADS - 1) / L1_THREADS;
-        const int nb = (int)(want < (size_t)L1_BLOCKS ? (want > 0 ? want : 1) : L1_BLOCKS);
-        hipLaunchKernelGGL(l1_kernel, dim3(nb), dim3(L1_THREADS), 0, s, x, y, grad, n, a.invN, partials);
+        const int nb = l1_blocks(n);
+        hipLaunchKernelGGL(l1_kernel, dim3(nb), dim3(L1_THREADS), 0, s, x, y, n, partials);
         hipLaunchKernelGGL(l1_ssim_finish_kernel, dim3(1), dim3(1024), 0, s, (const float *)partials, nb, lambda,
                            a.invN, out);
         return hipGetLastError();

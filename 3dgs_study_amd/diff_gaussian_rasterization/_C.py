@@ -63,7 +63,7 @@ EXPORTED = (
     "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2",
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
-    "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end",
+    "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -223,6 +223,8 @@ def load_library():
     lib.gsr_l1_ssim_scratch_bytes.restype = sz
     lib.gsr_l1_ssim.argtypes = [vp, vp, i32, i32, i32, ctypes.c_float, vp, vp, vp, vp]
     lib.gsr_l1_ssim.restype = ctypes.c_int
+    lib.gsr_l1_grad.argtypes = [vp, vp, i64, vp, vp, vp]
+    lib.gsr_l1_grad.restype = ctypes.c_int
     lib.gsr_adam_step.argtypes = [ctypes.POINTER(GsrAdamSegment), i32, i32, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, vp]
     lib.gsr_adam_step.restype = ctypes.c_int

@@ -287,13 +287,14 @@ def _input_sources(rs, means3D, colors_precomp, opacities, scales, rotations, co
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings):
+                raster_settings, grad_on=True):
         rs = raster_settings
         args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
                 rs.sh_degree, rs.campos, rs.prefiltered, rs.debug)
         # a backward may follow: the forward zeroes its accumulator beside the blend
-        prep = any(ctx.needs_input_grad[:8])
+        # (needs_input_grad is set under no_grad too: the caller's grad mode decides)
+        prep = grad_on and any(ctx.needs_input_grad[:8])
         num_rendered, color, radii, geom, binning, img, vin = _call_native(
             lambda *a: _C._rasterize(*a, prepare_backward=prep), args, rs.debug, "snapshot_fw.dump", "forward")
         ctx.raster_settings = rs
@@ -314,12 +315,17 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom, binning,
                               img, opacities, *copies.values())
         ctx.mark_non_differentiable(radii)
+        # radii never carry a gradient: no zero int32 [P] tensor materialised per backward
+        ctx.set_materialize_grads(False)
         return color, radii
 
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii):
         rs = ctx.raster_settings
         saved = ctx.saved_tensors
+        if grad_out_color is None:  # the image was not used (set_materialize_grads(False))
+            grad_out_color = torch.zeros((3, rs.image_height, rs.image_width), dtype=torch.float32,
+                                         device=saved[1].device)
         colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom, binning, img, opacities = saved[:11]
         inputs = None
         if ctx.inputs is not None:
@@ -358,7 +364,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         if plan:
             for p, g in fresh:
                 p.grad = g
-        return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None)
+        return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None, None)
 
 
 class _RasterizeModel(torch.autograd.Function):
@@ -367,14 +373,15 @@ class _RasterizeModel(torch.autograd.Function):
     the two leaves, and its backward writes the stored parameters' gradients."""
 
     @staticmethod
-    def forward(ctx, means3D, means2D, features_dc, features_rest, opacity, scaling, rotation, raster_settings):
+    def forward(ctx, means3D, means2D, features_dc, features_rest, opacity, scaling, rotation, raster_settings,
+                grad_on=True):
         rs = raster_settings
         empty = _empty_like_device(means3D)
         rest = features_rest if features_rest.numel() else None
         args = (rs.bg, means3D, empty, opacity, scaling, rotation, rs.scale_modifier, empty, rs.viewmatrix,
                 rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, features_dc, rs.sh_degree,
                 rs.campos, rs.prefiltered, rs.debug)
-        prep = any(ctx.needs_input_grad[:7])
+        prep = grad_on and any(ctx.needs_input_grad[:7])
         num_rendered, color, radii, geom, binning, img, (s, keep, device, M) = _call_native(
             lambda *a: _C._rasterize(*a, prepare_backward=prep, sh_rest=rest, activations=_C.ACT_ALL), args, rs.debug,
             "snapshot_fw.dump", "forward")
@@ -386,12 +393,17 @@ class _RasterizeModel(torch.autograd.Function):
         ctx.save_for_backward(means3D, features_dc, features_rest, opacity, scaling, rotation, radii, geom, binning,
                               img, *copies.values())
         ctx.mark_non_differentiable(radii)
+        # radii never carry a gradient: no zero int32 [P] tensor materialised per backward
+        ctx.set_materialize_grads(False)
         return color, radii
 
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii):
         rs = ctx.raster_settings
         saved = ctx.saved_tensors
+        if grad_out_color is None:  # the image was not used (set_materialize_grads(False))
+            grad_out_color = torch.zeros((3, rs.image_height, rs.image_width), dtype=torch.float32,
+                                         device=saved[1].device)
         means3D, f_dc, f_rest, opacity, scaling, rotation, radii, geom, binning, img = saved[:10]
         s, device, M, present, copy_names = ctx.inputs
         rest = f_rest if f_rest.numel() else None
@@ -452,7 +464,7 @@ class _RasterizeModel(torch.autograd.Function):
             torch.zeros_like(f_rest) if "dsh_rest" in kw else None)
         return (bucketed("means3D", kw["dmeans3D"]), d_means2D, kw.get("dsh_dc"), d_rest,
                 bucketed("opacities", kw["dopacity"]), bucketed("scales", kw["dscaling"]),
-                bucketed("rotations", kw["drotation"]), None)
+                bucketed("rotations", kw["drotation"]), None, None)
 
 
 def rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation, raster_settings):
@@ -471,13 +483,13 @@ def rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scali
     the activation kernels, their backwards or the cat's slice copies.
     ``means2D`` is the screen-space gradient carrier, as upstream."""
     return _RasterizeModel.apply(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation,
-                                 raster_settings)
+                                 raster_settings, torch.is_grad_enabled())
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                         raster_settings):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                                     cov3Ds_precomp, raster_settings)
+                                     cov3Ds_precomp, raster_settings, torch.is_grad_enabled())
 
 
 class GaussianRasterizationSettings(NamedTuple):

@@ -43,17 +43,30 @@ class _L1SSIM(torch.autograd.Function):
             raise RuntimeError(f"l1_ssim_loss: image {tuple(image.shape)} and gt {tuple(gt.shape)} must be equal [C,H,W]")
         x, y = image.contiguous(), gt.contiguous()
         C, H, W = x.shape
-        grad = torch.empty_like(x)
+        # L1 alone (lambda 0): the loss here, its gradient in the backward from the
+        # incoming dloss (gsr_l1_grad) — no map written here and scaled again there
+        l1_only = float(lambda_dssim) == 0.0
+        grad = None if l1_only else torch.empty_like(x)
         scratch = torch.empty(lib.gsr_l1_ssim_scratch_bytes(C, H, W), dtype=torch.uint8, device=x.device)
         out = torch.empty(3, dtype=torch.float32, device=x.device)
-        _C._check(lib.gsr_l1_ssim(x.data_ptr(), y.data_ptr(), C, H, W, float(lambda_dssim), grad.data_ptr(),
-                                  scratch.data_ptr(), out.data_ptr(), _C._stream(x.device)), "gsr_l1_ssim")
-        ctx.save_for_backward(grad)
+        _C._check(lib.gsr_l1_ssim(x.data_ptr(), y.data_ptr(), C, H, W, float(lambda_dssim),
+                                  None if l1_only else grad.data_ptr(), scratch.data_ptr(), out.data_ptr(),
+                                  _C._stream(x.device)), "gsr_l1_ssim")
+        ctx.l1_only = l1_only
+        ctx.save_for_backward(*((x, y) if l1_only else (grad,)))
         ctx.parts = out
         return out[0]
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.l1_only:
+            x, y = ctx.saved_tensors
+            lib = _C.load_library()
+            grad = torch.empty_like(x)
+            gd = g.detach().to(torch.float32).contiguous()
+            _C._check(lib.gsr_l1_grad(x.data_ptr(), y.data_ptr(), x.numel(), gd.data_ptr(), grad.data_ptr(),
+                                      _C._stream(x.device)), "gsr_l1_grad")
+            return grad, None, None
         (grad,) = ctx.saved_tensors
         return grad * g, None, None
 

@@ -356,10 +356,16 @@ int gsr_timing_end(int stage, void *stream);
  * gsr_l1_ssim: loss = (1 - lambda) L1(img, gt) + lambda (1 - SSIM(img, gt)) for
  * [C,H,W] float images (utils/loss_utils.py l1_loss + ssim, train.py:103-105),
  * AND its gradient dloss/dimg in the same pass.  loss_out (device, 3 floats):
- * loss, L1 term, mean SSIM.  scratch: gsr_l1_ssim_scratch_bytes. */
+ * loss, L1 term, mean SSIM.  scratch: gsr_l1_ssim_scratch_bytes.  With
+ * lambda_dssim == 0 grad_img may be NULL: the L1 loss alone, whose gradient
+ * gsr_l1_grad computes in the backward. */
 size_t gsr_l1_ssim_scratch_bytes(int32_t C, int32_t H, int32_t W);
 int gsr_l1_ssim(const float *img, const float *gt, int32_t C, int32_t H, int32_t W, float lambda_dssim,
                 float *grad_img, void *scratch, float *loss_out, void *stream);
+/* The L1 loss's backward for n floats: grad_img = (*dloss / n) * sign(img - gt)
+ * (torch's MeanBackward then AbsBackward, bit for bit); dloss is the incoming
+ * gradient of the loss, a device scalar. */
+int gsr_l1_grad(const float *img, const float *gt, int64_t n, const float *dloss, float *grad_img, void *stream);
 
 /* gsr_adam_step: torch.optim.Adam's update (no weight decay, no amsgrad) on up
  * to GSR_ADAM_MAX_SEGS tensors in one launch; step = the 1-based step count

@@ -9,7 +9,7 @@ for r in $(seq 1 $ROUNDS); do
   for v in "$@"; do
     lib=$PWD/3dgs_study_amd/lib/libgsr_$v.so
     [ "$v" = base ] && lib=$PWD/3dgs_study_amd/lib/libgsr.so
-    GSR_LIBRARY=$lib timeout -k 10 200 python bench.py --steps 60 --warmup 10 --no-cpu-baseline --full-steps 0 --exchange-steps 0 --footprint-steps 0 \
+    GSR_LIBRARY=$lib timeout -k 10 200 python bench.py --steps 60 --warmup 10 --no-cpu-baseline --full-steps 0 --exchange-steps 0 --footprint-steps 0 --glue-steps 0 \
         > gpurun_out/var_${v}_$r.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/var_${v}_$r.log; exit 1; }
     python - "$v" gpurun_out/var_${v}_$r.log <<'PY'
 import json, sys
