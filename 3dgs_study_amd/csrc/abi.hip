@@ -250,6 +250,7 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     const bool dbg = in->debug != 0;
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
+    g_pinned[CTRL_DSORT_PASSES] = 0;
     // The depth sort needs only the view depths.  By default it runs in line, before
     // preprocess; with GSR_SIDE_STREAM=1 on the library's second stream beside
     // preprocess (debug mode: always in line, every kernel checked on one stream).
@@ -262,7 +263,10 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
         if (int rc = check_hip(hipStreamWaitEvent(ds, side->fork, 0), "fork")) return rc;
     }
     const int sort_stage = side ? GSR_STAGE_DSORT_CONCURRENT : GSR_STAGE_DEPTH_SORT;
-    if (int rc = step(timed(sort_stage, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, ds); }), "depth sort", dbg, ds))
+    // in line, the host reads the published pass count after its sync and runs a
+    // fourth pass only when the keys need it; on the second stream all four are queued
+    uint32_t *pass_word = side ? nullptr : (uint32_t *)g_pinned;
+    if (int rc = step(timed(sort_stage, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, pass_word, ds); }), "depth sort", dbg, ds))
         return rc;
     if (side)
         if (int rc = check_hip(hipEventRecord(side->join, ds), "join")) return rc;
@@ -274,12 +278,22 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
             return rc;
     // the rects in rank order and the emission offsets (upstream's InclusiveSum of
     // tiles_touched, in depth order), queued before the host waits: the device stays busy
-    if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, s); }),
+    if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, !side, s); }),
                       "rank gather", dbg, s))
         return rc;
     if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;
     if (g_pinned[CTRL_PREFILTER_ERR])
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (!side && g_pinned[CTRL_DSORT_PASSES] != 3u) {
+        // the keys span more than 2^24: the fourth pass, then the rank gather the
+        // queued one skipped (rank_gather_kernel returns at once on a four-pass sort)
+        if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] { return launch_depth_sort_fourth(in->P, in->W, in->H, geom, s); }),
+                          "depth sort (fourth pass)", dbg, s))
+            return rc;
+        if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, false, s); }),
+                          "rank gather", dbg, s))
+            return rc;
+    }
     const int64_t I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
     if (I > 0xFFFFFFFFll) return fail(GSR_ERR_CAPACITY, "num_rendered %lld exceeds 32-bit list indexing", (long long)I);
     *num_rendered = I;

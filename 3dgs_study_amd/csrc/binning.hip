@@ -97,6 +97,7 @@ struct RadixPass {
     const uint32_t *ctrl;  // GeomLayout::dsort_ctrl
     uint2 *minmax;         // first depth pass: the candidate key range per block (its digit scan reduces it)
     uint32_t *ctrl_out;    // ... into these control words
+    uint32_t *host_ctrl;   // ... and the pass count into the caller's pinned words (CTRL_DSORT_PASSES), or NULL
     int role;              // RX_PLAIN, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH
     uint32_t *vout_final;  // RX_DEPTH_THIRD in three-pass mode: the order lands here
     // packed two-pass tile sort (tile_sort_packed): the first pass (RXM_PACK)
@@ -295,8 +296,13 @@ __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPa
             }
             const bool any = kmin <= kmax;
             const uint32_t base = any ? (kmin & ~0xffu) : 0u;
+            const uint32_t passes = any && kmax - base > 0xffffffu ? 4u : 3u;
             a.ctrl_out[DCTRL_KEY_BASE] = base;
-            a.ctrl_out[DCTRL_PASSES] = any && kmax - base > 0xffffffu ? 4u : 3u;
+            a.ctrl_out[DCTRL_PASSES] = passes;
+            if (a.host_ctrl) {  // the host launches the fourth pass only when it is needed
+                __hip_atomic_store(&a.host_ctrl[CTRL_DSORT_PASSES], passes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+            }
         }
         return;
     }
@@ -493,8 +499,11 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t lo, uint32_t hi, uint32
 // so no scan launch sits between this kernel and the emission.
 __global__ void __launch_bounds__(RG_THREADS)
     rank_gather_kernel(const uint32_t *order, const uint4 *rects, int P, uint4 *rects_ranked, uint32_t *local,
-                       uint32_t *super) {
+                       uint32_t *super, const uint32_t *dsort_ctrl) {
     __shared__ uint32_t wsum[RG_RANKS][RG_THREADS / 64];
+    // queued before the host knows the pass count: a four-pass sort is not done yet
+    // (the host launches its fourth pass and this kernel again)
+    if (dsort_ctrl && dsort_ctrl[DCTRL_PASSES] != 3u) return;
     const int r0 = blockIdx.x * RG_THREADS * RG_RANKS + threadIdx.x;
     uint32_t id[RG_RANKS];
 #pragma unroll
@@ -827,7 +836,7 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
 
 template <int ITEMS>
 static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                                   hipStream_t s) {
+                                   uint32_t *host_ctrl, hipStream_t s) {
     const GeomLayout L = geom_layout(P, W, H);
     DepthKeyArgs k;
     k.means3D = means3D;
@@ -838,29 +847,41 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     k.hist = at<uint32_t>(geom, L.dsort_hist);
     k.minmax = at<uint2>(geom, L.dsort_minmax);
     hipLaunchKernelGGL(depth_keys_kernel<ITEMS>, dim3(k.NB), dim3(RX_THREADS), 0, s, k);
-    for (int p = 0; p < 4; p++) {
-        hipError_t e = radix_pass<ITEMS>(depth_pass(P, W, H, geom, p), s, p == 0);
+    // host_ctrl: passes 1-3 only; the host reads the published pass count after its
+    // one sync and launches the fourth (launch_depth_sort_fourth) when the keys need
+    // it — three early-returning launches (~14 us at config C) saved in the common case
+    for (int p = 0; p < (host_ctrl ? 3 : 4); p++) {
+        RadixPass a = depth_pass(P, W, H, geom, p);
+        if (p == 0) a.host_ctrl = host_ctrl;
+        hipError_t e = radix_pass<ITEMS>(a, s, p == 0);
         if (e != hipSuccess) return e;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             hipStream_t s) {
+                             uint32_t *host_ctrl, hipStream_t s) {
     if (P <= 0) return hipSuccess;
-    return dsort_items(P) == DSORT_ITEMS_BIG ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, s)
-                                             : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, s);
+    return dsort_items(P) == DSORT_ITEMS_BIG
+               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s)
+               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s);
+}
+
+hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s) {
+    if (P <= 0) return hipSuccess;
+    return dsort_items(P) == DSORT_ITEMS_BIG ? radix_pass<DSORT_ITEMS_BIG>(depth_pass(P, W, H, geom, 3), s)
+                                             : radix_pass<DSORT_ITEMS>(depth_pass(P, W, H, geom, 3), s);
 }
 
 // After both streams: the rects in rank order and the rank-order instance offsets
 // of the emit blocks.
-hipError_t launch_rank_gather(int P, int W, int H, void *geom, hipStream_t s) {
+hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hipStream_t s) {
     if (P <= 0) return hipSuccess;
     const GeomLayout L = geom_layout(P, W, H);
     hipLaunchKernelGGL(rank_gather_kernel, dim3(rg_blocks(P)), dim3(RG_THREADS), 0, s,
                        at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), at<const uint4>(geom, L.rects), P,
                        at<uint4>(geom, L.rects_ranked), at<uint32_t>(geom, L.emit_sums),
-                       at<uint32_t>(geom, L.emit_super));
+                       at<uint32_t>(geom, L.emit_super), require3 ? at<const uint32_t>(geom, L.dsort_ctrl) : nullptr);
     return hipGetLastError();
 }
 

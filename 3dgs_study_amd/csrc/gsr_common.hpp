@@ -101,10 +101,11 @@ enum CtrlWord {
     CTRL_NUM_RENDERED_LO = 0,
     CTRL_NUM_RENDERED_HI = 1,
     CTRL_PREFILTER_ERR = 2,
+    CTRL_DSORT_PASSES = 3,  // host copy only: the depth sort's pass count (its first digit scan publishes it)
     CTRL_WORDS = 16
 };
 // the depth sort's own control words (GeomLayout::dsort_ctrl, a line of their own:
-// the sort runs on a second stream beside preprocess, binning.hip)
+// with GSR_SIDE_STREAM=1 the sort runs on a second stream beside preprocess, binning.hip)
 enum DsortCtrlWord {
     DCTRL_KEY_BASE = 0,  // smallest depth key (bits) of a candidate Gaussian, low byte cleared
     DCTRL_PASSES = 1,    // 3 when every candidate key lies within 2^24 of the base, else 4

@@ -14,8 +14,9 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 
 // binning.hip
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             hipStream_t s);
-hipError_t launch_rank_gather(int P, int W, int H, void *geom, hipStream_t s);
+                             uint32_t *host_ctrl, hipStream_t s);
+hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s);
+hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hipStream_t s);
 hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
                        hipStream_t s);
 hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, hipStream_t s);
