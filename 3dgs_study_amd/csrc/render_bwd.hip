@@ -24,6 +24,15 @@
 
 namespace gsr {
 
+// Ablation switches for timing builds (results are wrong with any of them on):
+// GSR_XB_NOSWZ: the exchanges read the lane's own value (no ds_swizzle),
+// GSR_XB_NOTRANS: exp and rcp replaced by multiplies.
+#ifdef GSR_XB_NOSWZ
+#define GSR_SWZ(v, pat) (v)
+#else
+#define GSR_SWZ(v, pat) __builtin_amdgcn_ds_swizzle((v), (pat))
+#endif
+
 // Wave order: per XCD, most forward work first (the buckets the forward filed,
 // gsr_blend.hpp), so that the longest replays start at once instead of forming
 // the kernel's tail.
@@ -61,7 +70,7 @@ template <int K>
 __device__ __forceinline__ float swz_stage(float c, float d, int lane) {
     const bool hi = (lane & K) != 0;
     const float keep = hi ? d : c, send = hi ? c : d;
-    return keep + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send), 0x1F | (K << 10)));
+    return keep + __builtin_bit_cast(float, GSR_SWZ(__builtin_bit_cast(int, send), 0x1F | (K << 10)));
 }
 
 // The same step for an odd register out (c paired with a zero): every lane adds
@@ -72,7 +81,7 @@ __device__ __forceinline__ float swz_stage(float c, float d, int lane) {
 // whole exchange sequence).
 template <int K>
 __device__ __forceinline__ float swz_fold(float c) {
-    return c + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, c), 0x1F | (K << 10)));
+    return c + __builtin_bit_cast(float, GSR_SWZ(__builtin_bit_cast(int, c), 0x1F | (K << 10)));
 }
 
 
@@ -160,7 +169,11 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         const int k = __float_as_int(r2.y);  // entry lo + k = upstream `contributor`
         const bool valid = k < lim && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
         const float av = valid ? alpha : 0.0f;
+#ifdef GSR_XB_NOTRANS
+        const float inv_1ma = 1.f + av;
+#else
         const float inv_1ma = __builtin_amdgcn_rcpf(1.f - av);
+#endif
         T = T * inv_1ma;
         const float cd = fmaf(cg, dpx1, cr * dpx0) + r2.x * dpx2;  // sum_c colour_c dL/dpix_c
         const float dot = cd - D;                                      // sum_c (colour_c - accum_rec_c) dL/dpix_c
@@ -189,17 +202,21 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // terms fused into FMAs.  Then four
     // more ds_swizzle stages (xor 8, 4, 2, 1: LDS-pipe exchanges, 3 plain VALU per
     // output register) and one final v_permlane32 self-swap adding the two halves.
-    auto reduce_emit = [&](const Part &pa, const Part &pb, uint32_t gida, uint32_t gidb, bool two) {
-#ifdef GSR_BWD_SETPRIO  // experiment: the dependent exchange chain first in the SIMD's arbitration
-        __builtin_amdgcn_s_setprio(GSR_BWD_SETPRIO);
-#endif
+    // the pair's two atomic wave-instructions: row base in SGPRs + per-lane slot;
+    // lane-dependent addresses keep the compiler's atomic optimizer (a wave-scan
+    // loop) out
+    auto emit = [&](float v, uint32_t gida, uint32_t gidb, bool two) {
+        if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, v);
+        if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
+    };
+    auto reduce_sum = [&](const Part &pa, const Part &pb) -> float {
         const float k5 = h16 ? pb.g5 : pa.g5, s5 = h16 ? pa.g5 : pb.g5;
         const float kx = h16 ? pb.dx : pa.dx, sx = h16 ? pa.dx : pb.dx;
         const float ky = h16 ? pb.dy : pa.dy, sy = h16 ? pa.dy : pb.dy;
         const float kt = h16 ? pb.t : pa.t, st_ = h16 ? pa.t : pb.t;
         auto x16 = [&](float send) {
             return __builtin_bit_cast(float,
-                                      __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send), 0x1F | (16 << 10)));
+                                      GSR_SWZ(__builtin_bit_cast(int, send), 0x1F | (16 << 10)));
         };
         // the colour terms cross as the sender's own products t dL/dpix_c (no
         // registers held for the partner pixel's dL/dpix)
@@ -227,14 +244,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         const float w0 = swz_stage<2>(u0, u1, lane);
         const float w1 = swz_fold<2>(u2);
         const float x0 = swz_stage<1>(w0, w1, lane);
-        const float v = swap32_sum(x0, x0);  // both halves: the full sum
-        // row base in SGPRs + per-lane slot; lane-dependent addresses keep the
-        // compiler's atomic optimizer (a wave-scan loop) out
-        if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, v);
-        if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
-#ifdef GSR_BWD_SETPRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
+        return swap32_sum(x0, x0);  // both halves: the full sum
     };
 
     // Replay one 64-entry chunk [lo, lo + 64) from the back (lane l <-> entry lo + l),
@@ -252,38 +262,57 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         uint32_t boff = (uint32_t)(ns - 1) * (uint32_t)sizeof(st.rec[0]);
         asm volatile("" : "+v"(boff));
         const volatile char *sbase = reinterpret_cast<const volatile char *>(&st.rec[0][0]);
-        for (int k = ns - 1; k >= 0; k -= 2) {
-            const bool two = k >= 1;  // wave-uniform
+        // one pair's records, power, G and alpha (the exact exp near 1/255 included)
+        struct Cur {
+            float pa, pb, Ga, Gb, ala, alb, dxa, dya, dxb, dyb;
+            float4 a1, a2, b1, b2;
+        };
+        auto front = [&](Cur &c) {
             // whole 16-B reads (volatile: the load vectorizer would otherwise split
             // the records into 8-B pieces around the unused fields)
             lds_f32x4 *rb = (lds_f32x4 *)(sbase + boff);
-            const float4 b0 = ld4(rb + 0), b1 = ld4(rb + 1), b2 = ld4(rb + 2);
-            const float4 a0 = ld4(rb + 3), a1 = ld4(rb + 4), a2 = ld4(rb + 5);
+            const float4 b0 = ld4(rb + 0), a0 = ld4(rb + 3);
+            c.b1 = ld4(rb + 1);
+            c.b2 = ld4(rb + 2);
+            c.a1 = ld4(rb + 4);
+            c.a2 = ld4(rb + 5);
             boff -= 2 * (uint32_t)sizeof(st.rec[0]);
-            float dxa, dya, dxb, dyb;
-            const float pa = exact_power(a0, a1, fx, fy, dxa, dya), pb = exact_power(b0, b1, fx, fy, dxb, dyb);
-            float Ga = __expf(pa), Gb = __expf(pb);
+            c.pa = exact_power(a0, c.a1, fx, fy, c.dxa, c.dya);
+            c.pb = exact_power(b0, c.b1, fx, fy, c.dxb, c.dyb);
+#ifdef GSR_XB_NOTRANS
+            c.Ga = 1.f + c.pa * 0.01f;
+            c.Gb = 1.f + c.pb * 0.01f;
+#else
+            c.Ga = __expf(c.pa);
+            c.Gb = __expf(c.pb);
+#endif
             // alpha before upstream's `power > 0` skip, which the replay applies (the
             // clamp cannot move a value into or out of the re-check band)
-            float ala = fminf(0.99f, a1.y * Ga), alb = fminf(0.99f, b1.y * Gb);
-            if (__builtin_expect(__ballot(blend_near(ala) || blend_near(alb)) != 0, 0)) {
+            c.ala = fminf(0.99f, c.a1.y * c.Ga);
+            c.alb = fminf(0.99f, c.b1.y * c.Gb);
+            if (__builtin_expect(__ballot(blend_near(c.ala) || blend_near(c.alb)) != 0, 0)) {
                 // rare: the correctly rounded exp near 1/255 (gsr_blend.hpp)
-                if (blend_near(ala)) {
-                    Ga = exp_rn_f32(pa);
-                    ala = fminf(0.99f, a1.y * Ga);
+                if (blend_near(c.ala)) {
+                    c.Ga = exp_rn_f32(c.pa);
+                    c.ala = fminf(0.99f, c.a1.y * c.Ga);
                 }
-                if (blend_near(alb)) {
-                    Gb = exp_rn_f32(pb);
-                    alb = fminf(0.99f, b1.y * Gb);
+                if (blend_near(c.alb)) {
+                    c.Gb = exp_rn_f32(c.pb);
+                    c.alb = fminf(0.99f, c.b1.y * c.Gb);
                 }
             }
-            // (no early-out for pairs without a contributing pixel: 98.6% of the
-            // walked pairs have one at config C, the test cost more than it saved)
-            const Part qa = replay(pa, Ga, ala, a1.z, a1.w, a2, dxa, dya, lim);  // back to front: a before b
-            const Part qb = replay(pb, Gb, alb, b1.z, b1.w, b2, dxb, dyb, lim);   // !two: b is the zero record (alpha 0)
-            const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(a2.z));
-            const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(b2.z));
-            reduce_emit(qa, qb, gida, gidb, two);
+        };
+        // (no early-out for pairs without a contributing pixel: 98.6% of the
+        // walked pairs have one at config C, the test cost more than it saved)
+        for (int k = ns - 1; k >= 0; k -= 2) {
+            const bool two = k >= 1;  // wave-uniform
+            Cur c;
+            front(c);
+            const Part qa = replay(c.pa, c.Ga, c.ala, c.a1.z, c.a1.w, c.a2, c.dxa, c.dya, lim);  // back to front: a before b
+            const Part qb = replay(c.pb, c.Gb, c.alb, c.b1.z, c.b1.w, c.b2, c.dxb, c.dyb, lim);   // !two: b is the zero record (alpha 0)
+            const uint32_t gida = __builtin_amdgcn_readfirstlane(__float_as_uint(c.a2.z));
+            const uint32_t gidb = __builtin_amdgcn_readfirstlane(__float_as_uint(c.b2.z));
+            emit(reduce_sum(qa, qb), gida, gidb, two);
         }
     };
     // Double-buffered backwards stream, unrolled by two so the buffers swap roles
