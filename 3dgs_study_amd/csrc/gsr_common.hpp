@@ -102,6 +102,7 @@ enum CtrlWord {
     CTRL_NUM_RENDERED_HI = 1,
     CTRL_PREFILTER_ERR = 2,
     CTRL_DSORT_PASSES = 3,  // host copy only: the depth sort's pass count (its first digit scan publishes it)
+    CTRL_SHJAC = 4,         // device only: 1 when this forward's preprocess stored the SH direction Jacobian
     CTRL_WORDS = 16
 };
 // the depth sort's own control words (GeomLayout::dsort_ctrl, a line of their own:
@@ -128,6 +129,7 @@ struct GeomLayout {
     size_t emit_super;    // uint32 [rg_blocks(P)] instances per rank-gather block (RG_SUPER emit blocks)
     size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts + the ORDER_FLAGS words (zeroed by preprocess)
     size_t accum;         // float [P][ACCUM_STRIDE] the backward's gradient accumulator (gsr.h GSR_FLAG_PREPARE_BACKWARD)
+    size_t shjac;         // float [9][P] d colour / d view direction (GSR_FLAG_PREPARE_BACKWARD with SH colours)
     size_t bytes;
 };
 __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
@@ -159,6 +161,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.emit_super = take((size_t)rg_blocks(P) * 4 + 4);
     L.order_cnt = take((8 * 32 + 2) * 4);
     L.accum = take((size_t)(P > 0 ? P : 1) * 16 * 4);
+    L.shjac = take((size_t)9 * (P > 0 ? P : 1) * 4);
     L.bytes = o;
     return L;
 }
@@ -281,6 +284,46 @@ __device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, flo
                 b[15] = SH_C3_6 * x * (xx - 3.f * yy);
             }
         }
+    }
+}
+
+// backward.cu computeColorFromSH (backward): the derivatives of the SH colour with
+// respect to the normalised view direction, dRGB/dx, dRGB/dy, dRGB/dz per
+// channel, J[3 axis + c].  The forward (preprocess, when a backward will follow)
+// and the backward (otherwise) evaluate them with this one function, so the
+// stored values are the backward's own bit for bit.  `sh` = the Gaussian's row.
+__device__ __forceinline__ void sh_dir_jacobian(const float *sh, int deg, float x, float y, float z, float J[9]) {
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+#define SH(k) sh[3 * (k) + c]
+        float dx = 0.f, dy = 0.f, dz = 0.f;
+        if (deg > 0) {
+            dx = -SH_C1 * SH(3);
+            dy = -SH_C1 * SH(1);
+            dz = SH_C1 * SH(2);
+            if (deg > 1) {
+                dx += SH_C2_0 * y * SH(4) + SH_C2_2 * 2.f * -x * SH(6) + SH_C2_3 * z * SH(7) + SH_C2_4 * 2.f * x * SH(8);
+                dy += SH_C2_0 * x * SH(4) + SH_C2_1 * z * SH(5) + SH_C2_2 * 2.f * -y * SH(6) + SH_C2_4 * 2.f * -y * SH(8);
+                dz += SH_C2_1 * y * SH(5) + SH_C2_2 * 2.f * 2.f * z * SH(6) + SH_C2_3 * x * SH(7);
+                if (deg > 2) {
+                    dx += (SH_C3_0 * SH(9) * 3.f * 2.f * xy + SH_C3_1 * SH(10) * yz + SH_C3_2 * SH(11) * -2.f * xy +
+                           SH_C3_3 * SH(12) * -3.f * 2.f * xz + SH_C3_4 * SH(13) * (-3.f * xx + 4.f * zz - yy) +
+                           SH_C3_5 * SH(14) * 2.f * xz + SH_C3_6 * SH(15) * 3.f * (xx - yy));
+                    dy += (SH_C3_0 * SH(9) * 3.f * (xx - yy) + SH_C3_1 * SH(10) * xz +
+                           SH_C3_2 * SH(11) * (-3.f * yy + 4.f * zz - xx) + SH_C3_3 * SH(12) * -3.f * 2.f * yz +
+                           SH_C3_4 * SH(13) * -2.f * xy + SH_C3_5 * SH(14) * -2.f * yz +
+                           SH_C3_6 * SH(15) * -3.f * 2.f * xy);
+                    dz += (SH_C3_1 * SH(10) * xy + SH_C3_2 * SH(11) * 4.f * 2.f * yz +
+                           SH_C3_3 * SH(12) * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * SH(13) * 4.f * 2.f * xz +
+                           SH_C3_5 * SH(14) * (xx - yy));
+                }
+            }
+        }
+#undef SH
+        J[c] = dx;
+        J[3 + c] = dy;
+        J[6 + c] = dz;
     }
 }
 

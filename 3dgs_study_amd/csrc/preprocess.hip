@@ -33,6 +33,8 @@ struct PreArgs {
     uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, 0, 0, 0}
     int32_t *radii;
     uint32_t *order_cnt;
+    float *shjac;     // [9][P] the SH direction Jacobian, when a backward will follow (else NULL)
+    uint32_t *ctrl;   // geom control words (CTRL_SHJAC)
 };
 
 // SH -> RGB for one Gaussian, per channel (forward.cu computeColorFromSH).
@@ -240,6 +242,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     if (idx == 0) {  // and the flag words (one block may be all there is)
         a.order_cnt[ORDER_FILED] = 0u;
         a.order_cnt[ORDER_FRESH] = 0u;
+        a.ctrl[CTRL_SHJAC] = a.shjac != nullptr && use_sh ? 1u : 0u;  // this call's Jacobian, or none
     }
     // colour stage: the SH rows land in LDS now, after the geometry
     if (use_sh && !DIRECT) __syncthreads();
@@ -260,6 +263,14 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 const float v = sh_channel(sh, c, in.D, x, y, z);
                 clampbits |= (v < 0) ? (uint8_t)(1u << c) : (uint8_t)0;
                 rgb[c] = fmaxf(v, 0.0f);
+            }
+            if (a.shjac) {
+                // a backward follows: its view-direction term needs d colour / d dir,
+                // 36 B here (coalesced planes) instead of the 192-B SH row there
+                float J[9];
+                sh_dir_jacobian(sh, in.D, x, y, z, J);
+#pragma unroll
+                for (int k = 0; k < 9; k++) a.shjac[(size_t)k * in.P + idx] = J[k];
             }
         }
         a.depths[idx] = depth;
@@ -362,6 +373,8 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
     a.block_sums = at<uint4>(geom, L.block_sums);
     a.radii = radii;
     a.order_cnt = at<uint32_t>(geom, L.order_cnt);
+    a.ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+    a.shjac = (in.flags & GSR_FLAG_PREPARE_BACKWARD) && in.sh && !in.colors_precomp ? at<float>(geom, L.shjac) : nullptr;
     const int nb = pre_blocks(in.P);
     const bool split = in.sh_rest != nullptr;
     // the register prefetch of cat rows reads them as float4: 16-B aligned only

@@ -22,48 +22,21 @@ struct PreBwdArgs {
     const uint8_t *clamped;
     const float *splat_f;  // the forward's splat records as floats (opacity at 12 i + 5), when in.opacities is NULL
     const float *accum;
+    const float *shjac;     // [9][P] the forward's SH direction Jacobian (valid iff ctrl[CTRL_SHJAC])
+    const uint32_t *ctrl;   // geom control words
     BwdOutputs o;
 };
 
-// backward.cu computeColorFromSH (backward).  `sh` and `dsh` may alias (the
-// same LDS row): every SH coefficient is read before any gradient is written.
-__device__ __forceinline__ void sh_backward(const float *sh, float *dsh, int deg, int M, float ox, float oy, float oz,
-                                   const float dRGB[3], f3 &dmean) {
+// backward.cu computeColorFromSH (backward), given the colour's derivatives with
+// respect to the normalised view direction (J[3 axis + c], sh_dir_jacobian: stored
+// by the forward, or computed here from the SH row): dsh (b[k] * dRGB[c] for the
+// active coefficients, zeros for the rest of the M) and the direction term of
+// dL/dmean3D.  `dsh` may be the row the Jacobian was computed from.
+__device__ __forceinline__ void sh_backward_j(const float J[9], float *dsh, int deg, int M, float ox, float oy,
+                                              float oz, const float dRGB[3], f3 &dmean) {
     const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
     const float x = ox / len, y = oy / len, z = oz / len;
-    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-    float dRGBdx[3] = {0, 0, 0}, dRGBdy[3] = {0, 0, 0}, dRGBdz[3] = {0, 0, 0};
     const int ncoef = (deg + 1) * (deg + 1);
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-#define SH(k) sh[3 * (k) + c]
-        if (deg > 0) {
-            dRGBdx[c] = -SH_C1 * SH(3);
-            dRGBdy[c] = -SH_C1 * SH(1);
-            dRGBdz[c] = SH_C1 * SH(2);
-            if (deg > 1) {
-                dRGBdx[c] += SH_C2_0 * y * SH(4) + SH_C2_2 * 2.f * -x * SH(6) + SH_C2_3 * z * SH(7) +
-                             SH_C2_4 * 2.f * x * SH(8);
-                dRGBdy[c] += SH_C2_0 * x * SH(4) + SH_C2_1 * z * SH(5) + SH_C2_2 * 2.f * -y * SH(6) +
-                             SH_C2_4 * 2.f * -y * SH(8);
-                dRGBdz[c] += SH_C2_1 * y * SH(5) + SH_C2_2 * 2.f * 2.f * z * SH(6) + SH_C2_3 * x * SH(7);
-                if (deg > 2) {
-                    dRGBdx[c] += (SH_C3_0 * SH(9) * 3.f * 2.f * xy + SH_C3_1 * SH(10) * yz +
-                                  SH_C3_2 * SH(11) * -2.f * xy + SH_C3_3 * SH(12) * -3.f * 2.f * xz +
-                                  SH_C3_4 * SH(13) * (-3.f * xx + 4.f * zz - yy) + SH_C3_5 * SH(14) * 2.f * xz +
-                                  SH_C3_6 * SH(15) * 3.f * (xx - yy));
-                    dRGBdy[c] += (SH_C3_0 * SH(9) * 3.f * (xx - yy) + SH_C3_1 * SH(10) * xz +
-                                  SH_C3_2 * SH(11) * (-3.f * yy + 4.f * zz - xx) + SH_C3_3 * SH(12) * -3.f * 2.f * yz +
-                                  SH_C3_4 * SH(13) * -2.f * xy + SH_C3_5 * SH(14) * -2.f * yz +
-                                  SH_C3_6 * SH(15) * -3.f * 2.f * xy);
-                    dRGBdz[c] += (SH_C3_1 * SH(10) * xy + SH_C3_2 * SH(11) * 4.f * 2.f * yz +
-                                  SH_C3_3 * SH(12) * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * SH(13) * 4.f * 2.f * xz +
-                                  SH_C3_5 * SH(14) * (xx - yy));
-                }
-            }
-        }
-#undef SH
-    }
     float b[16];
     sh_basis(deg, x, y, z, b);
 #pragma unroll
@@ -77,15 +50,24 @@ __device__ __forceinline__ void sh_backward(const float *sh, float *dsh, int deg
     for (int k = 0; k < 16; k++)
         if (k >= ncoef && k < M) dsh[3 * k + 0] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
     for (int k = max(ncoef, 16); k < M; k++) dsh[3 * k + 0] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
-    const float ddx = (dRGBdx[0] * dRGB[0] + dRGBdx[1] * dRGB[1]) + dRGBdx[2] * dRGB[2];
-    const float ddy = (dRGBdy[0] * dRGB[0] + dRGBdy[1] * dRGB[1]) + dRGBdy[2] * dRGB[2];
-    const float ddz = (dRGBdz[0] * dRGB[0] + dRGBdz[1] * dRGB[1]) + dRGBdz[2] * dRGB[2];
+    const float ddx = (J[0] * dRGB[0] + J[1] * dRGB[1]) + J[2] * dRGB[2];
+    const float ddy = (J[3] * dRGB[0] + J[4] * dRGB[1]) + J[5] * dRGB[2];
+    const float ddz = (J[6] * dRGB[0] + J[7] * dRGB[1]) + J[8] * dRGB[2];
     // auxiliary.h dnormvdv
     const float sum2 = ox * ox + oy * oy + oz * oz;
     const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
     dmean.x += ((+sum2 - ox * ox) * ddx - oy * ox * ddy - oz * ox * ddz) * invsum32;
     dmean.y += (-ox * oy * ddx + (sum2 - oy * oy) * ddy - oz * oy * ddz) * invsum32;
     dmean.z += (-ox * oz * ddx - oy * oz * ddy + (sum2 - oz * oz) * ddz) * invsum32;
+}
+// The same from the SH row itself (no stored Jacobian): every coefficient is read
+// (into J) before any gradient is written, so `sh` and `dsh` may alias.
+__device__ __forceinline__ void sh_backward(const float *sh, float *dsh, int deg, int M, float ox, float oy, float oz,
+                                            const float dRGB[3], f3 &dmean) {
+    const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
+    float J[9];
+    sh_dir_jacobian(sh, deg, ox / len, oy / len, oz / len, J);
+    sh_backward_j(J, dsh, deg, M, ox, oy, oz, dRGB, dmean);
 }
 
 constexpr int PB_THREADS = 256;
@@ -178,6 +160,9 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const int idx = g0 + (int)threadIdx.x;
     const bool live = idx < in.P;
     const int li = live ? idx : in.P - 1;
+    // the forward stored d colour / d direction (a backward was announced): the SH
+    // rows are not read at all — dsh needs only the basis, the direction term J
+    const bool jac = stage && a.ctrl[CTRL_SHJAC] != 0u;
     // per-Gaussian inputs (issued before the rows: vmcnt counts in issue order)
     const f3 mean = {in.means3D[3 * li], in.means3D[3 * li + 1], in.means3D[3 * li + 2]};
     const Mat4 V = load_mat4(in.viewmatrix);
@@ -219,7 +204,7 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
         }
     };
     if constexpr (!DIRECT) {
-        if (stage) {
+        if (stage && !jac) {
             if constexpr (SPLIT) {
                 rows_to_lds_cols<PB_THREADS>(in.sh, g0, n, 3, 0, RW + 1, sh_lds);
                 if (RW > 3) rows_to_lds_cols<PB_THREADS>(in.sh_rest, g0, n, RW - 3, 3, RW + 1, sh_lds);
@@ -244,18 +229,26 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
                  "v"(acc1.w), "v"(accb), "v"(opac), "v"(rad), "v"(cl));
     ShStage st{};
     if (live) st = preprocess_bwd_geom(a, idx, mean, gin, acc0, acc1, accb, opac, qnorm, rad, cl, V, Pm);
-    if constexpr (DIRECT)  // after the geometry (its registers are not held through it); culled: zeros
+    float J[9];
+    if (jac) {  // after the geometry, like the row (coalesced planes)
+        if (live && st.vis)
+#pragma unroll
+            for (int k = 0; k < 9; k++) J[k] = a.shjac[(size_t)k * in.P + li];
+    } else if constexpr (DIRECT) {  // after the geometry (its registers are not held through it); culled: zeros
         if (live && st.vis) load_row();
+    }
     if (stage && !DIRECT) __syncthreads();
     if (live) {
         f3 dmean = st.dmean;
         if (stage) {
             float *row = DIRECT ? rowv : sh_lds + threadIdx.x * (RW + 1);
-            if (st.vis)
-                sh_backward(row, row, in.D, DIRECT ? 16 : in.M, mean.x - in.campos[0], mean.y - in.campos[1],
-                            mean.z - in.campos[2], st.dRGB, dmean);
-            else
+            const float ox = mean.x - in.campos[0], oy = mean.y - in.campos[1], oz = mean.z - in.campos[2];
+            if (!st.vis)
                 for (int k = 0; k < RW; k++) row[k] = 0.f;
+            else if (jac)
+                sh_backward_j(J, row, in.D, DIRECT ? 16 : in.M, ox, oy, oz, st.dRGB, dmean);
+            else
+                sh_backward(row, row, in.D, DIRECT ? 16 : in.M, ox, oy, oz, st.dRGB, dmean);
         }
         float *dm = a.o.dmeans3D + 3 * (size_t)idx;
         if (a.o.leaf.accumulate & 16) {  // AccumulateGrad of the _xyz leaf: grad += new
@@ -570,6 +563,8 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     a.clamped = at<uint8_t>(geom, G.off[GSR_GEOM_CLAMPED]);
     a.splat_f = at<float>(geom, G.off[GSR_GEOM_SPLATS]);
     a.accum = accum;
+    a.shjac = at<float>(geom, G.shjac);
+    a.ctrl = at<uint32_t>(geom, G.off[GSR_GEOM_CTRL]);
     a.o = o;
     const bool stage = in.sh && (o.dsh || o.drgb || o.sh_dir || o.leaf.dsh_dc) && in.M > 0;
     const bool split = in.sh_rest != nullptr;
