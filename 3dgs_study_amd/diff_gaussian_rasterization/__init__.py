@@ -364,6 +364,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         if plan:
             for p, g in fresh:
                 p.grad = g
+            views = {k: v[3] for k, v in plan.items() if v[3] is not None}
+            if views and ex is not None and hasattr(ex, "rasterizer_done"):  # the exchange may start right away
+                ex.rasterizer_done(views)
         return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None, None)
 
 
@@ -456,6 +459,8 @@ class _RasterizeModel(torch.autograd.Function):
                                  "snapshot_bw.dump", "backward")[0]
         for p, g in fresh:
             p.grad = g
+        if views and hasattr(ex, "rasterizer_done"):  # the exchange may start right away
+            ex.rasterizer_done(views)
         global last_leaf_plan
         last_leaf_plan = tuple(sorted(["means3D", "opacities", "rotations", "scales"] +
                                       ([] if sink_takes_sh else ["sh"])))

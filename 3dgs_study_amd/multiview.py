@@ -215,6 +215,23 @@ class GradAllReduce:
                 out[name] = tuple(self._views[i] for i in idx)
         return out
 
+    def rasterizer_done(self, views: dict) -> None:
+        """Called by the rasterizer's backward right after its kernels are queued, with
+        the bucket views it wrote (``leaf_bucket``'s answer).  On the step's last
+        backward, when those views cover every reduced parameter, the bucket is
+        complete already: its all-reduce starts here and the SH rebuild is queued
+        behind the backward's last kernel.  Done from the end-of-backward callback
+        instead, the host's round trip through the autograd engine left the device
+        idle for ~65 us per step (``tools/exchange_profile.py`` traces)."""
+        if self._work is not None or self._bucket is None or self._backwards + 1 != self.views_per_step:
+            return
+        covered = {id(v) for vs in views.values() for v in vs if v is not None}
+        if any(id(v) not in covered for v in self._views):
+            return
+        self._work = dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self.launched_in_backward = True
+        self._sh_rebuild()
+
     # ---- the end of each backward: start the bucket's all-reduce on the step's last
     def _queue_callback(self):
         if not self._cb_queued:
@@ -238,6 +255,11 @@ class GradAllReduce:
             bucket = self._pack()
             self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self.launched_in_backward = True
+            # the SH rebuild needs only the gathered records: queued here, behind the
+            # backward's last kernel and beside the bucket's all-reduce, instead of
+            # after the host has returned from backward() into the caller's
+            # __call__ (a host round trip the device spent idle: 60-90 us per step)
+            self._sh_rebuild()
 
     # ---- the rasterizer's SH sink
     def accepts(self, sh, means3D: torch.Tensor) -> bool:
@@ -276,6 +298,20 @@ class GradAllReduce:
             self._gathers.append((out, world, work))
         else:
             self._gathers.append((rec, 1, None))
+
+    def _sh_rebuild(self) -> None:
+        """The compute stream waits for the records' all-gather, then rebuilds the SH
+        leaf gradients (no-op when there is nothing gathered)."""
+        if self._sh is None or not self._gathers:
+            return
+        self._begin("exchange_wait")
+        for _, _, w in self._gathers:
+            if w is not None:
+                w.wait()
+        self._end("exchange_wait")
+        self._begin("sh_rebuild")
+        self._finish_sh()
+        self._end("sh_rebuild")
 
     def _finish_sh(self) -> None:
         xyz, f_dc, f_rest = self._sh
@@ -364,16 +400,9 @@ class GradAllReduce:
                 self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         bucket = self._bucket
         # the SH rebuild needs only the gathered records: it runs while the bucket's
-        # all-reduce is still in flight, and the compute stream waits for the bucket last
-        self._begin("exchange_wait")
-        for _, _, w in self._gathers:
-            if w is not None:
-                w.wait()
-        self._end("exchange_wait")
-        if self._sh is not None:
-            self._begin("sh_rebuild")
-            self._finish_sh()
-            self._end("sh_rebuild")
+        # all-reduce is still in flight (queued at the end of the backward already,
+        # unless nothing started there), and the compute stream waits for the bucket last
+        self._sh_rebuild()
         self._begin("exchange_wait")
         if self._work is not None:
             self._work.wait()

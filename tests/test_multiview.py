@@ -827,3 +827,74 @@ def test_bucket_with_fused_writers_gloo_world2(views_per_step):
     for a, b, x in zip(g0, g1, p):
         assert torch.equal(a, b)
         torch.testing.assert_close(a, 2 * wsum * x, rtol=1e-6, atol=1e-6)
+
+
+class _AllWriter(torch.autograd.Function):
+    """The rasterizer at N > 1 with every reduced leaf fused: its backward writes all
+    of them into the exchange's bucket views and tells the exchange
+    (``rasterizer_done``), which starts the bucket's all-reduce right there on the
+    step's last backward instead of in the end-of-backward callback."""
+
+    @staticmethod
+    def forward(ctx, xyz, opacity, w):
+        ctx.save_for_backward(xyz, opacity)
+        ctx.w = w
+        return (w * (xyz * xyz).sum() + w * (opacity * opacity).sum()).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        import diff_gaussian_rasterization as dgr
+
+        xyz, opacity = ctx.saved_tensors
+        ex = dgr._exchange
+        views = ex.leaf_bucket({"xyz": (xyz,), "opacity": (opacity,)})
+        for name, leaf in (("xyz", xyz), ("opacity", opacity)):
+            v = views[name][0]
+            val = 2 * ctx.w * leaf.detach() * g
+            if leaf.grad is None:
+                v.copy_(val)
+                leaf.grad = v
+            else:
+                v.add_(val)
+        started_before = ex.pending
+        ex.rasterizer_done(views)
+        ctx.started = (started_before, ex.pending)
+        _AllWriter.started.append(ctx.started)
+        return None, None, None
+
+    started = []
+
+
+def _all_writer_worker(rank, world, port, out, views_per_step):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    xyz, opacity = (torch.randn(s, requires_grad=True) for s in ((7, 3), (7, 1)))
+    ar = GradAllReduce([xyz, opacity], views_per_step=views_per_step)
+    _AllWriter.started = []
+    for v in range(views_per_step):
+        _AllWriter.apply(xyz, opacity, float(rank + 1) * (v + 1)).backward()
+    started = list(_AllWriter.started)
+    ar()
+    out[rank] = ([p.grad.clone() for p in (xyz, opacity)], [p.detach().clone() for p in (xyz, opacity)], started)
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("views_per_step", [1, 2])
+def test_bucket_started_by_the_rasterizer_gloo_world2(views_per_step):
+    """Every reduced leaf written by the fused backward: the all-reduce starts inside
+    the step's last backward (not on an earlier one), and the sums are right."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_all_writer_worker, args=(2, port, out, views_per_step), nprocs=2, join=True)
+        res = dict(out)
+    (g0, p, s0), (g1, _, s1) = res[0], res[1]
+    expect = [(0, 0)] * (views_per_step - 1) + [(0, 1)]
+    assert s0 == s1 == expect
+    wsum = sum(float(r + 1) * (v + 1) for r in (0, 1) for v in range(views_per_step))
+    for a, b, x in zip(g0, g1, p):
+        assert torch.equal(a, b)
+        torch.testing.assert_close(a, 2 * wsum * x, rtol=1e-6, atol=1e-6)

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--only", default="plain,local,rccl", help="comma-separated variants to run")
     ap.add_argument("--no-wrap", action="store_true", help="do not time the forward's host sync")
+    ap.add_argument("--glue", default="fused", choices=["fused", "reference"])
     ap.add_argument("--pg", default="eager", choices=["eager", "lazy", "none"],
                     help="process group: RCCL with device_id (eager communicator), without (lazy), or none")
     args = ap.parse_args()
@@ -79,7 +80,7 @@ def main():
             def step():
                 for p in params:
                     p.grad = None
-                train_step.train_step(cam, g, target, bg)
+                train_step.train_step(cam, g, target, bg, glue=args.glue)
                 if ar is not None:
                     ar()
 
