@@ -100,6 +100,7 @@ class GradAllReduce:
         self._timing = timing
         self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0}
         self._prev_ex = None
+        self._hdr = None        # push()'s cached record header
         self._installed = False
         self._sh_on = sh is not None and (sh_force or self._active())
         self._bind()
@@ -135,6 +136,8 @@ class GradAllReduce:
         self._hook_ids = {h.id for h in self._hooks}
 
     def _stale(self) -> bool:
+        if not callable(self._params_src) and not callable(self._sh_src):
+            return False  # fixed tensors: bound once (the host path runs this several times a step)
         params, sh = self._resolve()
         return (len(params) != len(self.params) or any(a is not b for a, b in zip(params, self.params))
                 or (sh is not None and any(a is not b for a, b in zip(sh, self._sh))))
@@ -289,8 +292,14 @@ class GradAllReduce:
         return torch.empty(_C.sh_record_floats(P), dtype=torch.float32, device=self._sh[0].device)
 
     def push(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int) -> None:
-        rec[0:3].copy_(campos.reshape(-1)[:3])
-        rec[3:4].fill_(float(sh_degree))
+        # the record's header [campos, degree]: one copy from a cached 4-float tensor
+        # (the view's camera is usually the same object step after step)
+        h = self._hdr
+        if h is None or h[0] is not campos or h[1] != campos._version or h[2] != int(sh_degree):
+            h = self._hdr = (campos, campos._version, int(sh_degree),
+                             torch.cat([campos.reshape(-1)[:3].float(),
+                                        torch.full((1,), float(sh_degree), device=rec.device)]))
+        rec[0:4].copy_(h[3])
         if self._active():
             world = dist.get_world_size(self.group)
             out = torch.empty(world * rec.numel(), dtype=rec.dtype, device=rec.device)

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--only", default="plain,local,rccl", help="comma-separated variants to run")
     ap.add_argument("--no-wrap", action="store_true", help="do not time the forward's host sync")
     ap.add_argument("--glue", default="fused", choices=["fused", "reference"])
+    ap.add_argument("--host", action="store_true", help="host-side time of the exchange's calls (perf_counter)")
     ap.add_argument("--pg", default="eager", choices=["eager", "lazy", "none"],
                     help="process group: RCCL with device_id (eager communicator), without (lazy), or none")
     args = ap.parse_args()
@@ -68,6 +69,31 @@ def main():
 
     if not args.no_wrap:
         lib.gsr_forward_preprocess = wrapped
+    hostt = {}
+    if args.host:  # wrap the calls on the step's host path and sum their wall time
+        import multiview
+
+        def wrap(owner, name, label):
+            fn = getattr(owner, name)
+
+            def w(*a, **k):
+                t0 = time.perf_counter()
+                try:
+                    return fn(*a, **k)
+                finally:
+                    hostt[label] = hostt.get(label, 0.0) + time.perf_counter() - t0
+            setattr(owner, name, w)
+        wrap(dist, "all_reduce", "dist.all_reduce")
+        wrap(dist, "all_gather_into_tensor", "dist.all_gather")
+        wrap(multiview.GradAllReduce, "_on_backward_end", "cb:_on_backward_end")
+        wrap(multiview.GradAllReduce, "_sh_rebuild", "sh_rebuild")
+        wrap(multiview.GradAllReduce, "__call__", "reducer()")
+        wrap(multiview.GradAllReduce, "push", "push")
+        wrap(multiview.GradAllReduce, "leaf_bucket", "leaf_bucket")
+        wrap(_C, "rasterize_gaussians_backward", "_C.backward")
+        wrap(_C, "_rasterize", "_C._rasterize")
+        wrap(train_step, "train_step", "train_step")
+        wrap(torch.Tensor, "backward", "loss.backward")
     res = {}
     for rnd in range(args.rounds):
         for name in args.only.split(","):
@@ -91,6 +117,7 @@ def main():
                 ar.reset_stats()
             _C.timing_enable(["exchange_wait", "sh_rebuild"])
             sync["t"], sync["n"] = 0.0, 0
+            hostt.clear()
             t0 = time.perf_counter()
             host = 0.0
             for _ in range(args.steps):
@@ -101,6 +128,10 @@ def main():
             dt = time.perf_counter() - t0
             stages = _C.timing_read()
             _C.timing_enable(False)
+            if args.host:
+                print(name, rnd, "host us/step:", {k: round(1e6 * v / args.steps, 1) for k, v in sorted(hostt.items())},
+                      flush=True)
+                hostt.clear()
             r = {"it_s": round(args.steps / dt, 1), "ms": round(1e3 * dt / args.steps, 4),
                  "sync_wait_ms": round(1e3 * sync["t"] / max(sync["n"], 1), 4),
                  "plan": list(dgr.last_leaf_plan)}
