@@ -190,3 +190,15 @@ def test_library_was_built_from_this_tree(lib):
     from build_id import build_id
 
     assert lib.gsr_build_id().decode() == build_id(), "libgsr.so is stale: rebuild (make -C 3dgs_study_amd/csrc)"
+
+
+def test_l1_grad_validates(lib):
+    """gsr_l1_grad (the L1 loss's backward): host-side checks only."""
+    assert lib.gsr_l1_grad(None, None, 0, None, None, None) == 0  # nothing to do
+    assert lib.gsr_l1_grad(None, None, -1, None, None, None) != 0
+    assert "negative" in lib.gsr_last_error().decode()
+    assert lib.gsr_l1_grad(None, None, 5, None, None, None) != 0
+    assert "NULL" in lib.gsr_last_error().decode()
+    # with lambda 0 the loss alone may be asked for (no gradient map), else it is required
+    assert lib.gsr_l1_ssim(1, 1, 3, 4, 4, ctypes.c_float(0.5), None, 1, 1, None) != 0
+    assert "NULL" in lib.gsr_last_error().decode()
