@@ -112,6 +112,11 @@ struct RadixPass {
     int id_bits;
     uint2 *ranges;
     int T;
+    // grouped depth passes (dsort_grouped, passes 2-4): hist holds block rows
+    // [NB][RADIX], sup the digit counts per group of DSORT_SB blocks [nsup][RADIX]
+    // (zeroed by depth_keys_kernel); no digit-scan launch.  NULL otherwise.
+    uint32_t *sup;
+    int nsup;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
@@ -122,14 +127,26 @@ enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
 // in three-pass mode keys beyond 2^24 (only non-candidates, +inf keys, reach it)
 // saturate their top 16 bits and keep that low byte: every pass then sorts by the
 // digits of one and the same key.
+__device__ __forceinline__ uint32_t key_rel(uint32_t k, uint32_t base, uint32_t passes);
 __device__ __forceinline__ uint32_t key_of(const RadixPass &a, uint32_t k) {
     if (a.role != RX_DEPTH_FIRST) return k;
-    const uint32_t d = k - a.ctrl[DCTRL_KEY_BASE];
-    return a.ctrl[DCTRL_PASSES] == 3 && d > 0xffffffu ? (0xffff00u | (d & 0xffu)) : d;
+    return key_rel(k, a.ctrl[DCTRL_KEY_BASE], a.ctrl[DCTRL_PASSES]);
 }
 __device__ __forceinline__ uint32_t load_key(const RadixPass &a, uint32_t idx) { return key_of(a, a.kin[idx]); }
 __device__ __forceinline__ bool pass_skipped(const RadixPass &a) {
     return a.role == RX_DEPTH_FOURTH && a.ctrl[DCTRL_PASSES] == 3;
+}
+
+// Which candidate key range decides the depth sort: base = the smallest key with
+// its low byte cleared, three passes when every candidate lies within 2^24 of it.
+__device__ __forceinline__ uint2 dsort_base_passes(uint32_t kmin, uint32_t kmax) {
+    const bool any = kmin <= kmax;
+    const uint32_t base = any ? (kmin & ~0xffu) : 0u;
+    return make_uint2(base, any && kmax - base > 0xffffffu ? 4u : 3u);
+}
+__device__ __forceinline__ uint32_t key_rel(uint32_t k, uint32_t base, uint32_t passes) {
+    const uint32_t d = k - base;
+    return passes == 3 && d > 0xffffffu ? (0xffff00u | (d & 0xffu)) : d;
 }
 
 // Workgroup -> radix block.  The per-block digit counts live column-major
@@ -260,7 +277,12 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) c += h[k][threadIdx.x];
-    a.hist[(size_t)threadIdx.x * a.NB + blk] = c;
+    if (a.sup) {  // grouped: the block's row, and its group's running counts
+        a.hist[(size_t)blk * RADIX + threadIdx.x] = c;
+        if (c) atomicAdd(&a.sup[(size_t)(blk >> DSORT_SB_LOG2) * RADIX + threadIdx.x], c);
+    } else {
+        a.hist[(size_t)threadIdx.x * a.NB + blk] = c;
+    }
 }
 
 // One workgroup per digit: exclusive scan of that digit's block counts.
@@ -294,9 +316,8 @@ __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPa
                 kmin = min(kmin, wmin[k]);
                 kmax = max(kmax, wmax[k]);
             }
-            const bool any = kmin <= kmax;
-            const uint32_t base = any ? (kmin & ~0xffu) : 0u;
-            const uint32_t passes = any && kmax - base > 0xffffffu ? 4u : 3u;
+            const uint2 bp = dsort_base_passes(kmin, kmax);
+            const uint32_t base = bp.x, passes = bp.y;
             a.ctrl_out[DCTRL_KEY_BASE] = base;
             a.ctrl_out[DCTRL_PASSES] = passes;
             if (a.host_ctrl) {  // the host launches the fourth pass only when it is needed
@@ -347,10 +368,26 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         if constexpr (MODE != RXM_UNPACK) vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
     }
     {  // where this block's items of digit d go: all smaller digits + earlier blocks
-        const uint32_t t = a.totals[threadIdx.x];
+        uint32_t t, before;
+        if (a.sup) {  // grouped: the groups before this block's, then its group's blocks before it
+            const uint32_t d = threadIdx.x, g = blk >> DSORT_SB_LOG2;
+            t = 0u;
+            before = 0u;
+#pragma unroll 8
+            for (int q = 0; q < a.nsup; q++) {
+                const uint32_t v = a.sup[(size_t)q * RADIX + d];
+                t += v;
+                before += (uint32_t)q < g ? v : 0u;
+            }
+#pragma unroll 8
+            for (uint32_t j = g << DSORT_SB_LOG2; j < blk; j++) before += a.hist[(size_t)j * RADIX + d];
+        } else {
+            t = a.totals[threadIdx.x];
+            before = a.hist[(size_t)threadIdx.x * a.NB + blk];
+        }
         uint32_t tot;
         const uint32_t inc = block_inclusive_scan<RX_THREADS>(t, wsum, &tot);
-        gshift[threadIdx.x] = inc - t + a.hist[(size_t)threadIdx.x * a.NB + blk];
+        gshift[threadIdx.x] = inc - t + before;
         if constexpr (MODE == RXM_UNPACK) dstart[threadIdx.x] = inc - t;
     }
     if constexpr (MODE == RXM_PACK)
@@ -453,7 +490,8 @@ static hipError_t radix_pass(const RadixPass &a, hipStream_t s, bool counted = f
     if (a.n == 0) return hipSuccess;
     // counted: the digit counts are already in a.hist (depth_keys_kernel)
     if (!counted) hipLaunchKernelGGL((radix_upsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
-    hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(a.minmax ? RADIX + 1 : RADIX), dim3(DSCAN_THREADS), 0, s, a);
+    if (!a.sup)  // grouped depth passes: each downsweep block sums its own prefix
+        hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(a.minmax ? RADIX + 1 : RADIX), dim3(DSCAN_THREADS), 0, s, a);
     hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     return hipGetLastError();
 }
@@ -738,6 +776,8 @@ struct DepthKeyArgs {
     uint32_t *keys;
     uint32_t *hist;   // [RADIX][NB]
     uint2 *minmax;    // [NB]
+    uint32_t *zero;   // the grouped passes' group counts, cleared here (every block a slice), or NULL
+    int zero_n;
 };
 template <int ITEMS>
 __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) {
@@ -748,6 +788,8 @@ __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) 
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
     const uint32_t blk = radix_block(a.NB);
+    if (a.zero)
+        for (int i = blockIdx.x * RX_THREADS + threadIdx.x; i < a.zero_n; i += gridDim.x * RX_THREADS) a.zero[i] = 0u;
     const Mat4 V = load_mat4(a.viewmatrix);
     float z[ITEMS];
 #pragma unroll
@@ -831,6 +873,10 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     a.shift = 8 * p;
     a.nbits = RADIX_BITS;
     a.dmask = RADIX - 1;
+    if (p > 0 && dsort_grouped(P)) {
+        a.nsup = dsort_nsup(P);
+        a.sup = at<uint32_t>(geom, L.dsort_sup) + (size_t)(p - 1) * a.nsup * RADIX;
+    }
     return a;
 }
 
@@ -846,6 +892,8 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     k.keys = at<uint32_t>(geom, L.dsort_keys_a);
     k.hist = at<uint32_t>(geom, L.dsort_hist);
     k.minmax = at<uint2>(geom, L.dsort_minmax);
+    k.zero = dsort_grouped(P) ? at<uint32_t>(geom, L.dsort_sup) : nullptr;
+    k.zero_n = dsort_grouped(P) ? 3 * dsort_nsup(P) * RADIX : 0;
     hipLaunchKernelGGL(depth_keys_kernel<ITEMS>, dim3(k.NB), dim3(RX_THREADS), 0, s, k);
     // host_ctrl: passes 1-3 only; the host reads the published pass count after its
     // one sync and launches the fourth (launch_depth_sort_fourth) when the keys need

@@ -93,6 +93,19 @@ __host__ __device__ inline bool tile_sort_packed(int T, int P) {
     const int bits = tile_bits(T), hi = bits - bits / 2;
     return (uint64_t)P <= (1ull << (32 - hi));
 }
+// Depth passes 2-4 without a digit-scan launch (binning.hip, "grouped" passes):
+// the upsweep adds its digit counts into its group of DSORT_SB blocks as well, and
+// each downsweep block sums the groups before its own and the blocks before it in
+// its group.  For up to DSORT_GROUPED_NB blocks (1.5M Gaussians); beyond that the
+// per-block reads outgrow the scan launch they replace.
+constexpr int DSORT_SB_LOG2 = 5, DSORT_SB = 1 << DSORT_SB_LOG2;
+#ifndef GSR_DSORT_GROUPED_NB
+#define GSR_DSORT_GROUPED_NB 1536
+#endif
+__host__ __device__ inline bool dsort_grouped(int P) { return radix_blocks(P, dsort_items(P)) <= GSR_DSORT_GROUPED_NB; }
+__host__ __device__ inline int dsort_nsup(int P) {
+    return dsort_grouped(P) ? (radix_blocks(P, dsort_items(P)) + DSORT_SB - 1) / DSORT_SB : 1;
+}
 __host__ __device__ inline int pre_blocks(int P) { return (P + PRE_THREADS - 1) / PRE_THREADS; }
 
 // ---- control words (uint32 [16]) inside the geom buffer (a device copy of what
@@ -125,6 +138,7 @@ struct GeomLayout {
     size_t dsort_totals;  // uint32 [RADIX]
     size_t dsort_minmax;  // uint2 [radix_blocks(P, dsort_items(P))] candidate key range per first-pass block
     size_t dsort_ctrl;    // uint32 [16] DsortCtrlWord
+    size_t dsort_sup;     // uint32 [3][dsort_nsup(P)][RADIX] passes 2-4: digit counts per group of DSORT_SB blocks
     size_t emit_sums;     // uint32 [emit_blocks(P)] instances before each emit block within its rank-gather block
     size_t emit_super;    // uint32 [rg_blocks(P)] instances per rank-gather block (RG_SUPER emit blocks)
     size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts + the ORDER_FLAGS words (zeroed by preprocess)
@@ -156,6 +170,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_totals = take((size_t)RADIX * 4);
     L.dsort_minmax = take((size_t)radix_blocks(P, dsort_items(P)) * 8);
     L.dsort_ctrl = take(CTRL_WORDS * 4);
+    L.dsort_sup = take((size_t)3 * dsort_nsup(P) * RADIX * 4);
     L.off[GSR_GEOM_DSORT_CTRL] = L.dsort_ctrl;
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
     L.emit_super = take((size_t)rg_blocks(P) * 4 + 4);

@@ -179,9 +179,12 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
         for (int k = 0; k < 4; k++) gin[3 + k] = in.rotations[4 * (size_t)li + k];
     }
     const float *acc = a.accum + (size_t)li * ACCUM_STRIDE;
-    const float4 acc0 = *reinterpret_cast<const float4 *>(acc);      // mean2D.x, mean2D.y, conic.x, conic.y
-    const float4 acc1 = *reinterpret_cast<const float4 *>(acc + 4);  // conic.w, opacity, color r, color g
-    const float accb = acc[8];                                       // color b
+    // the row (render_bwd.hip): colour r, g, b, mean2D.x | mean2D.y, conic.x, conic.y, conic.w | opacity
+    const float4 row0 = *reinterpret_cast<const float4 *>(acc), row1 = *reinterpret_cast<const float4 *>(acc + 4);
+    const float row8 = acc[8];
+    const float4 acc0 = make_float4(row0.w, row1.x, row1.y, row1.z);  // mean2D.x, mean2D.y, conic.x, conic.y
+    const float4 acc1 = make_float4(row1.w, row8, row0.x, row0.y);    // conic.w, opacity, color r, color g
+    const float accb = row0.z;                                        // color b
     // the sums' per-Gaussian opacity factor: the caller's opacities (coalesced), else
     // the forward's splat record (4 B out of every 48)
     const float opac_in = in.opacities ? in.opacities[li] : a.splat_f[12 * (size_t)li + 5];

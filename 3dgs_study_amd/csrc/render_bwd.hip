@@ -149,6 +149,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         }
     }
     const bool act_a = slot_a >= 0, act_b = slot_b >= 0;
+    // slot -> float of the accumulator row: the colour sums (slots 6-8) first, so
+    // the exchange's colour read (sh_exchange.hip) touches one 32-B sector per row
+    const int off_a = slot_a >= 6 ? slot_a - 6 : slot_a + 3, off_b = slot_b >= 6 ? slot_b - 6 : slot_b + 3;
     // lanes 16-31 (and 48-63) keep Gaussian b's sums in the first exchange stage
     const bool h16 = (lane & 16) != 0;
 
@@ -206,8 +209,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // lane-dependent addresses keep the compiler's atomic optimizer (a wave-scan
     // loop) out
     auto emit = [&](float v, uint32_t gida, uint32_t gidb, bool two) {
-        if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + slot_a, v);
-        if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + slot_b, v);
+        if (act_a) atomicAdd(a.accum + (size_t)gida * ACCUM_STRIDE + off_a, v);
+        if (two && act_b) atomicAdd(a.accum + (size_t)gidb * ACCUM_STRIDE + off_b, v);
     };
     auto reduce_sum = [&](const Part &pa, const Part &pb) -> float {
         const float k5 = h16 ? pb.g5 : pa.g5, s5 = h16 ? pa.g5 : pb.g5;

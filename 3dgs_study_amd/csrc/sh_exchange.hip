@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(SX_THREADS) sh_from_colors_kernel(int P, int n
 }
 
 // The clamp-masked colour gradient of one view straight from render_bwd's
-// accumulator rows (dcolor at floats 6..8), before preprocess_bwd runs, so the
+// accumulator rows (dcolor at floats 0..2: one 32-B sector), before preprocess_bwd runs, so the
 // exchange can start while preprocess_bwd computes: preprocess_bwd's own masking
 // (dcol * (clamped ? 0 : 1), zero for culled Gaussians), bit for bit.
 __global__ void __launch_bounds__(256) colors_from_accum_kernel(int P, const int32_t *__restrict__ radii,
@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) colors_from_accum_kernel(int P, const int
     const uint32_t cl = clamped[i];
     const float *row = accum + (size_t)i * ACCUM_STRIDE;
 #pragma unroll
-    for (int c = 0; c < 3; c++) drgb[3 * (size_t)i + c] = vis ? row[6 + c] * ((cl >> c) & 1u ? 0.f : 1.f) : 0.f;
+    for (int c = 0; c < 3; c++) drgb[3 * (size_t)i + c] = vis ? row[c] * ((cl >> c) & 1u ? 0.f : 1.f) : 0.f;
 }
 
 hipError_t launch_colors_from_accum(int P, const int32_t *radii, const uint8_t *clamped, const float *accum,
