@@ -356,6 +356,64 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     const uint2 span = block_span<TILE_N, MODE>(a, blk, sfb, sst, wsum);
     const uint32_t b0 = span.x;
     const uint32_t base = b0 + w * (uint32_t)WAVE_N + lane;
+    // where this block's items of digit d go: all smaller digits + earlier blocks.
+    // The grouped prefix is summed before the item loads (its 16-B row loads and
+    // the items would otherwise be live together: 112 instead of 57 VGPRs).
+    uint32_t t, before;
+    bool grouped = false;
+    if constexpr (MODE == RXM_KV) grouped = a.sup != nullptr;
+    if (grouped) {
+        // grouped: the groups before this block's, then its group's blocks before
+        // it.  Wave w sums the rows w, w + 4, ... (a lane: 4 digits, one 16-B
+        // load per row, every load of the wave in flight at once); the four
+        // partial sums meet in LDS (the stages, not yet in use).
+        const uint32_t g = blk >> DSORT_SB_LOG2, g0 = g << DSORT_SB_LOG2;
+        auto add4 = [](uint4 &s, uint4 v, bool on) {
+            s.x += on ? v.x : 0u;
+            s.y += on ? v.y : 0u;
+            s.z += on ? v.z : 0u;
+            s.w += on ? v.w : 0u;
+        };
+        uint4 t4 = make_uint4(0u, 0u, 0u, 0u), b4 = t4;
+        const uint4 *sup4 = reinterpret_cast<const uint4 *>(a.sup), *hist4 = reinterpret_cast<const uint4 *>(a.hist);
+        for (int q0 = 0; q0 < a.nsup; q0 += 4 * RX_WAVES) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = sup4[(size_t)min(q0 + 4 * k + w, a.nsup - 1) * (RADIX / 4) + lane];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int q = q0 + 4 * k + w;
+                add4(t4, v[k], q < a.nsup);
+                add4(b4, v[k], (uint32_t)q < g);
+            }
+        }
+        {
+            constexpr int PER = DSORT_SB / RX_WAVES;  // rows of the group per wave, 4 loads at a time
+#pragma unroll
+            for (int k0 = 0; k0 < PER; k0 += 4) {
+                uint4 v[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t j = g0 + (uint32_t)(RX_WAVES * (k0 + k) + w);
+                    v[k] = hist4[(size_t)(j < blk ? j : 0u) * (RADIX / 4) + lane];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) add4(b4, v[k], g0 + (uint32_t)(RX_WAVES * (k0 + k) + w) < blk);
+            }
+        }
+        static_assert(TILE_N >= RX_WAVES * RADIX, "the stages hold the partial sums");
+        reinterpret_cast<uint4 *>(stage_k)[w * 64 + lane] = t4;
+        reinterpret_cast<uint4 *>(stage_v)[w * 64 + lane] = b4;
+        __syncthreads();
+        t = 0u;
+        before = 0u;
+#pragma unroll
+        for (int k = 0; k < RX_WAVES; k++) {
+            t += stage_k[k * RADIX + threadIdx.x];
+            before += stage_v[k * RADIX + threadIdx.x];
+        }
+        __syncthreads();
+    }
     uint32_t kk[ITEMS], vv[MODE == RXM_UNPACK ? 1 : ITEMS], rk[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
@@ -367,21 +425,8 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
             kk[r] = ok ? load_key(a, idx) : 0u;
         if constexpr (MODE != RXM_UNPACK) vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
     }
-    {  // where this block's items of digit d go: all smaller digits + earlier blocks
-        uint32_t t, before;
-        if (a.sup) {  // grouped: the groups before this block's, then its group's blocks before it
-            const uint32_t d = threadIdx.x, g = blk >> DSORT_SB_LOG2;
-            t = 0u;
-            before = 0u;
-#pragma unroll 8
-            for (int q = 0; q < a.nsup; q++) {
-                const uint32_t v = a.sup[(size_t)q * RADIX + d];
-                t += v;
-                before += (uint32_t)q < g ? v : 0u;
-            }
-#pragma unroll 8
-            for (uint32_t j = g << DSORT_SB_LOG2; j < blk; j++) before += a.hist[(size_t)j * RADIX + d];
-        } else {
+    {
+        if (!grouped) {
             t = a.totals[threadIdx.x];
             before = a.hist[(size_t)threadIdx.x * a.NB + blk];
         }
