@@ -10,7 +10,9 @@
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
+#include <mutex>
 #include <string>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -25,6 +27,28 @@ thread_local std::string g_err;
 // (the call waits for that launch's event before returning, so calls from one
 // thread never share them in flight).
 thread_local uint32_t *g_pinned = nullptr;
+
+// geom buffers whose last forward prepared the backward (GSR_FLAG_PREPARE_BACKWARD:
+// accumulator zeroed, quadrants filed) and that no backward has used since: the
+// first backward then skips its bwd_prepare launch (the kernel would only read the
+// flag words and return).  Host-side, in call order; a forward_preprocess on the
+// buffer forgets it.  Shared by all threads (autograd runs the backward on its own
+// thread).  Anything not in the set takes the launch, so the set is only a hint.
+std::mutex g_prep_mu;
+std::unordered_set<const void *> g_prepared;
+void prepared_set(const void *geom, bool on) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    if (!on) {
+        g_prepared.erase(geom);
+        return;
+    }
+    if (g_prepared.size() > 4096) g_prepared.clear();  // forwards whose backward never came
+    g_prepared.insert(geom);
+}
+bool prepared_take(const void *geom) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    return g_prepared.erase(geom) != 0;
+}
 // pinned words: num_rendered lo / hi, prefiltered error
 thread_local hipEvent_t g_ctrl_ready = nullptr;
 
@@ -161,7 +185,8 @@ int validate(const gsr_inputs *in, bool forward) {
         return fail(GSR_ERR_CAPACITY, "image too large");
     if (in->footprint != GSR_FOOTPRINT_RECT && in->footprint != GSR_FOOTPRINT_TIGHT)
         return fail(GSR_ERR_ARGS, "footprint must be GSR_FOOTPRINT_RECT or GSR_FOOTPRINT_TIGHT (got %d)", in->footprint);
-    if (in->flags & ~GSR_FLAG_PREPARE_BACKWARD) return fail(GSR_ERR_ARGS, "unknown flags 0x%x", in->flags);
+    if (in->flags & ~(GSR_FLAG_PREPARE_BACKWARD | GSR_FLAG_L1_SEED)) return fail(GSR_ERR_ARGS, "unknown flags 0x%x", in->flags);
+    if (forward && (in->flags & GSR_FLAG_L1_SEED)) return fail(GSR_ERR_ARGS, "GSR_FLAG_L1_SEED is a backward flag");
     if (in->activations & ~(GSR_ACT_OPACITY | GSR_ACT_SCALE | GSR_ACT_ROTATION))
         return fail(GSR_ERR_ARGS, "unknown activations 0x%x", in->activations);
     if (in->P == 0) return GSR_OK;
@@ -248,6 +273,7 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (!geom || !radii) return fail(GSR_ERR_ARGS, "geom/radii buffers are NULL");
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
+    prepared_set(geom, false);  // preprocess resets the device's flag words too
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
     g_pinned[CTRL_DSORT_PASSES] = 0;
@@ -340,7 +366,10 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
     if (!prep) return GSR_OK;
     if (side)
         if (int rc = check_hip(hipStreamWaitEvent(s, side->join, 0), "join")) return rc;
-    return step(launch_bwd_prepare(*in, geom, img, (float *)acc, num_rendered > 0, true, true, s), "backward prepare", dbg, s);
+    if (int rc = step(launch_bwd_prepare(*in, geom, img, (float *)acc, num_rendered > 0, true, true, s), "backward prepare", dbg, s))
+        return rc;
+    prepared_set(geom, true);
+    return GSR_OK;
 }
 
 static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
@@ -375,13 +404,21 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
     const bool dbg = in->debug != 0;
     float *acc = (float *)accum;
     const bool colors = drgb && in->sh && in->M > 0;
+    // GSR_FLAG_L1_SEED: dL_dout_color is a gsr_l1_seed (the render backward forms
+    // the L1 loss's pixel gradient itself)
+    const gsr_l1_seed *seed = (in->flags & GSR_FLAG_L1_SEED) ? reinterpret_cast<const gsr_l1_seed *>(dL_dout_color) : nullptr;
+    if (seed && (!seed->image || !seed->gt || !seed->dloss || seed->n != (int64_t)3 * in->W * in->H))
+        return fail(GSR_ERR_ARGS, "l1 seed: image, gt and dloss required, n must be 3 W H = %lld (got %lld)",
+                    (long long)3 * in->W * in->H, (long long)seed->n);
     if (phases & 1) {
-        // zeroes the accumulator and files the quadrants for render_bwd's wave order
-        if (int rc = step(timed(GSR_STAGE_BWD_PREPARE, s, [&] { return launch_bwd_prepare(*in, const_cast<void *>(geom), img, acc, num_rendered > 0, internal, false, s); }),
-                          "backward prepare", dbg, s))
-            return rc;
+        // zeroes the accumulator and files the quadrants for render_bwd's wave order,
+        // unless this forward's prepare did both and no backward has run since
+        if (!(internal && prepared_take(geom)))
+            if (int rc = step(timed(GSR_STAGE_BWD_PREPARE, s, [&] { return launch_bwd_prepare(*in, const_cast<void *>(geom), img, acc, num_rendered > 0, internal, false, s); }),
+                              "backward prepare", dbg, s))
+                return rc;
         if (num_rendered > 0) {
-            if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, num_rendered, img, dL_dout_color, acc, s); }),
+            if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, num_rendered, img, seed ? nullptr : dL_dout_color, seed, acc, s); }),
                               "render backward", dbg, s))
                 return rc;
         }

@@ -31,7 +31,7 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
                               bool internal, bool forward, hipStream_t s);
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
-                             const void *img, const float *dL_dpix, float *accum, hipStream_t s);
+                             const void *img, const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s);
 
 // preprocess_bwd.hip
 struct BwdOutputs {

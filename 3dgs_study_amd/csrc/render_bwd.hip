@@ -49,9 +49,12 @@ struct RenderBwdArgs {
     const float *bg;
     const float *final_T;
     const uint32_t *n_contrib;
-    const float *dL_dpix;
+    const float *dL_dpix;       // [3][H][W], or NULL: the L1 loss's gradient from l1_* (GSR_FLAG_L1_SEED)
+    const float *l1_image, *l1_gt, *l1_dloss;
+    float l1_n;
     float *accum;
 };
+__device__ __forceinline__ float l1_sign(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }  // torch.sign
 
 // NB: copy the builtin's pair into scalars before bit-casting: with ROCm 7.2's
 // clang, __builtin_bit_cast(float, r[1]) on the returned vector silently reads
@@ -109,9 +112,16 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     const int last_contrib = inside ? (int)a.n_contrib[pix] : 0;
     float dpx0 = 0.f, dpx1 = 0.f, dpx2 = 0.f;
     if (inside) {
-        dpx0 = a.dL_dpix[pix];
-        dpx1 = a.dL_dpix[HW + pix];
-        dpx2 = a.dL_dpix[2 * HW + pix];
+        if (a.dL_dpix) {
+            dpx0 = a.dL_dpix[pix];
+            dpx1 = a.dL_dpix[HW + pix];
+            dpx2 = a.dL_dpix[2 * HW + pix];
+        } else {  // L1 seed: gsr_l1_grad's (dloss / n) * sign(image - gt), the same operations
+            const float q = a.l1_dloss[0] / a.l1_n;
+            dpx0 = q * l1_sign(a.l1_image[pix] - a.l1_gt[pix]);
+            dpx1 = q * l1_sign(a.l1_image[HW + pix] - a.l1_gt[HW + pix]);
+            dpx2 = q * l1_sign(a.l1_image[2 * HW + pix] - a.l1_gt[2 * HW + pix]);
+        }
     }
     const float bg_dot = a.bg[0] * dpx0 + a.bg[1] * dpx1 + a.bg[2] * dpx2;
     const float nTbg = -T_final * bg_dot;
@@ -427,7 +437,8 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
 }
 
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
-                             const void *img, const float *dL_dpix, float *accum, hipStream_t s) {
+                             const void *img, const float *dL_dpix, const gsr_l1_seed *l1, float *accum,
+                             hipStream_t s) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -443,6 +454,10 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.final_T = at<float>(img, Im.off[GSR_IMG_FINAL_T]);
     a.n_contrib = at<uint32_t>(img, Im.off[GSR_IMG_N_CONTRIB]);
     a.dL_dpix = dL_dpix;
+    a.l1_image = l1 ? l1->image : nullptr;
+    a.l1_gt = l1 ? l1->gt : nullptr;
+    a.l1_dloss = l1 ? l1->dloss : nullptr;
+    a.l1_n = l1 ? (float)(double)l1->n : 0.f;  // gsr_l1_grad's fN
     a.accum = accum;
     a.order_cnt = at<uint32_t>(geom, G.order_cnt);
     a.flags = at<uint32_t>(const_cast<void *>(geom), G.order_cnt) + ORDER_FILED;

@@ -103,6 +103,11 @@ class GsrLeafGrads(ctypes.Structure):
                 ("reserved", ctypes.c_int32)]
 
 
+class GsrL1Seed(ctypes.Structure):  # gsr.h gsr_l1_seed
+    _fields_ = [("image", ctypes.c_void_p), ("gt", ctypes.c_void_p), ("dloss", ctypes.c_void_p),
+                ("n", ctypes.c_int64)]
+
+
 class LeafGrads:
     """Outputs (and their inputs) of ``rasterize_gaussians_backward(leaf=...)``: the
     leaf gradients of the caller's activations written by the library itself
@@ -151,7 +156,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lib = None
 
@@ -287,6 +292,33 @@ def _stream(device):
 
 
 FLAG_PREPARE_BACKWARD = 1  # gsr.h gsr_flags
+FLAG_L1_SEED = 2
+
+
+def l1_loss(image: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+    """mean|image - gt| (utils/loss_utils.py l1_loss) as a 0-dim float32 device
+    tensor: gsr_l1_ssim's loss-only form (lambda 0), no gradient map."""
+    lib = load_library()
+    x, y = image.contiguous(), gt.contiguous()
+    if x.shape != y.shape or x.dim() != 3 or x.dtype != torch.float32 or y.dtype != torch.float32:
+        raise RuntimeError(f"l1_loss: image {tuple(x.shape)} and gt {tuple(y.shape)} must be equal float32 [C,H,W]")
+    C, H, W = x.shape
+    scratch = torch.empty(lib.gsr_l1_ssim_scratch_bytes(C, H, W), dtype=torch.uint8, device=x.device)
+    out = torch.empty(3, dtype=torch.float32, device=x.device)
+    _check(lib.gsr_l1_ssim(x.data_ptr(), y.data_ptr(), C, H, W, 0.0, None, scratch.data_ptr(), out.data_ptr(),
+                           _stream(x.device)), "gsr_l1_ssim")
+    return out[0]
+
+
+def l1_grad(image: torch.Tensor, gt: torch.Tensor, dloss: torch.Tensor) -> torch.Tensor:
+    """(dloss / n) * sign(image - gt): the L1 mean's image gradient (gsr_l1_grad)."""
+    lib = load_library()
+    x, y = image.contiguous(), gt.contiguous()
+    g = torch.empty_like(x)
+    d = dloss.detach().to(torch.float32).contiguous()
+    _check(lib.gsr_l1_grad(x.data_ptr(), y.data_ptr(), x.numel(), d.data_ptr(), g.data_ptr(), _stream(x.device)),
+           "gsr_l1_grad")
+    return g
 
 
 def _inputs(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
@@ -378,7 +410,7 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                  viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
                                  geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None, dsh_planar=False,
-                                 on_drgb=None, leaf=None, opacities=None, inputs=None):
+                                 on_drgb=None, leaf=None, opacities=None, inputs=None, l1_seed=None):
     """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)
 
     Not upstream (keyword-only extensions; the defaults are upstream's behaviour):
@@ -399,10 +431,14 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     it from the geom buffer; passed here it is read coalesced); required with a
     leaf opacity gradient.
     ``inputs`` (private) — the forward's validated inputs (``_rasterize``): the
-    same tensors as the positional ones, not re-checked."""
+    same tensors as the positional ones, not re-checked.
+    ``l1_seed`` — ``(image, gt, dloss)``: the image's gradient is the L1 loss
+    mean|image - gt|'s (gsr.h GSR_FLAG_L1_SEED), formed per pixel by the render
+    backward; ``dL_dout_color`` is then ignored (may be None)."""
     lib = load_library()
     if inputs is None:
-        H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+        ref = l1_seed[0] if l1_seed is not None else dL_dout_color
+        H, W = int(ref.size(1)), int(ref.size(2))
         inputs = _inputs(background, means3D, colors, opacities, scales, rotations, scale_modifier, cov3D_precomp,
                          viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
     s, keep, device, M = inputs
@@ -434,7 +470,17 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     ret = (dmeans2D, dcolors, dopacity, None if own_xyz else dmeans3D, dcov3D, dsh, dscales, drot)
     if P == 0:
         return ret
-    grad = _prep(dL_dout_color, "dL_dout_color", device)
+    if l1_seed is not None:
+        image, gt, dloss = (_prep(t, n, device) for t, n in zip(l1_seed, ("l1 image", "l1 gt", "l1 dloss")))
+        if image.shape != (3, s.H, s.W) or gt.shape != image.shape or dloss.numel() != 1:
+            raise RuntimeError(f"l1_seed: image and gt must be [3,{s.H},{s.W}] and dloss one element")
+        seed = GsrL1Seed(image.data_ptr(), gt.data_ptr(), dloss.data_ptr(), 3 * s.H * s.W)
+        s = GsrInputs.from_buffer_copy(s)  # the forward's struct, with the backward flag
+        s.flags |= FLAG_L1_SEED
+        grad_ptr = ctypes.addressof(seed)
+    else:
+        grad = _prep(dL_dout_color, "dL_dout_color", device)
+        grad_ptr = grad.data_ptr()
     if not radii.is_contiguous():
         radii = radii.contiguous()
     if drgb_out is not None and (drgb_out.dtype != torch.float32 or drgb_out.device != device
@@ -442,7 +488,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         raise RuntimeError("drgb_out must be a contiguous float32 tensor of >= 3P elements on the input device")
     head = (ctypes.byref(s), radii.data_ptr(), geomBuffer.data_ptr(),
             binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(), int(R),
-            grad.data_ptr(), None, dmeans2D.data_ptr(), _ptr(dcolors), _ptr(dopacity),
+            grad_ptr, None, dmeans2D.data_ptr(), _ptr(dcolors), _ptr(dopacity),
             dmeans3D.data_ptr(), _ptr(dcov3D))
     stream = _stream(device)
     if leaf is None and drgb_out is None:

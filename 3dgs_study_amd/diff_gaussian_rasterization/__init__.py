@@ -377,7 +377,7 @@ class _RasterizeModel(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means3D, means2D, features_dc, features_rest, opacity, scaling, rotation, raster_settings,
-                grad_on=True):
+                grad_on=True, l1_target=None):
         rs = raster_settings
         empty = _empty_like_device(means3D)
         rest = features_rest if features_rest.numel() else None
@@ -393,25 +393,38 @@ class _RasterizeModel(torch.autograd.Function):
         src = _input_sources(rs, means3D, None, opacity, scaling, rotation, None, features_dc, rest)
         copies = {k: t for k, t in keep.items() if t is not None and t is not src[k]}
         ctx.inputs = (s, device, M, frozenset(k for k, t in keep.items() if t is not None), tuple(copies))
+        # l1_target: the L1 loss mean|color - target| as a third output, its image
+        # gradient formed inside the render backward (gsr.h GSR_FLAG_L1_SEED)
+        l1 = l1_target is not None
+        ctx.l1 = l1
+        loss = _C.l1_loss(color, l1_target) if l1 else None
         ctx.save_for_backward(means3D, features_dc, features_rest, opacity, scaling, rotation, radii, geom, binning,
-                              img, *copies.values())
+                              img, *copies.values(), *((color, l1_target) if l1 else ()))
         ctx.mark_non_differentiable(radii)
         # radii never carry a gradient: no zero int32 [P] tensor materialised per backward
         ctx.set_materialize_grads(False)
-        return color, radii
+        return (color, radii, loss) if l1 else (color, radii)
 
     @staticmethod
-    def backward(ctx, grad_out_color, _grad_radii):
+    def backward(ctx, grad_out_color, _grad_radii, grad_loss=None):
         rs = ctx.raster_settings
         saved = ctx.saved_tensors
-        if grad_out_color is None:  # the image was not used (set_materialize_grads(False))
+        s, device, M, present, copy_names = ctx.inputs
+        nc = 10 + len(copy_names)
+        seed = None
+        if ctx.l1 and grad_loss is not None:
+            color, gt = saved[nc:nc + 2]
+            if grad_out_color is None:  # the image only feeds the loss: no gradient map at all
+                seed = (color, gt, grad_loss)
+            else:
+                grad_out_color = grad_out_color + _C.l1_grad(color, gt, grad_loss)
+        if grad_out_color is None and seed is None:  # the image was not used (set_materialize_grads(False))
             grad_out_color = torch.zeros((3, rs.image_height, rs.image_width), dtype=torch.float32,
                                          device=saved[1].device)
         means3D, f_dc, f_rest, opacity, scaling, rotation, radii, geom, binning, img = saved[:10]
-        s, device, M, present, copy_names = ctx.inputs
         rest = f_rest if f_rest.numel() else None
         src = _input_sources(rs, means3D, None, opacity, scaling, rotation, None, f_dc, rest)
-        src.update(zip(copy_names, saved[10:]))
+        src.update(zip(copy_names, saved[10:nc]))
         inputs = (s, {k: (src[k] if k in present else None) for k in _INPUT_SRC}, device, M)
         needs = ctx.needs_input_grad
         ex = _exchange
@@ -448,7 +461,7 @@ class _RasterizeModel(torch.autograd.Function):
         kw["drotation"] = out("rotations", rotation, (P, 4), 8)
         kw["dmeans3D"] = out("means3D", means3D, (P, 3), 16)
         leaf = _C.LeafGrads(accumulate=acc, **kw)
-        bkw = dict(inputs=inputs, leaf=leaf)
+        bkw = dict(inputs=inputs, leaf=leaf, l1_seed=seed)
         if sink_takes_sh:
             rec = ex.record(P)
             bkw["drgb_out"], bkw["on_drgb"] = rec[4:], lambda: ex.push(rec, rs.campos, rs.sh_degree)
@@ -469,10 +482,11 @@ class _RasterizeModel(torch.autograd.Function):
             torch.zeros_like(f_rest) if "dsh_rest" in kw else None)
         return (bucketed("means3D", kw["dmeans3D"]), d_means2D, kw.get("dsh_dc"), d_rest,
                 bucketed("opacities", kw["dopacity"]), bucketed("scales", kw["dscaling"]),
-                bucketed("rotations", kw["drotation"]), None, None)
+                bucketed("rotations", kw["drotation"]), None, None, None)
 
 
-def rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation, raster_settings):
+def rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation, raster_settings,
+                    l1_target=None):
     """The rasterizer over GaussianModel's stored parameters (not upstream).
 
     The reference renders with activations of the model's leaves
@@ -486,9 +500,14 @@ def rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scali
     and the backward writes the leaves' gradients (through the activations'
     backwards) — the same values the reference's autograd produces, without the cat,
     the activation kernels, their backwards or the cat's slice copies.
-    ``means2D`` is the screen-space gradient carrier, as upstream."""
+    ``means2D`` is the screen-space gradient carrier, as upstream.
+    ``l1_target`` (a [3,H,W] float32 image, or None): also return the L1 loss
+    mean|image - target| (utils/loss_utils.py l1_loss, train.py:102) as a third
+    output; when the image feeds nothing but that loss, the backward forms the loss's
+    pixel gradient inside the render backward (no gradient map, no separate loss
+    node or kernel).  Values equal ``l1_loss(image, target)`` and its backward."""
     return _RasterizeModel.apply(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation,
-                                 raster_settings, torch.is_grad_enabled())
+                                 raster_settings, torch.is_grad_enabled(), l1_target)
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
@@ -527,12 +546,13 @@ class GaussianRasterizer(nn.Module):
             rs = self.raster_settings
             return _C.mark_visible(positions, rs.viewmatrix, rs.projmatrix)
 
-    def forward_model(self, means3D, means2D, features_dc, features_rest, opacity, scaling, rotation):
+    def forward_model(self, means3D, means2D, features_dc, features_rest, opacity, scaling, rotation,
+                      l1_target=None):
         """``rasterize_model`` with these settings: GaussianModel's stored parameters
         (_xyz, _features_dc, _features_rest, _opacity, _scaling, _rotation) in place of
-        the activations ``forward`` takes."""
+        the activations ``forward`` takes (``l1_target``: also the L1 loss)."""
         return rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation,
-                               self.raster_settings)
+                               self.raster_settings, l1_target)
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
                 cov3D_precomp=None):

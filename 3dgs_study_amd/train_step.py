@@ -129,14 +129,17 @@ def stored_parameters(pc):
 
 
 def render_fused(viewpoint_camera, pc, bg_color: torch.Tensor, scaling_modifier: float = 1.0,
-                 debug: bool = False) -> dict:
+                 debug: bool = False, l1_target: torch.Tensor = None) -> dict:
     """``render`` (gaussian_renderer/__init__.py:20-112, SH and scale/rotation
     branches) over the model's stored parameters: the rasterizer activates them and
     reads the SH from _features_dc / _features_rest itself (rasterize_model).  The
-    screen-space gradient carrier is a zero leaf (upstream's ``zeros_like + 0`` with
-    ``retain_grad`` carries the same gradient in ``.grad``)."""
+    screen-space gradient carrier is a leaf whose values nothing reads (upstream's
+    ``zeros_like + 0`` with ``retain_grad`` carries the same gradient in ``.grad``;
+    the rasterizer ignores the values, so they are left unset here: no fill launch).
+    ``l1_target``: also the L1 loss against it (``out["l1"]``; rasterize_model), whose
+    image gradient the render backward forms itself."""
     xyz, f_dc, f_rest, opacity, scaling, rotation = stored_parameters(pc)
-    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device)
+    screenspace_points = torch.empty_like(xyz, dtype=xyz.dtype, device=xyz.device).requires_grad_(True)
     raster_settings = GaussianRasterizationSettings(
         image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
         tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5), bg=bg_color,
@@ -144,9 +147,12 @@ def render_fused(viewpoint_camera, pc, bg_color: torch.Tensor, scaling_modifier:
         projmatrix=viewpoint_camera.full_proj_transform, sh_degree=pc.active_sh_degree,
         campos=viewpoint_camera.camera_center, prefiltered=False, debug=debug)
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
-    rendered_image, radii = rasterizer.forward_model(xyz, screenspace_points, f_dc, f_rest, opacity, scaling, rotation)
-    return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
-            "radii": radii}
+    res = rasterizer.forward_model(xyz, screenspace_points, f_dc, f_rest, opacity, scaling, rotation, l1_target)
+    out = {"render": res[0], "viewspace_points": screenspace_points, "visibility_filter": res[1] > 0,
+           "radii": res[1]}
+    if l1_target is not None:
+        out["l1"] = res[2]
+    return out
 
 
 # ---------------------------------------------------------------- losses (utils/loss_utils.py)
@@ -181,6 +187,18 @@ def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11) -> torch
 
 
 GLUES = ("fused", "reference")
+_SEEDS: dict = {}
+
+
+def _unit_seed(loss: torch.Tensor) -> torch.Tensor:
+    """A cached 1.0 of the loss's device and dtype: ``loss.backward(seed)`` is
+    ``loss.backward()`` without the per-step ``ones_like`` fill kernel.  Nothing
+    writes the seed (the loss backward only reads dloss)."""
+    key = (loss.device, loss.dtype)
+    t = _SEEDS.get(key)
+    if t is None:
+        t = _SEEDS[key] = torch.ones((), device=loss.device, dtype=loss.dtype)
+    return t
 
 
 def train_step(camera, gaussians, target: torch.Tensor, bg: torch.Tensor, lambda_dssim: float = 0.0,
@@ -192,9 +210,15 @@ def train_step(camera, gaussians, target: torch.Tensor, bg: torch.Tensor, lambda
     if glue == "fused":
         import train_ops
 
-        out = render_fused(camera, gaussians, bg)
-        image = out["render"]
-        loss = train_ops.l1_ssim_loss(image, target, lambda_dssim)
+        if lambda_dssim:
+            out = render_fused(camera, gaussians, bg)
+            loss = train_ops.l1_ssim_loss(out["render"], target, lambda_dssim)
+        else:  # the L1 loss out of the rasterizer: its gradient formed in the render backward
+            out = render_fused(camera, gaussians, bg, l1_target=target)
+            loss = out["l1"]
+        loss.backward(_unit_seed(loss))  # the seed dloss = 1 without a fill launch per step
+        out["loss"] = loss
+        return out
     elif glue == "reference":
         out = render(camera, gaussians, bg)
         image = out["render"]

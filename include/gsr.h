@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 8
+#define GSR_ABI_VERSION 9
 
 enum gsr_status {
     GSR_OK = 0,
@@ -76,7 +76,21 @@ enum gsr_footprint { GSR_FOOTPRINT_RECT = 0, GSR_FOOTPRINT_TIGHT = 1 };
  * work the backward then skips (its accum argument NULL: the geom buffer's
  * accumulator; a second backward of the same forward zeroes it again itself).
  * Only a speed hint: every backward is correct with or without it. */
-enum gsr_flags { GSR_FLAG_PREPARE_BACKWARD = 1 };
+enum gsr_flags { GSR_FLAG_PREPARE_BACKWARD = 1, GSR_FLAG_L1_SEED = 2 };
+
+/* GSR_FLAG_L1_SEED (backward calls; not upstream): the image's gradient is that of
+ * the L1 loss mean|image - gt| (utils/loss_utils.py l1_loss, train.py:102 with
+ * lambda_dssim = 0), and the backward's dL_dout_color argument points to this
+ * struct instead of a [3,H,W] map.  The render backward forms each pixel's
+ * dL/dpixel = (dloss / n) * sign(image - gt) itself — gsr_l1_grad's values bit
+ * for bit — so no gradient map is written or read.  image is the forward's
+ * out_color, gt a [3,H,W] float32 image, dloss one float on the device, n = 3 H W. */
+typedef struct gsr_l1_seed {
+    const float *image;
+    const float *gt;
+    const float *dloss;
+    int64_t n;
+} gsr_l1_seed;
 
 /* gsr_inputs.activations (not upstream; 0 = upstream's inputs, used as given).
  * The reference hands the rasterizer activations of GaussianModel's stored

@@ -35,7 +35,8 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 8
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 9
+    assert ctypes.sizeof(_C.GsrL1Seed) == 32  # struct gsr_l1_seed: three pointers and an int64
     # 12 x 4-byte scalars, 11 pointers, then sh_rest and two int32 (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 48 + 12 * 8 + 8
     assert _C.GsrInputs.footprint.offset == 40
@@ -190,6 +191,25 @@ def test_library_was_built_from_this_tree(lib):
     from build_id import build_id
 
     assert lib.gsr_build_id().decode() == build_id(), "libgsr.so is stale: rebuild (make -C 3dgs_study_amd/csrc)"
+
+
+def test_l1_seed_flag_validates(lib):
+    """GSR_FLAG_L1_SEED: a backward flag (a forward rejects it), and the backward
+    checks the seed struct before any device work."""
+    from diff_gaussian_rasterization import _C
+
+    s = _inputs(flags=_C.FLAG_L1_SEED)
+    n = ctypes.c_int64(-1)
+    assert lib.gsr_forward_preprocess(ctypes.byref(s), None, None, ctypes.byref(n), None) != 0
+    assert "backward flag" in lib.gsr_last_error().decode()
+    for seed in (_C.GsrL1Seed(1, 1, 1, 3 * 16 * 16 + 1), _C.GsrL1Seed(None, 1, 1, 3 * 16 * 16),
+                 _C.GsrL1Seed(1, 1, None, 3 * 16 * 16)):
+        # (in, radii, geom, binning, img, num_rendered, seed, accum, dmeans2D, dcolors, dopacity,
+        #  dmeans3D, dcov3D, dsh, dscales, drot, stream)
+        rc = lib.gsr_backward(ctypes.byref(s), 1, 1, 1, 1, 0, ctypes.addressof(seed), None, 1, None, 1, 1, None,
+                              1, 1, 1, None)
+        assert rc != 0
+        assert "l1 seed" in lib.gsr_last_error().decode()
 
 
 def test_l1_grad_validates(lib):

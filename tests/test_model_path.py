@@ -200,3 +200,61 @@ def test_train_step_glues_agree(dev):
     assert torch.equal(outs["fused"][1], outs["reference"][1])
     for name, a, b in zip(NAMES, outs["fused"][2], outs["reference"][2]):
         assert _rel(a, b) <= 1e-5, (name, _rel(a, b))
+
+
+def _l1_run(cam, g, dev, gt, fused, extra=None):
+    """render_fused -> L1 against gt (+ sum(image * extra)) -> backward; fused: the
+    loss out of the rasterizer (rasterize_model(l1_target=...), the render backward
+    forming the L1 pixel gradient), else train_ops' L1 kernel on the image."""
+    import train_ops
+    import train_step
+
+    gd = g.to(dev, requires_grad=True)
+    out = train_step.render_fused(cam.to(dev), gd, torch.zeros(3, device=dev), l1_target=gt if fused else None)
+    loss = out["l1"] if fused else train_ops.l1_ssim_loss(out["render"], gt, 0.0)
+    total = loss if extra is None else loss + (out["render"] * extra).sum()
+    total.backward()
+    torch.cuda.synchronize()
+    return (loss.detach().cpu(), out["render"].detach().cpu(), [p.grad.cpu() for p in gd.params()],
+            out["viewspace_points"].grad.cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mixed", [False, True], ids=["loss_only", "image_also_used"])
+def test_rasterizer_l1_seed_bit_identical_on_isolated_scene(dev, mixed):
+    """The L1 loss out of the rasterizer (gsr.h GSR_FLAG_L1_SEED: the render backward
+    forms (dloss / n) sign(image - gt) per pixel) against the separate L1 kernel and its
+    gradient map: same loss bits, and — one atomic addend per accumulator row on this
+    scene — the same gradient bits.  ``image_also_used``: the image feeds a second term
+    too, so the backward adds the L1 map to that gradient instead (same bits)."""
+    from helpers import random_dL
+    from test_leaf_grads import _isolated_scene
+
+    cam, g = _isolated_scene()
+    H, W = cam.image_height, cam.image_width
+    gt = torch.rand(3, H, W, generator=torch.Generator().manual_seed(4)).to(dev)
+    extra = torch.from_numpy(random_dL(H, W)).to(dev) if mixed else None
+    a = _l1_run(cam, g, dev, gt, True, extra)
+    b = _l1_run(cam, g, dev, gt, False, extra)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for name, x, y in zip(NAMES, a[2], b[2]):
+        assert float(y.abs().max()) > 0, name
+        assert torch.equal(x, y), (name, float((x - y).abs().max()))
+    assert torch.equal(a[3], b[3])
+
+
+@pytest.mark.gpu
+def test_rasterizer_l1_seed_general_scene(dev):
+    """The same at a shared-pixel scene: loss bits equal, gradients within the
+    accumulator atomics' run-to-run spread."""
+    from helpers import case
+
+    cam, g = case(50_000, 480, 360, 3, seed=9, view=4)
+    gt = torch.rand(3, 360, 480, generator=torch.Generator().manual_seed(2)).to(dev)
+    a = _l1_run(cam, g, dev, gt, True)
+    b = _l1_run(cam, g, dev, gt, False)
+    b2 = _l1_run(cam, g, dev, gt, False)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for name, x, y, y2 in zip(NAMES, a[2], b[2], b2[2]):
+        noise = _rel(y2, y)
+        assert _rel(x, y) <= max(4e-6, 4 * noise), (name, _rel(x, y), noise)
