@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import case, rel_l2, random_dL, run_hip, run_oracle
+from helpers import activated, case, read_intermediates, rel_l2, random_dL, run_hip, run_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -555,3 +555,33 @@ def test_sh_rows_unaligned_take_the_staged_path(dev):
     np.testing.assert_array_equal(a["color"], b["color"])
     for n in a["grads"]:
         assert rel_l2(b["grads"][n], a["grads"][n]) <= 1e-6, n
+
+
+@pytest.mark.parametrize("P", [33 * 1024 + 5, 1536 * 1024, 1536 * 1024 + 1],
+                         ids=["two_groups_ragged", "grouped_max", "past_grouped"])
+def test_depth_sort_grouped_boundaries(dev, P):
+    """The grouped depth passes (gsr_common.hpp dsort_grouped: no digit-scan launch up
+    to 1,536 radix blocks) at a ragged group count, at the largest grouped size (48
+    groups) and one Gaussian past it (the digit scans again): the order is a
+    permutation, and the visible Gaussians appear in (depth bits, index) order of the
+    device's own depths (the sort's keys come from the same operations)."""
+    from diff_gaussian_rasterization import _C
+
+    cam, g = case(P, 64, 48, 0, seed=3, radius=2.0)
+    a = activated(g, False, 1.0)
+    t = lambda x: x.to(dev)  # noqa: E731
+    I, color, radii, geom, binning, img = _C.rasterize_gaussians(
+        torch.zeros(3, device=dev), t(a["means3D"]), torch.empty(0, device=dev), t(a["opacities"]),
+        t(a["scales"]), t(a["rotations"]), 1.0, torch.empty(0, device=dev), t(cam.world_view_transform),
+        t(cam.full_proj_transform), math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5), 48, 64, t(a["shs"]), 0,
+        t(cam.camera_center), False, False)
+    torch.cuda.synchronize()
+    h = read_intermediates(geom, binning, img, P, 64, 48, I)
+    order = h["depth_order"]
+    assert np.array_equal(np.sort(order), np.arange(P, dtype=np.uint32))
+    vis = radii.cpu().numpy() > 0
+    assert vis.sum() > P // 4
+    vis_order = order[vis[order]]
+    dbits = h["depths"].view(np.uint32)
+    idx = np.nonzero(vis)[0]
+    np.testing.assert_array_equal(vis_order, idx[np.lexsort((idx, dbits[vis]))])
