@@ -326,14 +326,21 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     return GSR_OK;
 }
 
-int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
-                       const int32_t *radii, float *out_color, void *stream) {
+static int forward_render_impl(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
+                               const int32_t *radii, float *out_color, const float *gt, float *loss_out,
+                               void *stream) {
     if (int rc = validate(in, true)) return rc;
     if (!out_color) return fail(GSR_ERR_ARGS, "out_color is NULL");
+    if (gt && (!loss_out || !img)) return fail(GSR_ERR_ARGS, "l1: loss_out and img required");
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
-    if (in->P == 0)  // upstream returns the zero-initialised image untouched
-        return check_hip(hipMemsetAsync(out_color, 0, (size_t)3 * in->W * in->H * sizeof(float), s), "memset");
+    const size_t npix = (size_t)3 * in->W * in->H;
+    float *l1_part = gt ? at<float>(img, img_layout(in->W, in->H).l1_part) : nullptr;
+    if (in->P == 0) {  // upstream returns the zero-initialised image untouched
+        if (int rc = check_hip(hipMemsetAsync(out_color, 0, npix * sizeof(float), s), "memset")) return rc;
+        if (!gt) return GSR_OK;
+        return step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", dbg, s);
+    }
     if (!geom || !img || (num_rendered > 0 && !binning)) return fail(GSR_ERR_ARGS, "scratch buffers are NULL");
     if (num_rendered > 0) {
         if (int rc = step(timed(GSR_STAGE_DUPLICATE, s, [&] { return launch_emit(in->P, in->W, in->H, geom, radii, binning, num_rendered, s); }),
@@ -363,13 +370,31 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
     float *zero = prep && !side ? (float *)acc : nullptr;
     if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, zero, acc_bytes, s); }), "render", dbg, s))
         return rc;
-    if (!prep) return GSR_OK;
+    if (!prep)  // the L1 loss, if asked for, on its own
+        return gt ? step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", dbg, s)
+                  : GSR_OK;
     if (side)
         if (int rc = check_hip(hipStreamWaitEvent(s, side->join, 0), "join")) return rc;
-    if (int rc = step(launch_bwd_prepare(*in, geom, img, (float *)acc, num_rendered > 0, true, true, s), "backward prepare", dbg, s))
+    // the L1 loss's partial sums ride in the same launch as the quadrant filing
+    int l1_nb = 0;
+    if (int rc = step(launch_bwd_prepare(*in, geom, img, (float *)acc, num_rendered > 0, true, true, s, gt ? out_color : nullptr, gt, &l1_nb), "backward prepare", dbg, s))
         return rc;
+    if (gt)
+        if (int rc = step(launch_l1_finish(nullptr, nullptr, npix, l1_part, l1_nb, false, loss_out, s), "l1 loss", dbg, s))
+            return rc;
     prepared_set(geom, true);
     return GSR_OK;
+}
+
+int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
+                       const int32_t *radii, float *out_color, void *stream) {
+    return forward_render_impl(in, geom, binning, img, num_rendered, radii, out_color, nullptr, nullptr, stream);
+}
+
+int gsr_forward_render_l1(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
+                          const int32_t *radii, float *out_color, const float *gt, float *loss_out, void *stream) {
+    if (!gt) return fail(GSR_ERR_ARGS, "gt is NULL");
+    return forward_render_impl(in, geom, binning, img, num_rendered, radii, out_color, gt, loss_out, stream);
 }
 
 static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,

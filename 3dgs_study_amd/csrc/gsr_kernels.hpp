@@ -28,8 +28,11 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
                              float *out_color, float *acc_zero, size_t acc_bytes, hipStream_t s);
 
 // render_bwd.hip
+// l1 (forward only, or NULL): {image, gt, n} whose L1 partial sums (gsr_l1.hpp) the
+// same launch writes into img's l1_part; returns their count in *l1_nb
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
-                              bool internal, bool forward, hipStream_t s);
+                              bool internal, bool forward, hipStream_t s, const float *l1_x = nullptr,
+                              const float *l1_y = nullptr, int *l1_nb = nullptr);
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
                              const void *img, const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s);
 
@@ -55,6 +58,8 @@ size_t l1_ssim_scratch_floats(int C, int H, int W);
 hipError_t launch_l1_ssim(const float *x, const float *y, int C, int H, int W, float lambda, float *grad,
                           float *partials, float *out, hipStream_t s);
 hipError_t launch_l1_grad(const float *x, const float *y, size_t n, const float *dloss, float *grad, hipStream_t s);
+hipError_t launch_l1_finish(const float *x, const float *y, size_t n, float *partials, int nb, bool from_xy,
+                            float *out, hipStream_t s);
 hipError_t launch_adam(const gsr_adam_segment *segs, int nseg, int step, double beta1, double beta2, double eps,
                        hipStream_t s);
 hipError_t launch_densify_stats(int P, const int32_t *radii, const float *vgrad, int vstride, float *max_radii,

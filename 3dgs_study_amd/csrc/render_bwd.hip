@@ -21,6 +21,7 @@
 // doubled the kernel's time).
 #include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
+#include "gsr_l1.hpp"
 
 namespace gsr {
 
@@ -374,11 +375,22 @@ struct BwdPrepArgs {
     int nq, maxc;
     int internal;         // accum4 is geom's accumulator (ORDER_FRESH applies to it)
     int forward;
+    // gsr_forward_render_l1: workgroups [file_blocks, file_blocks + l1_nb) write the
+    // L1 loss's partial sums instead (l1_x NULL: none)
+    int file_blocks, l1_nb;
+    const float *l1_x, *l1_y;
+    size_t l1_n;
+    float *l1_part;
 };
 constexpr int PREP_THREADS = 256;
+static_assert(PREP_THREADS == L1_THREADS, "the L1 partial blocks share the launch");
 __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a) {
+    if ((int)blockIdx.x >= a.file_blocks) {  // workgroup-uniform: an L1 partial-sum block
+        l1_block_partial(a.l1_x, a.l1_y, a.l1_n, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_part);
+        return;
+    }
     const size_t tid = (size_t)blockIdx.x * PREP_THREADS + threadIdx.x;
-    const size_t nthreads = (size_t)gridDim.x * PREP_THREADS;
+    const size_t nthreads = (size_t)a.file_blocks * PREP_THREADS;
     if (a.forward) {
         // the next kernel (a backward's first) reads these; no block of this one does
         if (tid == 0) {
@@ -416,7 +428,8 @@ __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a
 }
 
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
-                              bool internal, bool forward, hipStream_t s) {
+                              bool internal, bool forward, hipStream_t s, const float *l1_x, const float *l1_y,
+                              int *l1_nb) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -432,7 +445,14 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
     a.forward = forward ? 1 : 0;
     const size_t want = forward ? ((size_t)a.nq + PREP_THREADS - 1) / PREP_THREADS : (a.n4 + PREP_THREADS - 1) / PREP_THREADS;
     const int blocks = (int)(want < 2048 ? (want > 0 ? want : 1) : 2048);
-    hipLaunchKernelGGL(bwd_prepare_kernel, dim3(blocks), dim3(PREP_THREADS), 0, s, a);
+    a.file_blocks = blocks;
+    a.l1_x = l1_x;
+    a.l1_y = l1_y;
+    a.l1_n = (size_t)3 * in.W * in.H;
+    a.l1_nb = l1_x ? l1_blocks(a.l1_n) : 0;
+    a.l1_part = l1_x ? at<float>(const_cast<void *>(img), Im.l1_part) : nullptr;
+    if (l1_nb) *l1_nb = a.l1_nb;
+    hipLaunchKernelGGL(bwd_prepare_kernel, dim3(blocks + a.l1_nb), dim3(PREP_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 #include <cmath>
 
 #include "gsr_kernels.hpp"
+#include "gsr_l1.hpp"
 #include "gsr_wave.hpp"
 
 namespace gsr {
@@ -266,29 +267,9 @@ __global__ void __launch_bounds__(1024) l1_ssim_finish_kernel(const float *parti
 // sign(x - y), bit for bit, with the incoming dloss read on the device — no
 // gradient map is written in the forward and scaled again in the backward.
 // Per workgroup one partial sum for l1_ssim_finish_kernel.
-constexpr int L1_THREADS = 256, L1_BLOCKS = 1024;
+// (L1_THREADS, L1_BLOCKS, l1_blocks and the block body: gsr_l1.hpp)
 __global__ void __launch_bounds__(L1_THREADS) l1_kernel(const float *x, const float *y, size_t n, float *partials) {
-    __shared__ float wsum[L1_THREADS / 64];
-    const size_t n4 = n >> 2, stride = (size_t)gridDim.x * L1_THREADS;
-    const float4 *x4 = reinterpret_cast<const float4 *>(x), *y4 = reinterpret_cast<const float4 *>(y);
-    float acc = 0.f;
-    for (size_t i = (size_t)blockIdx.x * L1_THREADS + threadIdx.x; i < n4; i += stride) {
-        const float4 a = x4[i], b = y4[i];
-        acc += (fabsf(a.x - b.x) + fabsf(a.y - b.y)) + (fabsf(a.z - b.z) + fabsf(a.w - b.w));
-    }
-    if (blockIdx.x == 0)  // the tail of a length that is not a multiple of 4
-        for (size_t i = (n4 << 2) + threadIdx.x; i < n; i += L1_THREADS) acc += fabsf(x[i] - y[i]);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float tot = 0.f;
-#pragma unroll
-        for (int k = 0; k < L1_THREADS / 64; k++) tot += wsum[k];
-        partials[2 * blockIdx.x] = tot;
-        partials[2 * blockIdx.x + 1] = 0.f;
-    }
+    l1_block_partial(x, y, n, blockIdx.x, gridDim.x, partials);
 }
 
 __device__ __forceinline__ float sign_f(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
@@ -306,9 +287,19 @@ __global__ void __launch_bounds__(L1_THREADS) l1_grad_kernel(const float *x, con
         for (size_t i = (n4 << 2) + threadIdx.x; i < n; i += L1_THREADS) g[i] = q * sign_f(x[i] - y[i]);
 }
 
-static int l1_blocks(size_t n) {
-    const size_t want = (n / 4 + L1_THREADS - 1) / L1_THREADS;
-    return (int)(want < (size_t)L1_BLOCKS ? (want > 0 ? want : 1) : L1_BLOCKS);
+
+// The L1 loss from partial sums [nb][2] already in partials (bwd_prepare_kernel's,
+// gsr_forward_render_l1), or, with from_xy, from x and y (l1_kernel into partials:
+// room for 2 L1_BLOCKS floats).  out: gsr_l1_ssim's [3] (loss, L1 term, 0).
+hipError_t launch_l1_finish(const float *x, const float *y, size_t n, float *partials, int nb, bool from_xy,
+                            float *out, hipStream_t s) {
+    const float invN = 1.0f / (float)(double)n;  // launch_l1_ssim's invN for C H W = n
+    if (from_xy) {
+        nb = l1_blocks(n);
+        hipLaunchKernelGGL(l1_kernel, dim3(nb), dim3(L1_THREADS), 0, s, x, y, n, partials);
+    }
+    hipLaunchKernelGGL(l1_ssim_finish_kernel, dim3(1), dim3(1024), 0, s, (const float *)partials, nb, 0.0f, invN, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_l1_grad(const float *x, const float *y, size_t n, const float *dloss, float *grad, hipStream_t s) {

@@ -64,6 +64,7 @@ EXPORTED = (
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
     "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
+    "gsr_forward_render_l1",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -190,6 +191,8 @@ def load_library():
     lib.gsr_forward_preprocess.restype = ctypes.c_int
     lib.gsr_forward_render.argtypes = [pin, vp, vp, vp, i64, vp, vp, vp]
     lib.gsr_forward_render.restype = ctypes.c_int
+    lib.gsr_forward_render_l1.argtypes = [pin, vp, vp, vp, i64, vp, vp, vp, vp, vp]
+    lib.gsr_forward_render_l1.restype = ctypes.c_int
     lib.gsr_backward.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward.restype = ctypes.c_int
     lib.gsr_backward_planar.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
@@ -375,14 +378,16 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
                projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-               footprint=None, prepare_backward=False, sh_rest=None, activations=0):
+               footprint=None, prepare_backward=False, sh_rest=None, activations=0, l1_target=None):
     """rasterize_gaussians plus its validated inputs ``(struct, kept tensors, device,
     M)``, which the autograd Function hands back to the backward (``inputs=``) so the
     same tensors are not re-checked there: the host's backward path is on the
     step's critical path once the GPU work is short.  ``sh_rest`` / ``activations``
     (not upstream; gsr_inputs): GaussianModel's stored parameters as the inputs —
     ``sh`` = _features_dc and ``sh_rest`` = _features_rest instead of their cat, and
-    the ACT_* bits of the opacity / scale / rotation inputs the library activates."""
+    the ACT_* bits of the opacity / scale / rotation inputs the library activates.
+    ``l1_target`` (not upstream; gsr_forward_render_l1): also the L1 loss
+    mean|color - l1_target|, appended to the result as a 0-dim tensor."""
     lib = load_library()
     H, W = int(image_height), int(image_width)
     if footprint is not None and footprint not in FOOTPRINTS:
@@ -401,10 +406,19 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
     _check(lib.gsr_forward_preprocess(ctypes.byref(s), geom.data_ptr(), _ptr(radii), ctypes.byref(num_rendered),
                                       stream), "rasterize_gaussians (preprocess)")
     binning = _alloc((lib.gsr_binning_bytes(num_rendered.value, W, H),), torch.uint8, device)
-    _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
-                                  num_rendered.value, _ptr(radii), out_color.data_ptr(), stream),
-           "rasterize_gaussians (render)")
-    return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M)
+    if l1_target is None:
+        _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
+                                      num_rendered.value, _ptr(radii), out_color.data_ptr(), stream),
+               "rasterize_gaussians (render)")
+        return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M)
+    gt = _prep(l1_target, "l1_target", device)
+    if gt is None or gt.shape != (3, H, W):
+        raise RuntimeError(f"l1_target must be a float32 [3,{H},{W}] tensor on {device}")
+    loss = torch.empty(3, dtype=torch.float32, device=device)
+    _check(lib.gsr_forward_render_l1(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
+                                     num_rendered.value, _ptr(radii), out_color.data_ptr(), gt.data_ptr(),
+                                     loss.data_ptr(), stream), "rasterize_gaussians (render + L1)")
+    return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M), loss[0]
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,

@@ -385,19 +385,23 @@ class _RasterizeModel(torch.autograd.Function):
                 rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, features_dc, rs.sh_degree,
                 rs.campos, rs.prefiltered, rs.debug)
         prep = grad_on and any(ctx.needs_input_grad[:7])
-        num_rendered, color, radii, geom, binning, img, (s, keep, device, M) = _call_native(
-            lambda *a: _C._rasterize(*a, prepare_backward=prep, sh_rest=rest, activations=_C.ACT_ALL), args, rs.debug,
+        # l1_target: the L1 loss mean|color - target| as a third output — its partial
+        # sums in the same launch as the backward's preparation (gsr_forward_render_l1),
+        # its image gradient formed inside the render backward (GSR_FLAG_L1_SEED)
+        fwd_l1 = l1_target is not None and os.environ.get("GSR_FWD_L1", "1") != "0"  # (A/B switch)
+        res = _call_native(
+            lambda *a: _C._rasterize(*a, prepare_backward=prep, sh_rest=rest, activations=_C.ACT_ALL,
+                                     l1_target=l1_target if fwd_l1 else None), args, rs.debug,
             "snapshot_fw.dump", "forward")
+        num_rendered, color, radii, geom, binning, img, (s, keep, device, M) = res[:7]
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         src = _input_sources(rs, means3D, None, opacity, scaling, rotation, None, features_dc, rest)
         copies = {k: t for k, t in keep.items() if t is not None and t is not src[k]}
         ctx.inputs = (s, device, M, frozenset(k for k, t in keep.items() if t is not None), tuple(copies))
-        # l1_target: the L1 loss mean|color - target| as a third output, its image
-        # gradient formed inside the render backward (gsr.h GSR_FLAG_L1_SEED)
         l1 = l1_target is not None
         ctx.l1 = l1
-        loss = _C.l1_loss(color, l1_target) if l1 else None
+        loss = (res[7] if fwd_l1 else _C.l1_loss(color, l1_target)) if l1 else None
         ctx.save_for_backward(means3D, features_dc, features_rest, opacity, scaling, rotation, radii, geom, binning,
                               img, *copies.values(), *((color, l1_target) if l1 else ()))
         ctx.mark_non_differentiable(radii)

@@ -170,6 +170,15 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
 int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
                        const int32_t *radii, float *out_color, void *stream);
 
+/* gsr_forward_render plus the L1 loss mean|out_color - gt| (utils/loss_utils.py
+ * l1_loss, train.py:102; not upstream) into loss_out [3] = {loss, loss, 0}
+ * (gsr_l1_ssim's layout with lambda 0, the same bits).  With
+ * GSR_FLAG_PREPARE_BACKWARD the loss's partial sums are computed in the same
+ * launch as the backward's preparation.  gt is [3,H,W] float32; img is required.
+ * The backward's GSR_FLAG_L1_SEED (above) is its gradient. */
+int gsr_forward_render_l1(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
+                          const int32_t *radii, float *out_color, const float *gt, float *loss_out, void *stream);
+
 /* Replaces RasterizeGaussiansBackwardCUDA -> Rasterizer::backward.
  * accum: NULL = the accumulator inside geom (zeroed by a forward called with
  * GSR_FLAG_PREPARE_BACKWARD, else here), or a caller buffer of gsr_accum_bytes(P).

@@ -212,6 +212,17 @@ def test_l1_seed_flag_validates(lib):
         assert "l1 seed" in lib.gsr_last_error().decode()
 
 
+def test_forward_render_l1_validates(lib):
+    """gsr_forward_render_l1: gt, loss_out and img required (host-side checks)."""
+    s = _inputs()
+    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, 1, 0, 1, 1, None, 1, None) != 0
+    assert "gt is NULL" in lib.gsr_last_error().decode()
+    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, None, 0, 1, 1, 1, 1, None) != 0
+    assert "loss_out and img required" in lib.gsr_last_error().decode()
+    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, 1, 0, 1, 1, 1, None, None) != 0
+    assert "loss_out and img required" in lib.gsr_last_error().decode()
+
+
 def test_l1_grad_validates(lib):
     """gsr_l1_grad (the L1 loss's backward): host-side checks only."""
     assert lib.gsr_l1_grad(None, None, 0, None, None, None) == 0  # nothing to do

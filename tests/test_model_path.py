@@ -258,3 +258,37 @@ def test_rasterizer_l1_seed_general_scene(dev):
     for name, x, y, y2 in zip(NAMES, a[2], b[2], b2[2]):
         noise = _rel(y2, y)
         assert _rel(x, y) <= max(4e-6, 4 * noise), (name, _rel(x, y), noise)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grad", [True, False], ids=["prepared", "no_grad"])
+def test_rasterizer_l1_loss_bits(dev, grad):
+    """gsr_forward_render_l1's loss — its partial sums in the backward preparation's
+    launch (a forward that will be differentiated) or in the L1 kernel of its own —
+    equals train_ops' L1 kernel on the same image bit for bit (one block decomposition,
+    gsr_l1.hpp), and an empty scene gives mean|gt| over upstream's zero image."""
+    import math
+
+    import synthetic
+    import train_ops
+    import train_step
+    from diff_gaussian_rasterization import _C
+    from helpers import case
+
+    cam, g = case(20_000, 320, 240, 3, seed=5, view=1)
+    gt = torch.rand(3, 240, 320, generator=torch.Generator().manual_seed(8)).to(dev)
+    gd = g.to(dev, requires_grad=grad)
+    with torch.set_grad_enabled(grad):
+        out = train_step.render_fused(cam.to(dev), gd, torch.zeros(3, device=dev), l1_target=gt)
+    ref = train_ops.l1_ssim_loss(out["render"].detach(), gt, 0.0)
+    torch.cuda.synchronize()
+    assert torch.equal(out["l1"].detach(), ref)
+    cam0 = synthetic.make_camera(64, 48, view=0).to(dev)
+    gt0 = gt[:, :48, :64].contiguous()
+    z3, z1, z4 = (torch.zeros(0, k, device=dev) for k in (3, 1, 4))
+    res = _C._rasterize(torch.zeros(3, device=dev), z3, torch.empty(0, device=dev), z1, z3, z4, 1.0,
+                        torch.empty(0, device=dev), cam0.world_view_transform, cam0.full_proj_transform,
+                        math.tan(cam0.FoVx * 0.5), math.tan(cam0.FoVy * 0.5), 48, 64, torch.zeros(0, 1, 3, device=dev),
+                        0, cam0.camera_center, False, False, l1_target=gt0)
+    assert res[0] == 0 and float(res[1].abs().max()) == 0.0
+    assert torch.equal(res[7], train_ops.l1_ssim_loss(torch.zeros_like(gt0), gt0, 0.0))
