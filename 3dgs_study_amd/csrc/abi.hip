@@ -328,7 +328,7 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
 
 static int forward_render_impl(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
                                const int32_t *radii, float *out_color, const float *gt, float *loss_out,
-                               void *stream) {
+                               uint8_t *visible_out, void *stream) {
     if (int rc = validate(in, true)) return rc;
     if (!out_color) return fail(GSR_ERR_ARGS, "out_color is NULL");
     if (gt && (!loss_out || !img)) return fail(GSR_ERR_ARGS, "l1: loss_out and img required");
@@ -377,7 +377,7 @@ static int forward_render_impl(const gsr_inputs *in, void *geom, void *binning, 
         if (int rc = check_hip(hipStreamWaitEvent(s, side->join, 0), "join")) return rc;
     // the L1 loss's partial sums ride in the same launch as the quadrant filing
     int l1_nb = 0;
-    if (int rc = step(launch_bwd_prepare(*in, geom, img, (float *)acc, num_rendered > 0, true, true, s, gt ? out_color : nullptr, gt, &l1_nb), "backward prepare", dbg, s))
+    if (int rc = step(launch_bwd_prepare(*in, geom, img, (float *)acc, num_rendered > 0, true, true, s, gt ? out_color : nullptr, gt, &l1_nb, radii, visible_out), "backward prepare", dbg, s))
         return rc;
     if (gt)
         if (int rc = step(launch_l1_finish(nullptr, nullptr, npix, l1_part, l1_nb, false, loss_out, s), "l1 loss", dbg, s))
@@ -388,13 +388,19 @@ static int forward_render_impl(const gsr_inputs *in, void *geom, void *binning, 
 
 int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
                        const int32_t *radii, float *out_color, void *stream) {
-    return forward_render_impl(in, geom, binning, img, num_rendered, radii, out_color, nullptr, nullptr, stream);
+    return forward_render_impl(in, geom, binning, img, num_rendered, radii, out_color, nullptr, nullptr, nullptr,
+                               stream);
 }
 
 int gsr_forward_render_l1(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
-                          const int32_t *radii, float *out_color, const float *gt, float *loss_out, void *stream) {
+                          const int32_t *radii, float *out_color, const float *gt, float *loss_out,
+                          uint8_t *visible_out, void *stream) {
     if (!gt) return fail(GSR_ERR_ARGS, "gt is NULL");
-    return forward_render_impl(in, geom, binning, img, num_rendered, radii, out_color, gt, loss_out, stream);
+    if (visible_out && !(in && (in->flags & GSR_FLAG_PREPARE_BACKWARD)))
+        return fail(GSR_ERR_ARGS, "visible_out needs GSR_FLAG_PREPARE_BACKWARD");
+    if (visible_out && !radii && in->P > 0) return fail(GSR_ERR_ARGS, "visible_out needs radii");
+    return forward_render_impl(in, geom, binning, img, num_rendered, radii, out_color, gt, loss_out, visible_out,
+                               stream);
 }
 
 static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,

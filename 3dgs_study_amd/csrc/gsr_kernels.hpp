@@ -29,10 +29,12 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
 
 // render_bwd.hip
 // l1 (forward only, or NULL): {image, gt, n} whose L1 partial sums (gsr_l1.hpp) the
-// same launch writes into img's l1_part; returns their count in *l1_nb
+// same launch writes into img's l1_part; returns their count in *l1_nb.  visible
+// (forward only, or NULL): visible[i] = radii[i] > 0 in the same launch.
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
                               bool internal, bool forward, hipStream_t s, const float *l1_x = nullptr,
-                              const float *l1_y = nullptr, int *l1_nb = nullptr);
+                              const float *l1_y = nullptr, int *l1_nb = nullptr, const int32_t *radii = nullptr,
+                              uint8_t *visible = nullptr);
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
                              const void *img, const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s);
 

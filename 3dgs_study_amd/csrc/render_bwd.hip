@@ -381,10 +381,22 @@ struct BwdPrepArgs {
     const float *l1_x, *l1_y;
     size_t l1_n;
     float *l1_part;
+    // ... and workgroups after those write visible[i] = radii[i] > 0 (render()'s
+    // visibility_filter), or NULL
+    const int32_t *radii;
+    uint8_t *visible;
+    int P, vis_nb;
 };
 constexpr int PREP_THREADS = 256;
 static_assert(PREP_THREADS == L1_THREADS, "the L1 partial blocks share the launch");
 __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a) {
+    if ((int)blockIdx.x >= a.file_blocks + a.l1_nb) {  // workgroup-uniform: a visibility block
+        const int v = ((int)blockIdx.x - a.file_blocks - a.l1_nb) * PREP_THREADS * 4 + (int)threadIdx.x * 4;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (v + k < a.P) a.visible[v + k] = a.radii[v + k] > 0 ? 1 : 0;
+        return;
+    }
     if ((int)blockIdx.x >= a.file_blocks) {  // workgroup-uniform: an L1 partial-sum block
         l1_block_partial(a.l1_x, a.l1_y, a.l1_n, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_part);
         return;
@@ -429,7 +441,7 @@ __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a
 
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
                               bool internal, bool forward, hipStream_t s, const float *l1_x, const float *l1_y,
-                              int *l1_nb) {
+                              int *l1_nb, const int32_t *radii, uint8_t *visible) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -452,7 +464,11 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
     a.l1_nb = l1_x ? l1_blocks(a.l1_n) : 0;
     a.l1_part = l1_x ? at<float>(const_cast<void *>(img), Im.l1_part) : nullptr;
     if (l1_nb) *l1_nb = a.l1_nb;
-    hipLaunchKernelGGL(bwd_prepare_kernel, dim3(blocks + a.l1_nb), dim3(PREP_THREADS), 0, s, a);
+    a.radii = radii;
+    a.visible = visible;
+    a.P = in.P;
+    a.vis_nb = visible ? (in.P + PREP_THREADS * 4 - 1) / (PREP_THREADS * 4) : 0;
+    hipLaunchKernelGGL(bwd_prepare_kernel, dim3(blocks + a.l1_nb + a.vis_nb), dim3(PREP_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

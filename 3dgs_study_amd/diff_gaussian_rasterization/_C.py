@@ -191,7 +191,7 @@ def load_library():
     lib.gsr_forward_preprocess.restype = ctypes.c_int
     lib.gsr_forward_render.argtypes = [pin, vp, vp, vp, i64, vp, vp, vp]
     lib.gsr_forward_render.restype = ctypes.c_int
-    lib.gsr_forward_render_l1.argtypes = [pin, vp, vp, vp, i64, vp, vp, vp, vp, vp]
+    lib.gsr_forward_render_l1.argtypes = [pin, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
     lib.gsr_forward_render_l1.restype = ctypes.c_int
     lib.gsr_backward.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward.restype = ctypes.c_int
@@ -387,7 +387,9 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
     ``sh`` = _features_dc and ``sh_rest`` = _features_rest instead of their cat, and
     the ACT_* bits of the opacity / scale / rotation inputs the library activates.
     ``l1_target`` (not upstream; gsr_forward_render_l1): also the L1 loss
-    mean|color - l1_target|, appended to the result as a 0-dim tensor."""
+    mean|color - l1_target|, appended to the result as a 0-dim tensor, and the
+    visibility ``radii > 0`` (bool [P]) after it — from the backward preparation's
+    launch when ``prepare_backward``, else computed here."""
     lib = load_library()
     H, W = int(image_height), int(image_width)
     if footprint is not None and footprint not in FOOTPRINTS:
@@ -415,10 +417,14 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
     if gt is None or gt.shape != (3, H, W):
         raise RuntimeError(f"l1_target must be a float32 [3,{H},{W}] tensor on {device}")
     loss = torch.empty(3, dtype=torch.float32, device=device)
+    vis = torch.empty(P, dtype=torch.bool, device=device) if prepare_backward and P > 0 else None
     _check(lib.gsr_forward_render_l1(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
                                      num_rendered.value, _ptr(radii), out_color.data_ptr(), gt.data_ptr(),
-                                     loss.data_ptr(), stream), "rasterize_gaussians (render + L1)")
-    return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M), loss[0]
+                                     loss.data_ptr(), None if vis is None else vis.data_ptr(), stream),
+           "rasterize_gaussians (render + L1)")
+    if vis is None:
+        vis = radii > 0
+    return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M), loss[0], vis
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,

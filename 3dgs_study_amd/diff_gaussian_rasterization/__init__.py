@@ -402,15 +402,18 @@ class _RasterizeModel(torch.autograd.Function):
         l1 = l1_target is not None
         ctx.l1 = l1
         loss = (res[7] if fwd_l1 else _C.l1_loss(color, l1_target)) if l1 else None
+        visible = (res[8] if fwd_l1 else radii > 0) if l1 else None
         ctx.save_for_backward(means3D, features_dc, features_rest, opacity, scaling, rotation, radii, geom, binning,
                               img, *copies.values(), *((color, l1_target) if l1 else ()))
         ctx.mark_non_differentiable(radii)
+        if l1:
+            ctx.mark_non_differentiable(visible)
         # radii never carry a gradient: no zero int32 [P] tensor materialised per backward
         ctx.set_materialize_grads(False)
-        return (color, radii, loss) if l1 else (color, radii)
+        return (color, radii, loss, visible) if l1 else (color, radii)
 
     @staticmethod
-    def backward(ctx, grad_out_color, _grad_radii, grad_loss=None):
+    def backward(ctx, grad_out_color, _grad_radii, grad_loss=None, _grad_visible=None):
         rs = ctx.raster_settings
         saved = ctx.saved_tensors
         s, device, M, present, copy_names = ctx.inputs
@@ -506,10 +509,12 @@ def rasterize_model(means3D, means2D, features_dc, features_rest, opacity, scali
     the activation kernels, their backwards or the cat's slice copies.
     ``means2D`` is the screen-space gradient carrier, as upstream.
     ``l1_target`` (a [3,H,W] float32 image, or None): also return the L1 loss
-    mean|image - target| (utils/loss_utils.py l1_loss, train.py:102) as a third
-    output; when the image feeds nothing but that loss, the backward forms the loss's
-    pixel gradient inside the render backward (no gradient map, no separate loss
-    node or kernel).  Values equal ``l1_loss(image, target)`` and its backward."""
+    mean|image - target| (utils/loss_utils.py l1_loss, train.py:102) and render()'s
+    ``visibility_filter`` (radii > 0, bool [P]) as a third and fourth output —
+    both computed in the backward preparation's launch; when the image feeds nothing
+    but that loss, the backward forms the loss's pixel gradient inside the render
+    backward (no gradient map, no separate loss node or kernel).  Values equal
+    ``l1_loss(image, target)``, ``radii > 0`` and the L1 backward."""
     return _RasterizeModel.apply(means3D, means2D, features_dc, features_rest, opacity, scaling, rotation,
                                  raster_settings, torch.is_grad_enabled(), l1_target)
 

@@ -148,8 +148,8 @@ def render_fused(viewpoint_camera, pc, bg_color: torch.Tensor, scaling_modifier:
         campos=viewpoint_camera.camera_center, prefiltered=False, debug=debug)
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
     res = rasterizer.forward_model(xyz, screenspace_points, f_dc, f_rest, opacity, scaling, rotation, l1_target)
-    out = {"render": res[0], "viewspace_points": screenspace_points, "visibility_filter": res[1] > 0,
-           "radii": res[1]}
+    out = {"render": res[0], "viewspace_points": screenspace_points,
+           "visibility_filter": res[3] if l1_target is not None else res[1] > 0, "radii": res[1]}
     if l1_target is not None:
         out["l1"] = res[2]
     return out

@@ -174,10 +174,14 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
  * l1_loss, train.py:102; not upstream) into loss_out [3] = {loss, loss, 0}
  * (gsr_l1_ssim's layout with lambda 0, the same bits).  With
  * GSR_FLAG_PREPARE_BACKWARD the loss's partial sums are computed in the same
- * launch as the backward's preparation.  gt is [3,H,W] float32; img is required.
- * The backward's GSR_FLAG_L1_SEED (above) is its gradient. */
+ * launch as the backward's preparation, and so, when visible_out is not NULL, is
+ * visible_out [P] bytes = radii > 0 (render()'s visibility_filter,
+ * gaussian_renderer/__init__.py; visible_out requires the flag).  gt is [3,H,W]
+ * float32; img is required.  The backward's GSR_FLAG_L1_SEED (above) is its
+ * gradient. */
 int gsr_forward_render_l1(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
-                          const int32_t *radii, float *out_color, const float *gt, float *loss_out, void *stream);
+                          const int32_t *radii, float *out_color, const float *gt, float *loss_out,
+                          uint8_t *visible_out, void *stream);
 
 /* Replaces RasterizeGaussiansBackwardCUDA -> Rasterizer::backward.
  * accum: NULL = the accumulator inside geom (zeroed by a forward called with

@@ -215,12 +215,14 @@ def test_l1_seed_flag_validates(lib):
 def test_forward_render_l1_validates(lib):
     """gsr_forward_render_l1: gt, loss_out and img required (host-side checks)."""
     s = _inputs()
-    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, 1, 0, 1, 1, None, 1, None) != 0
+    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, 1, 0, 1, 1, None, 1, None, None) != 0
     assert "gt is NULL" in lib.gsr_last_error().decode()
-    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, None, 0, 1, 1, 1, 1, None) != 0
+    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, None, 0, 1, 1, 1, 1, None, None) != 0
     assert "loss_out and img required" in lib.gsr_last_error().decode()
-    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, 1, 0, 1, 1, 1, None, None) != 0
+    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, 1, 0, 1, 1, 1, None, None, None) != 0
     assert "loss_out and img required" in lib.gsr_last_error().decode()
+    assert lib.gsr_forward_render_l1(ctypes.byref(s), 1, 1, 1, 0, 1, 1, 1, 1, 1, None) != 0  # visible, no flag
+    assert "needs GSR_FLAG_PREPARE_BACKWARD" in lib.gsr_last_error().decode()
 
 
 def test_l1_grad_validates(lib):

@@ -283,6 +283,8 @@ def test_rasterizer_l1_loss_bits(dev, grad):
     ref = train_ops.l1_ssim_loss(out["render"].detach(), gt, 0.0)
     torch.cuda.synchronize()
     assert torch.equal(out["l1"].detach(), ref)
+    vis = out["visibility_filter"]
+    assert vis.dtype == torch.bool and torch.equal(vis, out["radii"] > 0) and int(vis.sum()) > 0
     cam0 = synthetic.make_camera(64, 48, view=0).to(dev)
     gt0 = gt[:, :48, :64].contiguous()
     z3, z1, z4 = (torch.zeros(0, k, device=dev) for k in (3, 1, 4))
