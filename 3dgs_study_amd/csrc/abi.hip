@@ -277,9 +277,11 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
     g_pinned[CTRL_DSORT_PASSES] = 0;
-    // The depth sort needs only the view depths.  By default it runs in line, before
-    // preprocess; with GSR_SIDE_STREAM=1 on the library's second stream beside
-    // preprocess (debug mode: always in line, every kernel checked on one stream).
+    // The depth sort needs only the view depths.  By default it runs in line, after
+    // preprocess, and its first digit scan also publishes num_rendered (one launch
+    // fewer than a publish kernel of its own); with GSR_SIDE_STREAM=1 it runs on the
+    // library's second stream beside preprocess (debug mode: always in line, every
+    // kernel checked on one stream).
     SideStream *side = nullptr;
     if (!dbg)
         if (int rc = side_stream(s, &side)) return rc;
@@ -292,11 +294,21 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     // in line, the host reads the published pass count after its sync and runs a
     // fourth pass only when the keys need it; on the second stream all four are queued
     uint32_t *pass_word = side ? nullptr : (uint32_t *)g_pinned;
-    if (int rc = step(timed(sort_stage, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, pass_word, ds); }), "depth sort", dbg, ds))
-        return rc;
+#ifdef GSR_SORT_FIRST  // A/B builds: the sort before preprocess, a publish kernel of its own
+    const bool after = false;
+#else
+    const bool after = side == nullptr;
+#endif
+    auto sort = [&] {
+        return step(timed(sort_stage, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, pass_word, ds, after ? g_pinned : nullptr); }), "depth sort", dbg, ds);
+    };
+    if (!after)
+        if (int rc = sort()) return rc;
     if (side)
         if (int rc = check_hip(hipEventRecord(side->join, ds), "join")) return rc;
-    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s); }), "preprocess", dbg, s)) return rc;
+    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s, !after); }), "preprocess", dbg, s)) return rc;
+    if (after)
+        if (int rc = sort()) return rc;
     if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
     // concurrent mode: the sort's exposed part, the launch stream's wait for its stream
     if (side)

@@ -45,6 +45,7 @@
 
 #include "gsr_kernels.hpp"
 #include "gsr_math.hpp"
+#include "gsr_publish.hpp"
 #include "gsr_wave.hpp"
 
 #include <type_traits>
@@ -117,6 +118,11 @@ struct RadixPass {
     // (zeroed by depth_keys_kernel); no digit-scan launch.  NULL otherwise.
     uint32_t *sup;
     int nsup;
+    // first depth pass after preprocess: one more digit-scan workgroup publishes
+    // num_rendered (gsr_publish.hpp) from preprocess's block sums; NULL otherwise
+    const uint4 *pub_sums;
+    int pub_n;
+    uint32_t *pub_ctrl, *pub_host;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
@@ -291,8 +297,13 @@ __global__ void __launch_bounds__(RX_THREADS) radix_upsweep_kernel(RadixPass a) 
 // 14.8k block counts: 27.7 us each as one block scan per 256 entries, 8.2 us like
 // this (256 x 16: 9.9, 512 x 8: 9.0, 1024 x 4: 8.8).
 constexpr int DSCAN_THREADS = 1024, DSCAN_PER = 16;
+static_assert(DSCAN_THREADS == TOTAL_THREADS, "the publish workgroup runs in the digit scan's launch");
 __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPass a) {
     __shared__ uint32_t wsum[DSCAN_THREADS / 64];
+    if (blockIdx.x == RADIX + 1) {  // (grid RADIX + 2 only with pub_sums)
+        publish_total(a.pub_sums, a.pub_n, a.pub_ctrl, a.pub_host);
+        return;
+    }
     if (blockIdx.x == RADIX) {  // first depth pass: one more workgroup reduces the candidate key range
         __shared__ uint32_t wmin[DSCAN_THREADS / 64], wmax[DSCAN_THREADS / 64];
         uint32_t kmin = 0xffffffffu, kmax = 0u;
@@ -536,7 +547,8 @@ static hipError_t radix_pass(const RadixPass &a, hipStream_t s, bool counted = f
     // counted: the digit counts are already in a.hist (depth_keys_kernel)
     if (!counted) hipLaunchKernelGGL((radix_upsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     if (!a.sup)  // grouped depth passes: each downsweep block sums its own prefix
-        hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(a.minmax ? RADIX + 1 : RADIX), dim3(DSCAN_THREADS), 0, s, a);
+        hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(a.pub_sums ? RADIX + 2 : a.minmax ? RADIX + 1 : RADIX),
+                           dim3(DSCAN_THREADS), 0, s, a);
     hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     return hipGetLastError();
 }
@@ -927,7 +939,7 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
 
 template <int ITEMS>
 static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                                   uint32_t *host_ctrl, hipStream_t s) {
+                                   uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl) {
     const GeomLayout L = geom_layout(P, W, H);
     DepthKeyArgs k;
     k.means3D = means3D;
@@ -945,7 +957,15 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     // it — three early-returning launches (~14 us at config C) saved in the common case
     for (int p = 0; p < (host_ctrl ? 3 : 4); p++) {
         RadixPass a = depth_pass(P, W, H, geom, p);
-        if (p == 0) a.host_ctrl = host_ctrl;
+        if (p == 0) {
+            a.host_ctrl = host_ctrl;
+            if (publish_ctrl) {
+                a.pub_sums = at<const uint4>(geom, L.block_sums);
+                a.pub_n = pre_blocks(P);
+                a.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+                a.pub_host = publish_ctrl;
+            }
+        }
         hipError_t e = radix_pass<ITEMS>(a, s, p == 0);
         if (e != hipSuccess) return e;
     }
@@ -953,11 +973,11 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
 }
 
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             uint32_t *host_ctrl, hipStream_t s) {
+                             uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl) {
     if (P <= 0) return hipSuccess;
     return dsort_items(P) == DSORT_ITEMS_BIG
-               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s)
-               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s);
+               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s, publish_ctrl)
+               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s, publish_ctrl);
 }
 
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s) {

@@ -1,0 +1,60 @@
+// gsr_publish.hpp — num_rendered from the preprocess workgroups' instance sums,
+// published into the geom control words and the caller's pinned host words.  One
+// 1024-thread workgroup: publish_total_kernel (preprocess.hip), or one extra
+// workgroup of the depth sort's first digit scan (binning.hip) when the sort runs
+// after preprocess in line — one launch fewer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace gsr {
+
+constexpr int TOTAL_THREADS = 1024;
+__device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t *ctrl, uint32_t *host_ctrl) {
+    __shared__ unsigned long long part[TOTAL_THREADS / 64];
+    __shared__ uint32_t perr[TOTAL_THREADS / 64];
+    unsigned long long t = 0;
+    uint32_t e = 0;
+    // 8 loads in flight per thread (one at a time: 12 us for config E's 19.5k
+    // workgroup records, on the host's critical path)
+    constexpr int U = 8;
+    for (int i0 = threadIdx.x; i0 < n; i0 += TOTAL_THREADS * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const int i = i0 + j * TOTAL_THREADS;
+            v[j] = i < n ? sums[i] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            t += v[j].x & 0x7fffffffu;
+            e |= v[j].x >> 31;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        t += __shfl_xor(t, o);
+        e |= __shfl_xor(e, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[threadIdx.x >> 6] = t;
+        perr[threadIdx.x >> 6] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < TOTAL_THREADS / 64; k++) {
+            t += part[k];
+            e |= perr[k];
+        }
+        const uint32_t w[3] = {(uint32_t)t, (uint32_t)(t >> 32), e};
+        for (int k = 0; k < 3; k++) {
+            ctrl[k] = w[k];
+            __hip_atomic_store(&host_ctrl[k], w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __threadfence_system();
+    }
+}
+
+}  // namespace gsr

@@ -13,6 +13,7 @@
 #include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
 #include "gsr_math.hpp"
+#include "gsr_publish.hpp"
 #include "gsr_rows.hpp"
 #include "gsr_wave.hpp"
 
@@ -296,51 +297,9 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
 // One workgroup totals the block sums and publishes num_rendered and the error
 // flag into the geom control words and, with system-scope stores, straight into
 // the caller's pinned host words (no copy; the host waits for this kernel's event).
-constexpr int TOTAL_THREADS = 1024;
 __global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint4 *sums, int n, uint32_t *ctrl,
                                                                       uint32_t *host_ctrl) {
-    __shared__ unsigned long long part[TOTAL_THREADS / 64];
-    __shared__ uint32_t perr[TOTAL_THREADS / 64];
-    unsigned long long t = 0;
-    uint32_t e = 0;
-    // 8 loads in flight per thread (one at a time: 12 us for config E's 19.5k
-    // workgroup records, on the host's critical path)
-    constexpr int U = 8;
-    for (int i0 = threadIdx.x; i0 < n; i0 += TOTAL_THREADS * U) {
-        uint4 v[U];
-#pragma unroll
-        for (int j = 0; j < U; j++) {
-            const int i = i0 + j * TOTAL_THREADS;
-            v[j] = i < n ? sums[i] : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int j = 0; j < U; j++) {
-            t += v[j].x & 0x7fffffffu;
-            e |= v[j].x >> 31;
-        }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        t += __shfl_xor(t, o);
-        e |= __shfl_xor(e, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        part[threadIdx.x >> 6] = t;
-        perr[threadIdx.x >> 6] = e;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < TOTAL_THREADS / 64; k++) {
-            t += part[k];
-            e |= perr[k];
-        }
-        const uint32_t w[3] = {(uint32_t)t, (uint32_t)(t >> 32), e};
-        for (int k = 0; k < 3; k++) {
-            ctrl[k] = w[k];
-            __hip_atomic_store(&host_ctrl[k], w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        __threadfence_system();
-    }
+    publish_total(sums, n, ctrl, host_ctrl);
 }
 
 // auxiliary.h in_frustum via checkFrustum (markVisible).
@@ -353,7 +312,8 @@ __global__ void mark_visible_kernel(int P, const float *means3D, const float *vi
     present[idx] = !(pv.z <= 0.2f);
 }
 
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, uint32_t *host_ctrl, hipStream_t s) {
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, uint32_t *host_ctrl, hipStream_t s,
+                             bool publish) {
     const GeomLayout L = geom_layout(in.P, in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
     PreArgs a;
@@ -390,8 +350,9 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
         split ? go(preprocess_fwd_kernel<48, true>) : go(preprocess_fwd_kernel<48, false>);
     else
         split ? go(preprocess_fwd_kernel<0, true>) : go(preprocess_fwd_kernel<0, false>);
-    hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint4 *)a.block_sums, nb,
-                       at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl);
+    if (publish)  // else the depth sort's first digit scan publishes (binning.hip)
+        hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint4 *)a.block_sums, nb,
+                           at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl);
     return hipGetLastError();
 }
 
