@@ -10,11 +10,11 @@
 //  1. depth sort  — stable LSD radix sort of the P depth bit patterns with the
 //                   index as value (3 passes over P when the keys span < 2^24,
 //                   else 4; not over I): order[rank] = id in (depth_bits, id)
-//                   order.  It needs only the view depths, so it runs on a second
-//                   stream beside preprocess (depth_keys_kernel computes the keys
-//                   and the first pass's digit counts itself) and preprocess's
-//                   bytes and the sort's launch-bound chain overlap.  Gaussians
-//                   that preprocess culls sort anywhere: they emit nothing.
+//                   order.  It needs only the view depths (depth_keys_kernel
+//                   computes the keys and the first pass's digit counts itself);
+//                   it runs right after preprocess, and its first digit scan also
+//                   publishes num_rendered (gsr_publish.hpp).  Gaussians that
+//                   preprocess culls sort anywhere: they emit nothing.
 //  2. rank scan   — the tile rects gathered in rank order (rank_gather_kernel),
 //                   instances per emit block, an exclusive scan of those.
 //  3. emit        — each Gaussian, in rank order, writes (tile, id) for every
@@ -32,8 +32,8 @@
 //  5. ranges      — from the second pass's per-block digit counts (two-pass
 //                   case), else identifyTileRanges on the sorted tile keys.
 //
-// Steps 1-2 run in gsr_forward_preprocess (step 2 once both streams are done),
-// 3-5 in gsr_forward_render once the caller has sized the binning buffer.
+// Steps 1-2 run in gsr_forward_preprocess, 3-5 in gsr_forward_render once the
+// caller has sized the binning buffer.
 //
 // One radix pass = upsweep (per-block digit histogram), digit scan (one
 // workgroup per digit over the blocks), downsweep (stable scatter).  Inside a
@@ -896,10 +896,11 @@ __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) 
 }
 
 // ------------------------------------------------------------ launchers
-// The depth sort runs on its own stream beside preprocess (abi.hip forks it):
-// depth_keys_kernel, then passes 1-3 and the fourth pass, whose kernels return at
-// once unless the key range needs it (decided on the device from the first digit
-// scan's control words).  The order lands in GSR_GEOM_DEPTH_ORDER either way.
+// The depth sort: depth_keys_kernel, then passes 1-3; the fourth pass is launched
+// by the host after its sync when the published pass count needs it (in line), or
+// queued with kernels that return at once unless the key range needs it (on the
+// opt-in second stream, GSR_SIDE_STREAM=1).  The order lands in
+// GSR_GEOM_DEPTH_ORDER either way.
 static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     const GeomLayout L = geom_layout(P, W, H);
     RadixPass a = {};
