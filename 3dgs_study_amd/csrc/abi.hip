@@ -7,6 +7,8 @@
 // here: every buffer belongs to the caller (torch's caching allocator on the
 // Python side).  The only host synchronisation is the num_rendered read-back
 // in gsr_forward_preprocess, as upstream.
+#include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -51,6 +53,7 @@ bool prepared_take(const void *geom) {
 }
 // pinned words: num_rendered lo / hi, prefiltered error
 thread_local hipEvent_t g_ctrl_ready = nullptr;
+thread_local uint32_t g_seq = 0;  // forward sequence number the publish stores last (CTRL_SEQ)
 
 // Per host thread and device: the depth sort's own stream (highest priority: its
 // chain of short launches is the longer path) beside the caller's, and the fork /
@@ -277,6 +280,7 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
     g_pinned[CTRL_DSORT_PASSES] = 0;
+    const uint32_t seq = ++g_seq ? g_seq : ++g_seq;  // never 0 (the pinned word's initial value)
     // The depth sort needs only the view depths.  By default it runs in line, after
     // preprocess, and its first digit scan also publishes num_rendered (one launch
     // fewer than a publish kernel of its own); with GSR_SIDE_STREAM=1 it runs on the
@@ -300,16 +304,18 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     const bool after = side == nullptr;
 #endif
     auto sort = [&] {
-        return step(timed(sort_stage, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, pass_word, ds, after ? g_pinned : nullptr); }), "depth sort", dbg, ds);
+        return step(timed(sort_stage, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, pass_word, ds, after ? g_pinned : nullptr, seq); }), "depth sort", dbg, ds);
     };
     if (!after)
         if (int rc = sort()) return rc;
     if (side)
         if (int rc = check_hip(hipEventRecord(side->join, ds), "join")) return rc;
-    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s, !after); }), "preprocess", dbg, s)) return rc;
+    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s, !after, seq); }), "preprocess", dbg, s)) return rc;
     if (after)
         if (int rc = sort()) return rc;
+#ifdef GSR_EVENT_SYNC  // A/B builds: wait on an event instead of polling the pinned words
     if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
+#endif
     // concurrent mode: the sort's exposed part, the launch stream's wait for its stream
     if (side)
         if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] { return hipStreamWaitEvent(s, side->join, 0); }), "join", dbg, s))
@@ -319,7 +325,28 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, !side, s); }),
                       "rank gather", dbg, s))
         return rc;
+#ifdef GSR_EVENT_SYNC
     if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;
+#else
+    // Poll the pinned words: the publish stores num_rendered, then this forward's
+    // sequence number; the first digit scan the pass count (in line).  No event in
+    // the stream (its barrier packet left a ~6 us gap before the next kernel).  A
+    // device that never publishes (a faulted kernel) is caught by a stream sync
+    // after a second of polling.
+    {
+        volatile uint32_t *pw = g_pinned;
+        auto ready = [&] { return pw[CTRL_SEQ] == seq && (side || pw[CTRL_DSORT_PASSES] != 0u); };
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0; !ready(); spin++) {
+            if ((spin & 4095u) == 4095u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+                if (int rc = check_hip(hipStreamSynchronize(s), "num_rendered read-back")) return rc;
+                if (!ready()) return fail(GSR_ERR_HIP, "num_rendered was not published");
+                break;
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+#endif
     if (g_pinned[CTRL_PREFILTER_ERR])
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (!side && g_pinned[CTRL_DSORT_PASSES] != 3u) {

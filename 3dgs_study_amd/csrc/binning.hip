@@ -123,6 +123,7 @@ struct RadixPass {
     const uint4 *pub_sums;
     int pub_n;
     uint32_t *pub_ctrl, *pub_host;
+    uint32_t pub_seq;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
@@ -301,7 +302,7 @@ static_assert(DSCAN_THREADS == TOTAL_THREADS, "the publish workgroup runs in the
 __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPass a) {
     __shared__ uint32_t wsum[DSCAN_THREADS / 64];
     if (blockIdx.x == RADIX + 1) {  // (grid RADIX + 2 only with pub_sums)
-        publish_total(a.pub_sums, a.pub_n, a.pub_ctrl, a.pub_host);
+        publish_total(a.pub_sums, a.pub_n, a.pub_ctrl, a.pub_host, a.pub_seq);
         return;
     }
     if (blockIdx.x == RADIX) {  // first depth pass: one more workgroup reduces the candidate key range
@@ -940,7 +941,7 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
 
 template <int ITEMS>
 static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                                   uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl) {
+                                   uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl, uint32_t seq) {
     const GeomLayout L = geom_layout(P, W, H);
     DepthKeyArgs k;
     k.means3D = means3D;
@@ -965,6 +966,7 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
                 a.pub_n = pre_blocks(P);
                 a.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
                 a.pub_host = publish_ctrl;
+                a.pub_seq = seq;
             }
         }
         hipError_t e = radix_pass<ITEMS>(a, s, p == 0);
@@ -974,11 +976,11 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
 }
 
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl) {
+                             uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl, uint32_t seq) {
     if (P <= 0) return hipSuccess;
     return dsort_items(P) == DSORT_ITEMS_BIG
-               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s, publish_ctrl)
-               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s, publish_ctrl);
+               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s, publish_ctrl, seq)
+               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s, publish_ctrl, seq);
 }
 
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s) {

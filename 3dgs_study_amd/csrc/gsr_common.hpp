@@ -116,6 +116,7 @@ enum CtrlWord {
     CTRL_PREFILTER_ERR = 2,
     CTRL_DSORT_PASSES = 3,  // host copy only: the depth sort's pass count (its first digit scan publishes it)
     CTRL_SHJAC = 4,         // device only: 1 when this forward's preprocess stored the SH direction Jacobian
+    CTRL_SEQ = 5,           // host copy only: the forward's sequence number, stored after the words above
     CTRL_WORDS = 16
 };
 // the depth sort's own control words (GeomLayout::dsort_ctrl, a line of their own:

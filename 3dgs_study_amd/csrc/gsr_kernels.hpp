@@ -11,7 +11,7 @@ namespace gsr {
 // publish: num_rendered from publish_total_kernel (false: the depth sort's first
 // digit scan publishes it — launch_depth_sort with publish_ctrl, after preprocess)
 hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, uint32_t *host_ctrl, hipStream_t s,
-                             bool publish = true);
+                             bool publish = true, uint32_t seq = 0);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 
@@ -19,7 +19,7 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 // publish_ctrl (or NULL): the sort runs after preprocess and its first digit scan
 // also publishes num_rendered into these pinned words (launch_preprocess publish = false)
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl = nullptr);
+                             uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl = nullptr, uint32_t seq = 0);
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s);
 hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hipStream_t s);
 hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,

@@ -9,10 +9,14 @@
 
 #include <cstdint>
 
+#include "gsr_common.hpp"
+
 namespace gsr {
 
 constexpr int TOTAL_THREADS = 1024;
-__device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t *ctrl, uint32_t *host_ctrl) {
+// seq: stored into host_ctrl[CTRL_SEQ] after the other words (the host polls it)
+__device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t *ctrl, uint32_t *host_ctrl,
+                                              uint32_t seq) {
     __shared__ unsigned long long part[TOTAL_THREADS / 64];
     __shared__ uint32_t perr[TOTAL_THREADS / 64];
     unsigned long long t = 0;
@@ -53,6 +57,8 @@ __device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t
             ctrl[k] = w[k];
             __hip_atomic_store(&host_ctrl[k], w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        __threadfence_system();
+        __hip_atomic_store(&host_ctrl[CTRL_SEQ], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __threadfence_system();
     }
 }

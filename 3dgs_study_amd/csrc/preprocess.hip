@@ -298,8 +298,8 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
 // flag into the geom control words and, with system-scope stores, straight into
 // the caller's pinned host words (no copy; the host waits for this kernel's event).
 __global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint4 *sums, int n, uint32_t *ctrl,
-                                                                      uint32_t *host_ctrl) {
-    publish_total(sums, n, ctrl, host_ctrl);
+                                                                      uint32_t *host_ctrl, uint32_t seq) {
+    publish_total(sums, n, ctrl, host_ctrl, seq);
 }
 
 // auxiliary.h in_frustum via checkFrustum (markVisible).
@@ -313,7 +313,7 @@ __global__ void mark_visible_kernel(int P, const float *means3D, const float *vi
 }
 
 hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, uint32_t *host_ctrl, hipStream_t s,
-                             bool publish) {
+                             bool publish, uint32_t seq) {
     const GeomLayout L = geom_layout(in.P, in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
     PreArgs a;
@@ -352,7 +352,7 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
         split ? go(preprocess_fwd_kernel<0, true>) : go(preprocess_fwd_kernel<0, false>);
     if (publish)  // else the depth sort's first digit scan publishes (binning.hip)
         hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint4 *)a.block_sums, nb,
-                           at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl);
+                           at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl, seq);
     return hipGetLastError();
 }
 
