@@ -338,6 +338,7 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
         auto ready = [&] { return pw[CTRL_SEQ] == seq && (side || pw[CTRL_DSORT_PASSES] != 0u); };
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 0; !ready(); spin++) {
+            __builtin_ia32_pause();  // a polite spin for the core's other hardware thread
             if ((spin & 4095u) == 4095u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
                 if (int rc = check_hip(hipStreamSynchronize(s), "num_rendered read-back")) return rc;
                 if (!ready()) return fail(GSR_ERR_HIP, "num_rendered was not published");
