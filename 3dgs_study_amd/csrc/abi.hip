@@ -313,7 +313,7 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s, !after, seq); }), "preprocess", dbg, s)) return rc;
     if (after)
         if (int rc = sort()) return rc;
-#ifdef GSR_EVENT_SYNC  // A/B builds: wait on an event instead of polling the pinned words
+#ifndef GSR_POLL_SYNC  // the default: an event after the publish (GSR_POLL_SYNC builds poll the pinned words)
     if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
 #endif
     // concurrent mode: the sort's exposed part, the launch stream's wait for its stream
@@ -325,14 +325,16 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, !side, s); }),
                       "rank gather", dbg, s))
         return rc;
-#ifdef GSR_EVENT_SYNC
+#ifndef GSR_POLL_SYNC
     if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;
 #else
     // Poll the pinned words: the publish stores num_rendered, then this forward's
     // sequence number; the first digit scan the pass count (in line).  No event in
     // the stream (its barrier packet left a ~6 us gap before the next kernel).  A
     // device that never publishes (a faulted kernel) is caught by a stream sync
-    // after a second of polling.
+    // after a second of polling.  Not the default: +1 % in alternating A/B runs,
+    // but two of two round profiles with it had one benchmark segment 1.2-1.8x
+    // slower than every run with the event.
     {
         volatile uint32_t *pw = g_pinned;
         auto ready = [&] { return pw[CTRL_SEQ] == seq && (side || pw[CTRL_DSORT_PASSES] != 0u); };
