@@ -7,8 +7,6 @@
 // here: every buffer belongs to the caller (torch's caching allocator on the
 // Python side).  The only host synchronisation is the num_rendered read-back
 // in gsr_forward_preprocess, as upstream.
-#include <atomic>
-#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -51,22 +49,15 @@ bool prepared_take(const void *geom) {
     std::lock_guard<std::mutex> lk(g_prep_mu);
     return g_prepared.erase(geom) != 0;
 }
-// pinned words: num_rendered lo / hi, prefiltered error
+// the num_rendered read-back's event (per host thread, like g_pinned): timing off
+// and no system-scope fence — the pinned words are written with system-scope stores
+// already, and a fenced event's cache writeback / invalidate opened a ~6 us idle gap
+// before the next kernel (round 4 profile, before rank_gather_kernel)
 thread_local hipEvent_t g_ctrl_ready = nullptr;
-thread_local uint32_t g_seq = 0;  // forward sequence number the publish stores last (CTRL_SEQ)
-
-// Per host thread and device: the depth sort's own stream (highest priority: its
-// chain of short launches is the longer path) beside the caller's, and the fork /
-// join events (binning.hip: the sort needs only the view depths, so it overlaps
-// preprocess).  Events are reused call after call: a call's record / wait pairs are
-// enqueued in order, so a wait always sees this call's record.
-struct SideStream {
-    int device = -1;
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-constexpr int MAX_DEVICES = 64;
-thread_local SideStream g_side[MAX_DEVICES];
+// the last forward's depth-sort pass count (per host thread): 4 queues the fourth
+// pass up front (it returns at once when three suffice), so a scene whose depths
+// span more than 2^24 key steps keeps gsr_forward's speculation
+thread_local bool g_four_hint = false;
 
 int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -96,10 +87,9 @@ struct StageTimer {
 StageTimer g_timer;  // the ABI is driven from one host thread per process
 size_t g_open[GSR_STAGE_COUNT];  // gsr_timing_begin: the pool slot whose end event is pending, + 1
 
-const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess",     "scan",        "depth_sort",           "duplicate",
-                                            "tile_sort",      "render_fwd",  "render_bwd",           "preprocess_bwd",
-                                            "bwd_prepare",    "depth_sort_concurrent", "exchange_wait",
-                                            "sh_rebuild"};
+const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess", "scan",           "depth_sort",  "duplicate",
+                                            "tile_sort",  "render_fwd",     "render_bwd",  "preprocess_bwd",
+                                            "bwd_prepare", "exchange_wait", "sh_rebuild"};
 
 // st | TIMED_MORE: more work of a stage already counted once in this step (its
 // time is added, its launch count is not)
@@ -137,43 +127,6 @@ hipError_t timed(int st, hipStream_t s, F &&launch) {
 }
 
 // upstream debug mode: synchronise and check after every kernel
-int side_stream(hipStream_t main, SideStream **out) {
-    // Off by default (GSR_SIDE_STREAM=1 turns it on): the concurrent depth sort
-    // measured no faster than in line (1,014-1,028 vs 1,020 it/s at C), and once the
-    // process holds an eagerly initialised RCCL communicator (init_process_group with
-    // device_id) any second stream of ours took the whole step from 0.98 to 2.2-2.4 ms
-    // (DESIGN §9, round 4): every kernel ran ~2x longer.
-    static const bool off = [] {
-        const char *e = getenv("GSR_SIDE_STREAM");
-        return !(e && e[0] == '1');
-    }();
-    if (off) {
-        *out = nullptr;
-        return GSR_OK;
-    }
-    int dev = 0;
-    if (int rc = check_hip(hipStreamGetDevice(main, &dev), "hipStreamGetDevice")) return rc;
-    if (dev < 0 || dev >= MAX_DEVICES) return fail(GSR_ERR_ARGS, "device %d out of range", dev);
-    SideStream &x = g_side[dev];
-    if (x.s == nullptr) {
-        int cur = 0;
-        hipError_t e = hipGetDevice(&cur);
-        if (e == hipSuccess && cur != dev) e = hipSetDevice(dev);
-        int least = 0, greatest = 0;
-        if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-        const char *pe = getenv("GSR_SIDE_PRIORITY");  // diagnostics: "normal" = the default priority
-        const bool hi = !(pe && pe[0] == 'n');
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, hi ? greatest : least);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&x.join, hipEventDisableTiming);
-        if (cur != dev) (void)hipSetDevice(cur);
-        if (int rc = check_hip(e, "depth-sort stream")) return rc;
-        x.device = dev;
-    }
-    *out = &x;
-    return GSR_OK;
-}
-
 int step(hipError_t e, const char *what, bool debug, hipStream_t s) {
     int rc = check_hip(e, what);
     if (rc || !debug) return rc;
@@ -265,7 +218,64 @@ static int ensure_pinned() {
     // coherent: the kernel's system-scope stores land in host memory directly
     if (int rc = check_hip(hipHostMalloc((void **)&g_pinned, CTRL_WORDS * 4, hipHostMallocCoherent), "hipHostMalloc"))
         return rc;
-    return check_hip(hipEventCreateWithFlags(&g_ctrl_ready, hipEventDisableTiming), "hipEventCreate");
+    return check_hip(hipEventCreateWithFlags(&g_ctrl_ready, hipEventDisableTiming | hipEventDisableSystemFence),
+                     "hipEventCreate");
+}
+
+// Preprocess, the depth sort (its first digit scan publishes num_rendered and the
+// pass count into the pinned words), the read-back event and the rank-order gather:
+// queued, not waited for.  passes: the depth passes queued (3, or 4 up front).
+static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int passes, hipStream_t s, bool dbg) {
+    prepared_set(geom, false);  // preprocess resets the device's flag words too
+    if (int rc = ensure_pinned()) return rc;
+    g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
+    g_pinned[CTRL_DSORT_PASSES] = 0;
+    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, s); }),
+                      "preprocess", dbg, s))
+        return rc;
+    // the sort needs only the view depths; after preprocess, so that its first digit
+    // scan can also publish num_rendered (one launch fewer than a publish kernel)
+    if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s,
+                            [&] {
+                                return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom,
+                                                         passes, g_pinned, s);
+                            }),
+                      "depth sort", dbg, s))
+        return rc;
+    if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
+    // the rects in rank order and the emission offsets (upstream's InclusiveSum of
+    // tiles_touched, in depth order), queued before the host waits: the device stays
+    // busy (with three passes queued it returns at once if the keys need four)
+    return step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, passes == 3, s); }),
+                "rank gather", dbg, s);
+}
+
+// The host's one wait: num_rendered and the pass count.  When only three depth
+// passes were queued and the keys need four, the fourth pass and the rank gather
+// are queued now (*late).
+static int finish_preprocess(const gsr_inputs *in, void *geom, int passes, hipStream_t s, bool dbg, int64_t *I,
+                             bool *late) {
+    if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;
+    if (g_pinned[CTRL_PREFILTER_ERR])
+        return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    const bool four = g_pinned[CTRL_DSORT_PASSES] != 3u;
+    g_four_hint = four;
+    *late = four && passes == 3;
+    if (*late) {
+        // the keys span more than 2^24: the fourth pass, then the rank gather the
+        // queued one skipped (rank_gather_kernel returns at once on a four-pass sort)
+        if (int rc = step(timed(GSR_STAGE_DEPTH_SORT | TIMED_MORE, s,
+                                [&] { return launch_depth_sort_fourth(in->P, in->W, in->H, geom, s); }),
+                          "depth sort (fourth pass)", dbg, s))
+            return rc;
+        if (int rc = step(timed(GSR_STAGE_SCAN | TIMED_MORE, s,
+                                [&] { return launch_rank_gather(in->P, in->W, in->H, geom, false, s); }),
+                          "rank gather", dbg, s))
+            return rc;
+    }
+    *I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
+    if (*I > 0xFFFFFFFFll) return fail(GSR_ERR_CAPACITY, "num_rendered %lld exceeds 32-bit list indexing", (long long)*I);
+    return GSR_OK;
 }
 
 int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered, void *stream) {
@@ -276,95 +286,80 @@ int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int
     if (!geom || !radii) return fail(GSR_ERR_ARGS, "geom/radii buffers are NULL");
     hipStream_t s = (hipStream_t)stream;
     const bool dbg = in->debug != 0;
-    prepared_set(geom, false);  // preprocess resets the device's flag words too
-    if (int rc = ensure_pinned()) return rc;
-    g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
-    g_pinned[CTRL_DSORT_PASSES] = 0;
-    const uint32_t seq = ++g_seq ? g_seq : ++g_seq;  // never 0 (the pinned word's initial value)
-    // The depth sort needs only the view depths.  By default it runs in line, after
-    // preprocess, and its first digit scan also publishes num_rendered (one launch
-    // fewer than a publish kernel of its own); with GSR_SIDE_STREAM=1 it runs on the
-    // library's second stream beside preprocess (debug mode: always in line, every
-    // kernel checked on one stream).
-    SideStream *side = nullptr;
-    if (!dbg)
-        if (int rc = side_stream(s, &side)) return rc;
-    hipStream_t ds = side ? side->s : s;
-    if (side) {
-        if (int rc = check_hip(hipEventRecord(side->fork, s), "fork")) return rc;
-        if (int rc = check_hip(hipStreamWaitEvent(ds, side->fork, 0), "fork")) return rc;
-    }
-    const int sort_stage = side ? GSR_STAGE_DSORT_CONCURRENT : GSR_STAGE_DEPTH_SORT;
-    // in line, the host reads the published pass count after its sync and runs a
-    // fourth pass only when the keys need it; on the second stream all four are queued
-    uint32_t *pass_word = side ? nullptr : (uint32_t *)g_pinned;
-#ifdef GSR_SORT_FIRST  // A/B builds: the sort before preprocess, a publish kernel of its own
-    const bool after = false;
-#else
-    const bool after = side == nullptr;
-#endif
-    auto sort = [&] {
-        return step(timed(sort_stage, ds, [&] { return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom, pass_word, ds, after ? g_pinned : nullptr, seq); }), "depth sort", dbg, ds);
-    };
-    if (!after)
-        if (int rc = sort()) return rc;
-    if (side)
-        if (int rc = check_hip(hipEventRecord(side->join, ds), "join")) return rc;
-    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, g_pinned, s, !after, seq); }), "preprocess", dbg, s)) return rc;
-    if (after)
-        if (int rc = sort()) return rc;
-#ifndef GSR_POLL_SYNC  // the default: an event after the publish (GSR_POLL_SYNC builds poll the pinned words)
-    if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
-#endif
-    // concurrent mode: the sort's exposed part, the launch stream's wait for its stream
-    if (side)
-        if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] { return hipStreamWaitEvent(s, side->join, 0); }), "join", dbg, s))
+    const int passes = g_four_hint ? 4 : 3;
+    if (int rc = queue_preprocess(in, geom, radii, passes, s, dbg)) return rc;
+    bool late = false;
+    return finish_preprocess(in, geom, passes, s, dbg, num_rendered, &late);
+}
+
+// P == 0: upstream returns the zero-initialised image untouched
+static int render_empty(const gsr_inputs *in, void *img, float *out_color, const float *gt, float *loss_out,
+                        hipStream_t s) {
+    const size_t npix = (size_t)3 * in->W * in->H;
+    if (int rc = check_hip(hipMemsetAsync(out_color, 0, npix * sizeof(float), s), "memset")) return rc;
+    if (!gt) return GSR_OK;
+    float *l1_part = at<float>(img, img_layout(in->W, in->H).l1_part);
+    return step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", in->debug != 0, s);
+}
+
+// Emit and the tile sort of n instances into a binning buffer of capacity cap (g:
+// speculative, then n = cap and the kernels take the published count), then the
+// blend, the backward's preparation and the L1 loss.
+static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t n, int64_t cap, const SpecGuard &g,
+                        void *img, const int32_t *radii, float *out_color, const float *gt, float *loss_out,
+                        uint8_t *visible_out, hipStream_t s, bool dbg) {
+    const size_t npix = (size_t)3 * in->W * in->H;
+    float *l1_part = gt ? at<float>(img, img_layout(in->W, in->H).l1_part) : nullptr;
+    if (n > 0) {
+        if (int rc = step(timed(GSR_STAGE_DUPLICATE, s,
+                                [&] { return launch_emit(in->P, in->W, in->H, geom, binning, cap, g, s); }),
+                          "duplicateWithKeys", dbg, s))
             return rc;
-    // the rects in rank order and the emission offsets (upstream's InclusiveSum of
-    // tiles_touched, in depth order), queued before the host waits: the device stays busy
-    if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, !side, s); }),
-                      "rank gather", dbg, s))
+        if (int rc = step(timed(GSR_STAGE_TILE_SORT, s,
+                                [&] { return launch_tile_sort(in->P, in->W, in->H, geom, binning, n, cap, g, s); }),
+                          "tile sort", dbg, s))
+            return rc;
+    }  // else every range stays (0, 0) as preprocess left it
+    // GSR_FLAG_PREPARE_BACKWARD: render_fwd zeroes the backward's accumulator beside
+    // its blend, and the quadrants are filed after it, so the backward starts with
+    // render_bwd
+    const bool prep = (in->flags & GSR_FLAG_PREPARE_BACKWARD) != 0;
+    const GeomLayout G = geom_layout(in->P, in->W, in->H);
+    void *acc = at<void>(geom, G.accum);
+    const size_t acc_bytes = (size_t)in->P * ACCUM_STRIDE * sizeof(float);
+    if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s,
+                            [&] {
+                                return launch_render_fwd(*in, geom, n > 0 ? binning : nullptr, img, out_color,
+                                                         prep ? (float *)acc : nullptr, acc_bytes, s);
+                            }),
+                      "render", dbg, s))
         return rc;
-#ifndef GSR_POLL_SYNC
-    if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;
-#else
-    // Poll the pinned words: the publish stores num_rendered, then this forward's
-    // sequence number; the first digit scan the pass count (in line).  No event in
-    // the stream (its barrier packet left a ~6 us gap before the next kernel).  A
-    // device that never publishes (a faulted kernel) is caught by a stream sync
-    // after a second of polling.  Not the default: +1 % in alternating A/B runs,
-    // but two of two round profiles with it had one benchmark segment 1.2-1.8x
-    // slower than every run with the event.
-    {
-        volatile uint32_t *pw = g_pinned;
-        auto ready = [&] { return pw[CTRL_SEQ] == seq && (side || pw[CTRL_DSORT_PASSES] != 0u); };
-        const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t spin = 0; !ready(); spin++) {
-            __builtin_ia32_pause();  // a polite spin for the core's other hardware thread
-            if ((spin & 4095u) == 4095u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-                if (int rc = check_hip(hipStreamSynchronize(s), "num_rendered read-back")) return rc;
-                if (!ready()) return fail(GSR_ERR_HIP, "num_rendered was not published");
-                break;
-            }
-        }
-        std::atomic_thread_fence(std::memory_order_acquire);
+    if (!prep) {  // the L1 loss, if asked for, on its own
+        prepared_set(geom, false);
+        return gt ? step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", dbg, s)
+                  : GSR_OK;
     }
-#endif
-    if (g_pinned[CTRL_PREFILTER_ERR])
-        return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    if (!side && g_pinned[CTRL_DSORT_PASSES] != 3u) {
-        // the keys span more than 2^24: the fourth pass, then the rank gather the
-        // queued one skipped (rank_gather_kernel returns at once on a four-pass sort)
-        if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s, [&] { return launch_depth_sort_fourth(in->P, in->W, in->H, geom, s); }),
-                          "depth sort (fourth pass)", dbg, s))
+    // the L1 loss's partial sums ride in the same launch as the quadrant filing
+    int l1_nb = 0;
+    if (int rc = step(launch_bwd_prepare(*in, geom, img, (float *)acc, n > 0, true, true, s, gt ? out_color : nullptr,
+                                         gt, &l1_nb, radii, visible_out),
+                      "backward prepare", dbg, s))
+        return rc;
+    if (gt)
+        if (int rc = step(launch_l1_finish(nullptr, nullptr, npix, l1_part, l1_nb, false, loss_out, s), "l1 loss", dbg, s))
             return rc;
-        if (int rc = step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, false, s); }),
-                          "rank gather", dbg, s))
-            return rc;
-    }
-    const int64_t I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
-    if (I > 0xFFFFFFFFll) return fail(GSR_ERR_CAPACITY, "num_rendered %lld exceeds 32-bit list indexing", (long long)I);
-    *num_rendered = I;
+    prepared_set(geom, true);
+    return GSR_OK;
+}
+
+static int check_render_args(const gsr_inputs *in, void *img, const int32_t *radii, float *out_color, const float *gt,
+                             float *loss_out, uint8_t *visible_out) {
+    if (!out_color) return fail(GSR_ERR_ARGS, "out_color is NULL");
+    if (gt && (!loss_out || !img)) return fail(GSR_ERR_ARGS, "l1: loss_out and img required");
+    if (visible_out && !gt) return fail(GSR_ERR_ARGS, "visible_out needs gt (the L1 form)");
+    if (visible_out && !(in->flags & GSR_FLAG_PREPARE_BACKWARD))
+        return fail(GSR_ERR_ARGS, "visible_out needs GSR_FLAG_PREPARE_BACKWARD");
+    if (visible_out && !radii && in->P > 0) return fail(GSR_ERR_ARGS, "visible_out needs radii");
     return GSR_OK;
 }
 
@@ -372,60 +367,13 @@ static int forward_render_impl(const gsr_inputs *in, void *geom, void *binning, 
                                const int32_t *radii, float *out_color, const float *gt, float *loss_out,
                                uint8_t *visible_out, void *stream) {
     if (int rc = validate(in, true)) return rc;
-    if (!out_color) return fail(GSR_ERR_ARGS, "out_color is NULL");
-    if (gt && (!loss_out || !img)) return fail(GSR_ERR_ARGS, "l1: loss_out and img required");
+    if (int rc = check_render_args(in, img, radii, out_color, gt, loss_out, visible_out)) return rc;
     hipStream_t s = (hipStream_t)stream;
-    const bool dbg = in->debug != 0;
-    const size_t npix = (size_t)3 * in->W * in->H;
-    float *l1_part = gt ? at<float>(img, img_layout(in->W, in->H).l1_part) : nullptr;
-    if (in->P == 0) {  // upstream returns the zero-initialised image untouched
-        if (int rc = check_hip(hipMemsetAsync(out_color, 0, npix * sizeof(float), s), "memset")) return rc;
-        if (!gt) return GSR_OK;
-        return step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", dbg, s);
-    }
+    if (in->P == 0) return render_empty(in, img, out_color, gt, loss_out, s);
     if (!geom || !img || (num_rendered > 0 && !binning)) return fail(GSR_ERR_ARGS, "scratch buffers are NULL");
-    if (num_rendered > 0) {
-        if (int rc = step(timed(GSR_STAGE_DUPLICATE, s, [&] { return launch_emit(in->P, in->W, in->H, geom, radii, binning, num_rendered, s); }),
-                          "duplicateWithKeys", dbg, s))
-            return rc;
-        if (int rc = step(timed(GSR_STAGE_TILE_SORT, s, [&] { return launch_tile_sort(in->P, in->W, in->H, geom, binning, num_rendered, s); }),
-                          "tile sort", dbg, s))
-            return rc;
-    }  // else every range stays (0, 0) as preprocess left it
-    // GSR_FLAG_PREPARE_BACKWARD: the backward's accumulator is zeroed beside the blend
-    // (by render_fwd itself; with GSR_SIDE_STREAM=1 by a memset on the second stream)
-    // and the quadrants are filed after it, so the backward starts with render_bwd
-    const bool prep = (in->flags & GSR_FLAG_PREPARE_BACKWARD) != 0;
-    SideStream *side = nullptr;
-    if (prep && !dbg)
-        if (int rc = side_stream(s, &side)) return rc;
-    const GeomLayout G = geom_layout(in->P, in->W, in->H);
-    void *acc = at<void>(geom, G.accum);
-    const size_t acc_bytes = (size_t)in->P * ACCUM_STRIDE * sizeof(float);
-    if (side) {
-        if (int rc = check_hip(hipEventRecord(side->fork, s), "fork")) return rc;
-        if (int rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "fork")) return rc;
-        if (int rc = check_hip(hipMemsetAsync(acc, 0, acc_bytes, side->s), "accumulator")) return rc;
-        if (int rc = check_hip(hipEventRecord(side->join, side->s), "join")) return rc;
-    }
-    // in line (the default): render_fwd zeroes the accumulator itself, beside its blend
-    float *zero = prep && !side ? (float *)acc : nullptr;
-    if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s, [&] { return launch_render_fwd(*in, geom, binning, num_rendered, img, out_color, zero, acc_bytes, s); }), "render", dbg, s))
-        return rc;
-    if (!prep)  // the L1 loss, if asked for, on its own
-        return gt ? step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", dbg, s)
-                  : GSR_OK;
-    if (side)
-        if (int rc = check_hip(hipStreamWaitEvent(s, side->join, 0), "join")) return rc;
-    // the L1 loss's partial sums ride in the same launch as the quadrant filing
-    int l1_nb = 0;
-    if (int rc = step(launch_bwd_prepare(*in, geom, img, (float *)acc, num_rendered > 0, true, true, s, gt ? out_color : nullptr, gt, &l1_nb, radii, visible_out), "backward prepare", dbg, s))
-        return rc;
-    if (gt)
-        if (int rc = step(launch_l1_finish(nullptr, nullptr, npix, l1_part, l1_nb, false, loss_out, s), "l1 loss", dbg, s))
-            return rc;
-    prepared_set(geom, true);
-    return GSR_OK;
+    if (num_rendered < 0 || num_rendered > 0xFFFFFFFFll) return fail(GSR_ERR_ARGS, "num_rendered out of range");
+    return queue_render(in, geom, binning, num_rendered, num_rendered, SpecGuard{}, img, radii, out_color, gt,
+                        loss_out, visible_out, s, in->debug != 0);
 }
 
 int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
@@ -438,11 +386,50 @@ int gsr_forward_render_l1(const gsr_inputs *in, void *geom, void *binning, void 
                           const int32_t *radii, float *out_color, const float *gt, float *loss_out,
                           uint8_t *visible_out, void *stream) {
     if (!gt) return fail(GSR_ERR_ARGS, "gt is NULL");
-    if (visible_out && !(in && (in->flags & GSR_FLAG_PREPARE_BACKWARD)))
-        return fail(GSR_ERR_ARGS, "visible_out needs GSR_FLAG_PREPARE_BACKWARD");
-    if (visible_out && !radii && in->P > 0) return fail(GSR_ERR_ARGS, "visible_out needs radii");
     return forward_render_impl(in, geom, binning, img, num_rendered, radii, out_color, gt, loss_out, visible_out,
                                stream);
+}
+
+int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning, int64_t capacity, void *img,
+                float *out_color, const float *gt, float *loss_out, uint8_t *visible_out, int64_t *num_rendered,
+                void *stream) {
+    if (int rc = validate(in, true)) return rc;
+    if (!num_rendered) return fail(GSR_ERR_ARGS, "num_rendered is NULL");
+    *num_rendered = 0;
+    if (int rc = check_render_args(in, img, radii, out_color, gt, loss_out, visible_out)) return rc;
+    if (capacity < 0 || capacity > 0xFFFFFFFFll) return fail(GSR_ERR_ARGS, "binning capacity out of range");
+    hipStream_t s = (hipStream_t)stream;
+    if (in->P == 0) return render_empty(in, img, out_color, gt, loss_out, s);
+    if (!geom || !radii || !img || (capacity > 0 && !binning)) return fail(GSR_ERR_ARGS, "scratch buffers are NULL");
+    const bool dbg = in->debug != 0;
+    const int passes = g_four_hint ? 4 : 3;
+    if (int rc = queue_preprocess(in, geom, radii, passes, s, dbg)) return rc;
+    // Speculative: everything after the depth sort is queued before the host reads
+    // num_rendered, into the caller's buffer of `capacity` instances; each binning
+    // kernel checks the published count on the device and does nothing unless it
+    // fits (SpecGuard).  Debug mode checks every kernel in turn instead.
+    const bool spec = !dbg && capacity > 0;
+    if (spec) {
+        const GeomLayout G = geom_layout(in->P, in->W, in->H);
+        const SpecGuard g{at<const uint32_t>(geom, G.off[GSR_GEOM_CTRL]), at<const uint32_t>(geom, G.dsort_ctrl),
+                          (uint32_t)capacity, passes == 3 ? 1 : 0};
+        if (int rc = queue_render(in, geom, binning, capacity, capacity, g, img, radii, out_color, gt, loss_out,
+                                  visible_out, s, dbg))
+            return rc;
+    }
+    int64_t I = 0;
+    bool late = false;
+    if (int rc = finish_preprocess(in, geom, passes, s, dbg, &I, &late)) return rc;
+    *num_rendered = I;
+    if (I > capacity) {
+        fail(GSR_NEED_BINNING, "binning capacity %lld < num_rendered %lld: call gsr_forward_render with a buffer of "
+             "gsr_binning_bytes(num_rendered)", (long long)capacity, (long long)I);
+        return GSR_NEED_BINNING;
+    }
+    if (spec && !late) return GSR_OK;
+    // debug mode, or the fourth depth pass queued only now: the rest, exactly
+    return queue_render(in, geom, binning, I, capacity, SpecGuard{}, img, radii, out_color, gt, loss_out, visible_out,
+                        s, dbg);
 }
 
 static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
@@ -491,7 +478,7 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
                               "backward prepare", dbg, s))
                 return rc;
         if (num_rendered > 0) {
-            if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, num_rendered, img, seed ? nullptr : dL_dout_color, seed, acc, s); }),
+            if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, img, seed ? nullptr : dL_dout_color, seed, acc, s); }),
                               "render backward", dbg, s))
                 return rc;
         }

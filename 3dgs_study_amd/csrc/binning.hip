@@ -123,7 +123,9 @@ struct RadixPass {
     const uint4 *pub_sums;
     int pub_n;
     uint32_t *pub_ctrl, *pub_host;
-    uint32_t pub_seq;
+    // tile sort queued before the host knows num_rendered (gsr_forward): n is the
+    // buffer's capacity and every kernel works on the published count instead
+    SpecGuard g;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
@@ -197,8 +199,8 @@ template <int TILE_N, int MODE>
 __device__ __forceinline__ uint2 block_span(const RadixPass &a, uint32_t blk, uint32_t *sfb, uint32_t *sst,
                                             uint32_t *wsum) {
     if constexpr (MODE != RXM_UNPACK) {
-        const uint32_t b0 = blk * (uint32_t)TILE_N;
-        return make_uint2(b0, min(b0 + (uint32_t)TILE_N, a.n));
+        const uint32_t n = spec_count(a.g, a.n), b0 = blk * (uint32_t)TILE_N;
+        return b0 < n ? make_uint2(b0, min(b0 + (uint32_t)TILE_N, n)) : make_uint2(0u, 0u);
     } else {
         (void)wsum;
         sfb[threadIdx.x] = a.seg_table[threadIdx.x];
@@ -302,7 +304,7 @@ static_assert(DSCAN_THREADS == TOTAL_THREADS, "the publish workgroup runs in the
 __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPass a) {
     __shared__ uint32_t wsum[DSCAN_THREADS / 64];
     if (blockIdx.x == RADIX + 1) {  // (grid RADIX + 2 only with pub_sums)
-        publish_total(a.pub_sums, a.pub_n, a.pub_ctrl, a.pub_host, a.pub_seq);
+        publish_total(a.pub_sums, a.pub_n, a.pub_ctrl, a.pub_host);
         return;
     }
     if (blockIdx.x == RADIX) {  // first depth pass: one more workgroup reduces the candidate key range
@@ -661,6 +663,7 @@ struct EmitArgs {
     const uint32_t *super;        // instances per rank-gather workgroup
     uint32_t *tile_keys;
     uint32_t *ids;
+    SpecGuard g;  // speculative (gsr_forward): nothing at all unless the published count fits
 };
 __device__ __forceinline__ uint32_t div_small(uint32_t pos, uint32_t w) {  // pos / w for pos < 2^24
     uint32_t y = (uint32_t)((float)pos * __builtin_amdgcn_rcpf((float)w));
@@ -669,6 +672,7 @@ __device__ __forceinline__ uint32_t div_small(uint32_t pos, uint32_t w) {  // po
     return y;
 }
 __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
+    if (!spec_ok(a.g)) return;
     __shared__ uint32_t wsum[2 * (EMIT_BLOCK / 64)];
     __shared__ uint32_t loff[EMIT_BLOCK + 1];
     __shared__ uint4 rect[EMIT_BLOCK];  // x0, width, y0, id
@@ -768,7 +772,8 @@ __global__ void __launch_bounds__(EMIT_BLOCK) emit_kernel(EmitArgs a) {
 // tile change closes the previous tile and opens the next.
 constexpr int RANGE_THREADS = 256;
 __global__ void __launch_bounds__(RANGE_THREADS) identify_ranges_kernel(const uint32_t *tile_keys, uint32_t n,
-                                                                         uint2 *ranges) {
+                                                                         uint2 *ranges, SpecGuard g) {
+    n = spec_count(g, n);
     const uint32_t i0 = (blockIdx.x * RANGE_THREADS + threadIdx.x) * 4u;
     if (i0 >= n) return;
     uint32_t v[4];
@@ -811,7 +816,7 @@ hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const v
                                   uint64_t *keys, hipStream_t s) {
     if (I <= 0) return hipSuccess;
     const GeomLayout L = geom_layout(P, W, H);
-    const BinningLayout B = binning_layout(I, W, H);
+    const BinningLayout B = binning_layout(I, W, H);  // (point_list: offset 0 for every capacity)
     hipLaunchKernelGGL(point_list_keys_kernel, dim3((unsigned)grid_dims(W, H).tiles), dim3(256), 0, s,
                        at<const uint2>(geom, L.off[GSR_GEOM_RANGES]),
                        at<const uint32_t>(binning, B.off[GSR_BIN_POINT_LIST]),
@@ -941,7 +946,7 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
 
 template <int ITEMS>
 static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                                   uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl, uint32_t seq) {
+                                   int passes, uint32_t *host_ctrl, hipStream_t s) {
     const GeomLayout L = geom_layout(P, W, H);
     DepthKeyArgs k;
     k.means3D = means3D;
@@ -954,20 +959,19 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     k.zero = dsort_grouped(P) ? at<uint32_t>(geom, L.dsort_sup) : nullptr;
     k.zero_n = dsort_grouped(P) ? 3 * dsort_nsup(P) * RADIX : 0;
     hipLaunchKernelGGL(depth_keys_kernel<ITEMS>, dim3(k.NB), dim3(RX_THREADS), 0, s, k);
-    // host_ctrl: passes 1-3 only; the host reads the published pass count after its
-    // one sync and launches the fourth (launch_depth_sort_fourth) when the keys need
-    // it — three early-returning launches (~14 us at config C) saved in the common case
-    for (int p = 0; p < (host_ctrl ? 3 : 4); p++) {
+    // passes 3: the host reads the published pass count after its sync and launches
+    // the fourth (launch_depth_sort_fourth) when the keys need it — three
+    // early-returning launches (~14 us at config C) saved in the common case;
+    // passes 4: queued up front (the last forward needed it), returning at once
+    // when three suffice
+    for (int p = 0; p < passes; p++) {
         RadixPass a = depth_pass(P, W, H, geom, p);
-        if (p == 0) {
+        if (p == 0) {  // the first digit scan publishes the pass count and num_rendered
             a.host_ctrl = host_ctrl;
-            if (publish_ctrl) {
-                a.pub_sums = at<const uint4>(geom, L.block_sums);
-                a.pub_n = pre_blocks(P);
-                a.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
-                a.pub_host = publish_ctrl;
-                a.pub_seq = seq;
-            }
+            a.pub_sums = at<const uint4>(geom, L.block_sums);
+            a.pub_n = pre_blocks(P);
+            a.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+            a.pub_host = host_ctrl;
         }
         hipError_t e = radix_pass<ITEMS>(a, s, p == 0);
         if (e != hipSuccess) return e;
@@ -976,11 +980,11 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
 }
 
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl, uint32_t seq) {
+                             int passes, uint32_t *host_ctrl, hipStream_t s) {
     if (P <= 0) return hipSuccess;
     return dsort_items(P) == DSORT_ITEMS_BIG
-               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s, publish_ctrl, seq)
-               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, host_ctrl, s, publish_ctrl, seq);
+               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, s)
+               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, s);
 }
 
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s) {
@@ -989,7 +993,7 @@ hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t
                                              : radix_pass<DSORT_ITEMS>(depth_pass(P, W, H, geom, 3), s);
 }
 
-// After both streams: the rects in rank order and the rank-order instance offsets
+// After the depth sort: the rects in rank order and the rank-order instance offsets
 // of the emit blocks.
 hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hipStream_t s) {
     if (P <= 0) return hipSuccess;
@@ -1001,10 +1005,10 @@ hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hi
     return hipGetLastError();
 }
 
-hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
+hipError_t launch_emit(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &guard,
                        hipStream_t s) {
     const GeomLayout L = geom_layout(P, W, H);
-    const BinningLayout B = binning_layout(I, W, H);
+    const BinningLayout B = binning_layout(cap, W, H);
     const GridDims g = grid_dims(W, H);
     EmitArgs a;
     a.P = P;
@@ -1023,13 +1027,18 @@ hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, vo
     a.id_bits = 32 - (bits - bits / 2);
     a.tile_keys = at<uint32_t>(binning, odd ? B.keys_b : B.off[GSR_BIN_KEYS]);
     a.ids = at<uint32_t>(binning, odd ? B.vals_b : B.off[GSR_BIN_POINT_LIST]);
+    a.g = guard;
     hipLaunchKernelGGL(emit_kernel, dim3(emit_blocks(P)), dim3(EMIT_BLOCK), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, hipStream_t s) {
+// n: the instances to sort (the capacity, when g is speculative); cap: the binning
+// buffer's capacity, which fixes its layout and the radix block size
+hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t n, int64_t cap,
+                            const SpecGuard &guard, hipStream_t s) {
+    const int64_t I = n;
     const GeomLayout L = geom_layout(P, W, H);
-    const BinningLayout B = binning_layout(I, W, H);
+    const BinningLayout B = binning_layout(cap, W, H);
     const GridDims g = grid_dims(W, H);
     const int npass = tile_sort_passes(g.tiles);
     uint32_t *keys[2] = {at<uint32_t>(binning, B.off[GSR_BIN_KEYS]), at<uint32_t>(binning, B.keys_b)};
@@ -1038,7 +1047,8 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
     int cur = npass & 1;
     RadixPass a = {};
     a.n = (uint32_t)I;
-    const int items = tsort_items(I);
+    a.g = guard;
+    const int items = tsort_items(cap);
     a.NB = radix_blocks(I, items);
     a.role = RX_PLAIN;
     a.hist = at<uint32_t>(binning, B.hist);
@@ -1095,7 +1105,7 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
     }
     const int64_t per_block = 4 * RANGE_THREADS;
     hipLaunchKernelGGL(identify_ranges_kernel, dim3((unsigned)((I + per_block - 1) / per_block)), dim3(RANGE_THREADS),
-                       0, s, (const uint32_t *)keys[0], (uint32_t)I, ranges);
+                       0, s, (const uint32_t *)keys[0], (uint32_t)I, ranges, guard);
     return hipGetLastError();
 }
 

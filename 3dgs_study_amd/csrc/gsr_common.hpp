@@ -116,15 +116,38 @@ enum CtrlWord {
     CTRL_PREFILTER_ERR = 2,
     CTRL_DSORT_PASSES = 3,  // host copy only: the depth sort's pass count (its first digit scan publishes it)
     CTRL_SHJAC = 4,         // device only: 1 when this forward's preprocess stored the SH direction Jacobian
-    CTRL_SEQ = 5,           // host copy only: the forward's sequence number, stored after the words above
     CTRL_WORDS = 16
 };
-// the depth sort's own control words (GeomLayout::dsort_ctrl, a line of their own:
-// with GSR_SIDE_STREAM=1 the sort runs on a second stream beside preprocess, binning.hip)
+// the depth sort's own control words (GeomLayout::dsort_ctrl, a line of their own)
 enum DsortCtrlWord {
     DCTRL_KEY_BASE = 0,  // smallest depth key (bits) of a candidate Gaussian, low byte cleared
     DCTRL_PASSES = 1,    // 3 when every candidate key lies within 2^24 of the base, else 4
 };
+
+// Speculative binning (gsr_forward): emit and the tile sort are queued before the
+// host has read num_rendered, into a binning buffer of `cap` instances.  Each of
+// their kernels reads the count the depth sort's first digit scan published into
+// the geom control words and does nothing at all unless it fits (and, when the
+// host queued only three depth passes, unless three sufficed: a four-pass sort's
+// rank order is not ready yet).  The host then re-runs what it must (gsr_forward).
+// ctrl == NULL: not speculative, the host-side count is exact.
+struct SpecGuard {
+    const uint32_t *ctrl;   // geom control words (CTRL_NUM_RENDERED_LO / HI)
+    const uint32_t *dctrl;  // the depth sort's control words (DCTRL_PASSES)
+    uint32_t cap;
+    int need3;              // only three depth passes were queued
+};
+__device__ __forceinline__ bool spec_ok(const SpecGuard &g) {
+    if (!g.ctrl) return true;
+    return g.ctrl[CTRL_NUM_RENDERED_HI] == 0u && g.ctrl[CTRL_NUM_RENDERED_LO] <= g.cap &&
+           (!g.need3 || g.dctrl[DCTRL_PASSES] == 3u);
+}
+// the instance count a binning kernel works on: the host's, or the published one
+// (0 when the speculation failed: every block is then empty)
+__device__ __forceinline__ uint32_t spec_count(const SpecGuard &g, uint32_t host_n) {
+    if (!g.ctrl) return host_n;
+    return spec_ok(g) ? g.ctrl[CTRL_NUM_RENDERED_LO] : 0u;
+}
 
 struct GeomLayout {
     size_t off[GSR_GEOM_NFIELDS];
@@ -182,23 +205,28 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     return L;
 }
 
+// The binning buffer of an instance capacity `cap` (>= num_rendered: gsr_forward
+// sizes it before the count is known).  point_list comes first, at offset 0 for
+// every capacity, so the blend kernels and the backward find it from the pointer
+// alone; the other fields are the forward's own scratch, laid out by the capacity
+// the forward was given.
 struct BinningLayout {
     size_t off[GSR_BIN_NFIELDS];
-    size_t keys_b;  // uint32 [I] tile-sort ping-pong
-    size_t vals_b;  // uint32 [I]
-    size_t hist;    // uint32 [RADIX][radix_blocks(I, tsort_items(I)) + RADIX] (+ RADIX: segment-aligned blocks)
+    size_t keys_b;  // uint32 [cap] tile-sort ping-pong
+    size_t vals_b;  // uint32 [cap]
+    size_t hist;    // uint32 [RADIX][radix_blocks(cap, tsort_items(cap)) + RADIX] (+ RADIX: segment-aligned blocks)
     size_t totals;  // uint32 [RADIX]
     size_t totals1; // uint32 [RADIX] the first tile pass's digit totals (the second pass's segments)
     size_t seg_table; // uint32 [2][RADIX + 1] the second pass's segment table: first block, first item
     size_t bytes;
 };
-__host__ __device__ inline BinningLayout binning_layout(int64_t I, int W, int H) {
+__host__ __device__ inline BinningLayout binning_layout(int64_t cap, int W, int H) {
     BinningLayout L;
-    size_t n = (size_t)(I > 0 ? I : 1);
+    size_t n = (size_t)(cap > 0 ? cap : 1);
     size_t o = 0;
     auto take = [&](size_t b) { size_t r = o; o = align_up(o + b, 256); return r; };
-    L.off[GSR_BIN_KEYS] = take(n * 4);
     L.off[GSR_BIN_POINT_LIST] = take(n * 4);
+    L.off[GSR_BIN_KEYS] = take(n * 4);
     L.keys_b = take(n * 4);
     L.vals_b = take(n * 4);
     L.hist = take((size_t)RADIX * (radix_blocks((int64_t)n, tsort_items((int64_t)n)) + RADIX) * 4);

@@ -7,30 +7,34 @@
 
 namespace gsr {
 
-// preprocess.hip
-// publish: num_rendered from publish_total_kernel (false: the depth sort's first
-// digit scan publishes it — launch_depth_sort with publish_ctrl, after preprocess)
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, uint32_t *host_ctrl, hipStream_t s,
-                             bool publish = true, uint32_t seq = 0);
+// preprocess.hip (num_rendered is published by the depth sort's first digit scan)
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 
 // binning.hip
-// publish_ctrl (or NULL): the sort runs after preprocess and its first digit scan
-// also publishes num_rendered into these pinned words (launch_preprocess publish = false)
+// passes: 3 (the host launches the fourth after its sync when the published pass
+// count says so) or 4 (queued up front; returns at once when three suffice).
+// host_ctrl: the caller's pinned words, which the first digit scan fills with the
+// pass count and num_rendered (after preprocess, in stream order).
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             uint32_t *host_ctrl, hipStream_t s, uint32_t *publish_ctrl = nullptr, uint32_t seq = 0);
+                             int passes, uint32_t *host_ctrl, hipStream_t s);
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s);
 hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hipStream_t s);
-hipError_t launch_emit(int P, int W, int H, void *geom, const int32_t *radii, void *binning, int64_t I,
+// cap: the binning buffer's instance capacity (its layout); g: speculative guard
+// (gsr_common.hpp SpecGuard; ctrl NULL = the count is exact, cap == num_rendered
+// or larger)
+hipError_t launch_emit(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g,
                        hipStream_t s);
-hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t I, hipStream_t s);
+hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t n, int64_t cap,
+                            const SpecGuard &g, hipStream_t s);
 hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const void *binning, int64_t I,
                                   uint64_t *keys, hipStream_t s);
 
 // render_fwd.hip
-hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,
-                             float *out_color, float *acc_zero, size_t acc_bytes, hipStream_t s);
+// (binning: point_list at offset 0, whatever the buffer's capacity)
+hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binning, void *img, float *out_color,
+                             float *acc_zero, size_t acc_bytes, hipStream_t s);
 
 // render_bwd.hip
 // l1 (forward only, or NULL): {image, gt, n} whose L1 partial sums (gsr_l1.hpp) the
@@ -40,8 +44,8 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
                               bool internal, bool forward, hipStream_t s, const float *l1_x = nullptr,
                               const float *l1_y = nullptr, int *l1_nb = nullptr, const int32_t *radii = nullptr,
                               uint8_t *visible = nullptr);
-hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
-                             const void *img, const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s);
+hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, const void *img,
+                             const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s);
 
 // preprocess_bwd.hip
 struct BwdOutputs {

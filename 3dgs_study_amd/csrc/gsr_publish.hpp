@@ -1,8 +1,7 @@
 // gsr_publish.hpp — num_rendered from the preprocess workgroups' instance sums,
 // published into the geom control words and the caller's pinned host words.  One
-// 1024-thread workgroup: publish_total_kernel (preprocess.hip), or one extra
-// workgroup of the depth sort's first digit scan (binning.hip) when the sort runs
-// after preprocess in line — one launch fewer.
+// 1024-thread workgroup: an extra workgroup of the depth sort's first digit scan
+// (binning.hip), which runs right after preprocess — no launch of its own.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -14,9 +13,7 @@
 namespace gsr {
 
 constexpr int TOTAL_THREADS = 1024;
-// seq: stored into host_ctrl[CTRL_SEQ] after the other words (the host polls it)
-__device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t *ctrl, uint32_t *host_ctrl,
-                                              uint32_t seq) {
+__device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t *ctrl, uint32_t *host_ctrl) {
     __shared__ unsigned long long part[TOTAL_THREADS / 64];
     __shared__ uint32_t perr[TOTAL_THREADS / 64];
     unsigned long long t = 0;
@@ -57,8 +54,6 @@ __device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t
             ctrl[k] = w[k];
             __hip_atomic_store(&host_ctrl[k], w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        __threadfence_system();
-        __hip_atomic_store(&host_ctrl[CTRL_SEQ], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __threadfence_system();
     }
 }

@@ -294,14 +294,6 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     if (threadIdx.x == 0) a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), 0u, 0u, 0u);
 }
 
-// One workgroup totals the block sums and publishes num_rendered and the error
-// flag into the geom control words and, with system-scope stores, straight into
-// the caller's pinned host words (no copy; the host waits for this kernel's event).
-__global__ void __launch_bounds__(TOTAL_THREADS) publish_total_kernel(const uint4 *sums, int n, uint32_t *ctrl,
-                                                                      uint32_t *host_ctrl, uint32_t seq) {
-    publish_total(sums, n, ctrl, host_ctrl, seq);
-}
-
 // auxiliary.h in_frustum via checkFrustum (markVisible).
 __global__ void mark_visible_kernel(int P, const float *means3D, const float *viewmatrix, uint8_t *present) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -312,8 +304,7 @@ __global__ void mark_visible_kernel(int P, const float *means3D, const float *vi
     present[idx] = !(pv.z <= 0.2f);
 }
 
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, uint32_t *host_ctrl, hipStream_t s,
-                             bool publish, uint32_t seq) {
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, hipStream_t s) {
     const GeomLayout L = geom_layout(in.P, in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
     PreArgs a;
@@ -350,9 +341,7 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, u
         split ? go(preprocess_fwd_kernel<48, true>) : go(preprocess_fwd_kernel<48, false>);
     else
         split ? go(preprocess_fwd_kernel<0, true>) : go(preprocess_fwd_kernel<0, false>);
-    if (publish)  // else the depth sort's first digit scan publishes (binning.hip)
-        hipLaunchKernelGGL(publish_total_kernel, dim3(1), dim3(TOTAL_THREADS), 0, s, (const uint4 *)a.block_sums, nb,
-                           at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]), host_ctrl, seq);
+    // num_rendered: the depth sort's first digit scan publishes it (binning.hip)
     return hipGetLastError();
 }
 

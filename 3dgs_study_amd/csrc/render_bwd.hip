@@ -472,9 +472,8 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
     return hipGetLastError();
 }
 
-hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I,
-                             const void *img, const float *dL_dpix, const gsr_l1_seed *l1, float *accum,
-                             hipStream_t s) {
+hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, const void *img,
+                             const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -484,7 +483,7 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.gx = g.gx;
     a.tiles = g.tiles;
     a.ranges = at<uint2>(geom, G.off[GSR_GEOM_RANGES]);
-    a.point_list = at<uint32_t>(binning, binning_layout(I, in.W, in.H).off[GSR_BIN_POINT_LIST]);
+    a.point_list = static_cast<const uint32_t *>(binning);  // GSR_BIN_POINT_LIST: offset 0 (gsr_common.hpp)
     a.splats = at<float4>(geom, G.off[GSR_GEOM_SPLATS]);
     a.bg = in.bg;
     a.final_T = at<float>(img, Im.off[GSR_IMG_FINAL_T]);

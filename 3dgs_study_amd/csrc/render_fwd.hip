@@ -34,6 +34,10 @@ struct RenderFwdArgs {
     // stores ride along (a separate memset launch took 10 us at config C)
     float4 *zero4;
     size_t zero_n4;
+    // the backward's wave-order counts and flag words (gsr_blend.hpp), cleared by
+    // workgroup 0: this forward's quadrants are filed afresh (bwd_prepare_kernel),
+    // however many forwards ran on the geom buffer since its preprocess
+    uint32_t *order_cnt;
 };
 
 #ifndef GSR_FWD_GROUP
@@ -57,6 +61,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     };
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < ORDER_FILED + 2; i += BLEND_THREADS) a.order_cnt[i] = 0u;
     if (tile < 0) {
         zero_slice();
         return;
@@ -211,8 +217,8 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     zero_slice();
 }
 
-hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void *binning, int64_t I, void *img,
-                             float *out_color, float *acc_zero, size_t acc_bytes, hipStream_t s) {
+hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binning, void *img, float *out_color,
+                             float *acc_zero, size_t acc_bytes, hipStream_t s) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -222,7 +228,7 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
     a.gx = g.gx;
     a.tiles = g.tiles;
     a.ranges = at<uint2>(geom, G.off[GSR_GEOM_RANGES]);
-    a.point_list = binning ? at<uint32_t>(binning, binning_layout(I, in.W, in.H).off[GSR_BIN_POINT_LIST]) : nullptr;
+    a.point_list = static_cast<const uint32_t *>(binning);  // GSR_BIN_POINT_LIST: offset 0 (gsr_common.hpp)
     a.splats = at<float4>(geom, G.off[GSR_GEOM_SPLATS]);
     a.bg = in.bg;
     a.out_color = out_color;
@@ -231,6 +237,7 @@ hipError_t launch_render_fwd(const gsr_inputs &in, const void *geom, const void 
     a.qbucket = at<uint8_t>(img, Im.qbucket);
     a.zero4 = reinterpret_cast<float4 *>(acc_zero);
     a.zero_n4 = acc_zero ? acc_bytes / sizeof(float4) : 0;
+    a.order_cnt = at<uint32_t>(geom, G.order_cnt);
     hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }

@@ -64,7 +64,7 @@ EXPORTED = (
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
     "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
-    "gsr_forward_render_l1",
+    "gsr_forward_render_l1", "gsr_forward",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -157,7 +157,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib = None
 
@@ -193,6 +193,8 @@ def load_library():
     lib.gsr_forward_render.restype = ctypes.c_int
     lib.gsr_forward_render_l1.argtypes = [pin, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
     lib.gsr_forward_render_l1.restype = ctypes.c_int
+    lib.gsr_forward.argtypes = [pin, vp, vp, vp, i64, vp, vp, vp, vp, vp, ctypes.POINTER(i64), vp]
+    lib.gsr_forward.restype = ctypes.c_int
     lib.gsr_backward.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
     lib.gsr_backward.restype = ctypes.c_int
     lib.gsr_backward_planar.argtypes = [pin, vp, vp, vp, vp, i64, vp, vp] + [vp] * 8 + [vp]
@@ -296,6 +298,42 @@ def _stream(device):
 
 FLAG_PREPARE_BACKWARD = 1  # gsr.h gsr_flags
 FLAG_L1_SEED = 2
+NEED_BINNING = 5  # gsr.h gsr_status: gsr_forward's binning capacity was too small
+
+
+# ------------------------------------------------------------------ binning capacity
+# gsr_forward queues the whole forward before the host reads num_rendered, into a
+# binning buffer sized from the last forward of the same image size and footprint
+# (its count scaled by the Gaussian count, plus a margin); a count above that
+# capacity costs one extra render call (gsr.h GSR_NEED_BINNING), never a wrong
+# result.  The first forward of a size takes the two-call form.
+_CAP_SLACK = 1.0625
+_CAP_PAD = 4096
+_capacity_level = {}  # (W, H, footprint) -> (P, num_rendered) of the last forward
+capacity_override = None  # test hook: an int capacity for every forward (0: always the two-call form)
+last_forward = {}  # how the last forward ran: {"capacity", "num_rendered", "path"} (tests, bench)
+
+
+def _capacity_for(key, P):
+    if capacity_override is not None:
+        return int(capacity_override) or None
+    lv = _capacity_level.get(key)
+    if lv is None:
+        return None
+    P0, I0 = lv
+    scaled = I0 * P / P0 if P0 > 0 else I0
+    return min(int(scaled * _CAP_SLACK) + _CAP_PAD, 0xFFFFFFFF)
+
+
+def _note_count(key, P, I):
+    """Grow the scene's level at once; shrink it slowly (1/128 per forward), so one
+    sparse view does not make the next dense one overflow."""
+    lv = _capacity_level.get(key)
+    if lv is not None and lv[0] == P and I < lv[1]:
+        I = max(I, lv[1] - (lv[1] >> 7))
+    if len(_capacity_level) > 64 and key not in _capacity_level:
+        _capacity_level.clear()
+    _capacity_level[key] = (P, I)
 
 
 def l1_loss(image: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
@@ -405,23 +443,43 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
     img = _alloc((lib.gsr_img_bytes(W, H),), torch.uint8, device)
     stream = _stream(device)
     num_rendered = ctypes.c_int64(0)
-    _check(lib.gsr_forward_preprocess(ctypes.byref(s), geom.data_ptr(), _ptr(radii), ctypes.byref(num_rendered),
-                                      stream), "rasterize_gaussians (preprocess)")
-    binning = _alloc((lib.gsr_binning_bytes(num_rendered.value, W, H),), torch.uint8, device)
-    if l1_target is None:
-        _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
-                                      num_rendered.value, _ptr(radii), out_color.data_ptr(), stream),
-               "rasterize_gaussians (render)")
+    gt = loss = vis = None
+    if l1_target is not None:
+        gt = _prep(l1_target, "l1_target", device)
+        if gt is None or gt.shape != (3, H, W):
+            raise RuntimeError(f"l1_target must be a float32 [3,{H},{W}] tensor on {device}")
+        loss = torch.empty(3, dtype=torch.float32, device=device)
+        vis = torch.empty(P, dtype=torch.bool, device=device) if prepare_backward and P > 0 else None
+    key = (W, H, s.footprint)
+    cap = None if s.debug or P == 0 else _capacity_for(key, P)
+    done = False
+    if cap is not None:  # one call, queued before the count is read (gsr_forward)
+        binning = _alloc((lib.gsr_binning_bytes(cap, W, H),), torch.uint8, device)
+        rc = lib.gsr_forward(ctypes.byref(s), geom.data_ptr(), _ptr(radii), binning.data_ptr(), cap, img.data_ptr(),
+                             out_color.data_ptr(), _ptr(gt), _ptr(loss), _ptr(vis), ctypes.byref(num_rendered), stream)
+        done = rc != NEED_BINNING
+        if done:
+            _check(rc, "rasterize_gaussians")
+        last_forward.update(capacity=cap, num_rendered=num_rendered.value, path="one call" if done else "regrown")
+    else:
+        _check(lib.gsr_forward_preprocess(ctypes.byref(s), geom.data_ptr(), _ptr(radii), ctypes.byref(num_rendered),
+                                          stream), "rasterize_gaussians (preprocess)")
+        last_forward.update(capacity=None, num_rendered=num_rendered.value, path="two calls")
+    if not done:
+        binning = _alloc((lib.gsr_binning_bytes(num_rendered.value, W, H),), torch.uint8, device)
+        if gt is None:
+            _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
+                                          num_rendered.value, _ptr(radii), out_color.data_ptr(), stream),
+                   "rasterize_gaussians (render)")
+        else:
+            _check(lib.gsr_forward_render_l1(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
+                                             num_rendered.value, _ptr(radii), out_color.data_ptr(), gt.data_ptr(),
+                                             loss.data_ptr(), _ptr(vis), stream),
+                   "rasterize_gaussians (render + L1)")
+    if P > 0:
+        _note_count(key, P, num_rendered.value)
+    if gt is None:
         return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M)
-    gt = _prep(l1_target, "l1_target", device)
-    if gt is None or gt.shape != (3, H, W):
-        raise RuntimeError(f"l1_target must be a float32 [3,{H},{W}] tensor on {device}")
-    loss = torch.empty(3, dtype=torch.float32, device=device)
-    vis = torch.empty(P, dtype=torch.bool, device=device) if prepare_backward and P > 0 else None
-    _check(lib.gsr_forward_render_l1(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
-                                     num_rendered.value, _ptr(radii), out_color.data_ptr(), gt.data_ptr(),
-                                     loss.data_ptr(), None if vis is None else vis.data_ptr(), stream),
-           "rasterize_gaussians (render + L1)")
     if vis is None:
         vis = radii > 0
     return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M), loss[0], vis
@@ -644,6 +702,6 @@ def layouts(P, W, H, num_rendered):
     im = (ctypes.c_size_t * 16)()
     ni = lib.gsr_img_layout(W, H, im, 16)
     geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "ranges", "ctrl", "depth_order",
-                  "dsort_ctrl")
+                  "dsort_ctrl")  # (binning: point_list at offset 0 for every capacity)
     return (dict(zip(geom_names, list(g)[:n])), dict(zip(("keys", "point_list"), list(b)[:nb])),
             dict(zip(("final_T", "n_contrib"), list(im)[:ni])))

@@ -115,7 +115,8 @@ def _leaf_state(leaf, shape, device, ex=None):
     if (leaf is None or not leaf.is_leaf or not leaf.requires_grad or leaf.dtype is not torch.float32
             or leaf.device != device or leaf.shape != shape or not leaf.is_contiguous() or leaf._backward_hooks):
         return -1
-    if getattr(leaf, "_post_accumulate_grad_hooks", None) and not (ex is not None and ex.owns_hooks(leaf)):
+    owns = getattr(ex, "owns_hooks", None)  # (a round-1 sink has no bucket protocol)
+    if getattr(leaf, "_post_accumulate_grad_hooks", None) and not (owns is not None and owns(leaf)):
         return -1
     g = leaf.grad
     if g is None:
@@ -199,7 +200,8 @@ def _leaf_plan(ctx, needs, sh, colors_precomp, opacities, scales, rotations, mea
                 plan["means3D"] = ((means3D,), s_, None)
     except (AttributeError, RuntimeError, TypeError):
         return {}
-    views = ex.leaf_bucket({k: v[0] for k, v in plan.items()}) if ex is not None and plan else {}
+    bucket = getattr(ex, "leaf_bucket", None)  # (a round-1 sink offers no bucket)
+    views = bucket({k: v[0] for k, v in plan.items()}) if bucket is not None and plan else {}
     if "means3D" not in views:
         plan.pop("means3D", None)
     return {k: (v[0], v[1], v[2], views.get(k)) for k, v in plan.items()}
@@ -440,11 +442,16 @@ class _RasterizeModel(torch.autograd.Function):
         sink_takes_sh = (ex is not None and (needs[2] or needs[3])
                          and ex.accepts((f_dc, f_rest), means3D))
         views = {}
-        if ex is not None:
+        bucket = getattr(ex, "leaf_bucket", None)  # (a round-1 sink offers no bucket)
+        if bucket is not None and not torch.is_grad_enabled():
+            # only leaves nothing else observes go to the bucket (the written view is
+            # their .grad and autograd never sees the gradient): no tensor hooks,
+            # retain_grad or post-accumulate hooks but the exchange's own, and no
+            # create_graph — the rest come back through autograd
             want = {k: (t,) for k, t, n in (("means3D", means3D, needs[0]), ("opacities", opacity, needs[4]),
                                             ("scales", scaling, needs[5]), ("rotations", rotation, needs[6]))
-                    if n and t.is_leaf}
-            views = ex.leaf_bucket(want) if want else {}
+                    if n and _leaf_state(t, t.shape, device, ex) >= 0}
+            views = bucket(want) if want else {}
         fresh, acc = [], 0
 
         def out(name, leaf, shape, bit):

@@ -94,6 +94,8 @@ class GradAllReduce:
         self._bucket = None     # this step's flat fp32 bucket over self._reduced
         self._views = None      # its per-parameter views
         self._work = None       # the bucket's async all-reduce
+        self._early = False     # ... started by the rasterizer (rasterizer_done): the leaves' .grad are cleared
+        self._extra = None      # (indices, flat, work): gradients that reached reduced leaves after that start
         self._backwards = 0     # backwards finished this step
         self._cb_queued = False
         self.launched_in_backward = False  # the bucket's all-reduce started from the end-of-backward callback
@@ -233,6 +235,17 @@ class GradAllReduce:
             return
         self._work = dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.launched_in_backward = True
+        # The bucket now belongs to the collective.  Another gradient path into a
+        # reduced leaf (an extra loss term, a regulariser on _scaling ...) reaches
+        # its AccumulateGrad after this backward — and would add in place into the
+        # .grad it finds, i.e. into the bucket RCCL is reading, never to be reduced
+        # (ADVICE r4).  So the leaves' .grad are cleared: such a contribution lands
+        # in a fresh tensor, reduced on its own at the end of the backward, and
+        # __call__ adds it to the reduced bucket and reinstalls the views.
+        self._early = True
+        self._early_version = self._bucket._version
+        for p in self._reduced:
+            p.grad = None
         self._sh_rebuild()
 
     # ---- the end of each backward: start the bucket's all-reduce on the step's last
@@ -254,6 +267,13 @@ class GradAllReduce:
         if self._backwards > self.views_per_step:
             raise RuntimeError(f"GradAllReduce: {self._backwards} backwards in one step (views_per_step="
                                f"{self.views_per_step}); the bucket's all-reduce already started")
+        if self._early and self._backwards == self.views_per_step:
+            extra = [(i, p.grad) for i, p in enumerate(self._reduced) if p.grad is not None]
+            if extra:
+                flat = torch.cat([g.detach().reshape(-1).to(torch.float32) for _, g in extra])
+                work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                self._extra = ([i for i, _ in extra], flat, work)
+            return
         if self._backwards == self.views_per_step and self._work is None and not self._stale():
             bucket = self._pack()
             self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -347,6 +367,14 @@ class GradAllReduce:
             else:
                 p.grad.add_(g)
 
+    def _split(self, flat, idx):
+        out, off = [], 0
+        for i in idx:
+            n = self._reduced[i].numel()
+            out.append(flat[off:off + n])
+            off += n
+        return out
+
     def remove_hooks(self) -> None:
         for h in self._hooks:
             h.remove()
@@ -397,7 +425,7 @@ class GradAllReduce:
         of the backward, or packed and reduced here when it was not: flat mode, a
         parameter swap, fewer backwards than announced), then the SH gradients from
         the gathered colour gradients (SH exchange on).  Returns the bucket."""
-        if self._stale():
+        if self._stale() and not self._early:
             # the model's tensors were replaced since the hooks were bound (densify /
             # prune): their gradients go through the bucket here, and the hooks move
             # to them for the next step
@@ -412,11 +440,23 @@ class GradAllReduce:
         # all-reduce is still in flight (queued at the end of the backward already,
         # unless nothing started there), and the compute stream waits for the bucket last
         self._sh_rebuild()
+        if self._early and self._bucket._version != self._early_version:
+            raise RuntimeError("GradAllReduce: the bucket was written while its all-reduce was in flight")
         self._begin("exchange_wait")
         if self._work is not None:
             self._work.wait()
+        if self._extra is not None:
+            self._extra[2].wait()
         self._end("exchange_wait")
+        if self._early:  # the views become the leaves' .grad again, plus what came after the start
+            extra = dict(zip(self._extra[0], self._split(self._extra[1], self._extra[0]))) if self._extra else {}
+            for i, (p, v) in enumerate(zip(self._reduced, self._views)):
+                if i in extra:
+                    v.add_(extra[i].view_as(v))
+                p.grad = v
         self._tstats["calls"] += 1
+        self._early = False
+        self._extra = None
         self._work = None
         self._bucket = self._views = None  # the grads keep the storage; next step gets a fresh bucket
         self._backwards = 0

@@ -105,6 +105,32 @@ def pmc_traffic(stage: str):
     return float(v) if v is not None else None
 
 
+def pmc_unit_bytes(key: str):
+    """profiles/pmc_summary.json's measured HBM bytes of one benchmark unit (every gsr
+    kernel's per-dispatch bytes x dispatches per unit; tools/pmc_summary.py), or None."""
+    f = ROOT / "profiles" / "pmc_summary.json"
+    try:
+        v = json.loads(f.read_text()).get("units", {}).get(key, {}).get("hbm_bytes_per_unit")
+    except (OSError, ValueError):
+        return None
+    return float(v) if v is not None else None
+
+
+def measured_frac(key: str, units_per_s: float):
+    """The iteration-level HBM roofline from the PMC-measured bytes per unit (VERDICT r4:
+    beside §8(d)'s model figure), or None without a PMC record for this workload."""
+    b = pmc_unit_bytes(key)
+    return round(b * units_per_s / 1e9 / HBM_PEAK_GBS, 4) if b else None
+
+
+def num_rendered_seen() -> int:
+    """num_rendered of the last forward the binding ran (the benchmarked view, read after
+    the warm-up: no extra forward, so PMC runs count whole units)."""
+    from diff_gaussian_rasterization import _C
+
+    return int(_C.last_forward.get("num_rendered", 0))
+
+
 def _host_cpu() -> dict:
     """Core count (`nproc`, which honours the box's CPU share / OMP_NUM_THREADS) and
     the CPU model name (lscpu's "Model name", from /proc/cpuinfo)."""
@@ -237,6 +263,8 @@ def main():
                          "with the fused loss kernel; 'reference' is the reference's render() + torch loss")
     ap.add_argument("--glue-steps", type=int, default=100,
                     help="N=1: timed steps of the same unit with the other glue, reported beside; 0 = skip")
+    ap.add_argument("--config-b-steps", type=int, default=200,
+                    help="N=1: timed steps of config B (100k, 800x800, SH3, fwd+bwd) reported beside; 0 = skip")
     args = ap.parse_args()
 
     import torch
@@ -286,11 +314,10 @@ def main():
             reducer()  # wait for the exchange started inside backward (+ rebuild the SH gradients)
         return out
 
-    # the instances of this rank's view (the byte model), found before the warm-up
-    I = _last_num_rendered(cam, g, bg)
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1)):
         out = one_step()
     torch.cuda.synchronize()
+    I = num_rendered_seen()  # the instances of this rank's view (the byte model)
     if world > 1:
         dist.barrier()
     # Stage split (HIP events on the launch stream around every rasterizer stage,
@@ -311,8 +338,11 @@ def main():
         reducer.reset_stats()
         dist.barrier()
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         out = one_step()
+        host += time.perf_counter() - h0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -382,6 +412,12 @@ def main():
             "raster_ms": raster_ms(per_stage),
             "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
             "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * value / world / 1e9 / HBM_PEAK_GBS, 4),
+            # the same with the PMC-measured HBM bytes per unit (profiles/pmc_summary.json,
+            # tools/pmc.sh on the default footprint and glue; null for other workloads)
+            "iter_hbm_frac_measured": (measured_frac("unit", value / world)
+                                       if args.config == "C" and args.glue == "fused" else None),
+            # host time inside one_step per step (launches, autograd, the one read-back wait)
+            "host_ms_per_step": round(1e3 * host / steps, 4),
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -407,6 +443,19 @@ def main():
             other = "reference" if args.glue == "fused" else "fused"
             line[f"{other}_glue"] = glue_rates(cam, g, target, bg, other, args.glue_steps, args.warmup,
                                                args.lambda_dssim)
+        if world == 1:
+            # the unmodified drop-in: the reference's render() (gaussian_renderer/__init__.py:
+            # 98-106) and torch L1 over this library, next to the headline (which uses the
+            # stored-parameter render + fused L1: INTEGRATION.md's caller edit)
+            dr = line if args.glue == "reference" else line.get("reference_glue")
+            if dr:
+                line["dropin"] = {"value": dr["value"], "unit": "train-iters/s", "ms_per_step": dr["ms_per_step"],
+                                  "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * dr["value"] / 1e9
+                                                         / HBM_PEAK_GBS, 4),
+                                  "glue": GLUE_NOTE["reference"]}
+        if world == 1 and args.config_b_steps > 0 and args.config == "C":
+            line["config_B"] = train_config_rates("B", dev, args.config_b_steps, args.warmup, args.glue,
+                                                  args.lambda_dssim)
         if world == 1 and args.full_steps > 0:
             line["full_step"] = full_step_rates(cam, P, deg, target, bg, args.full_steps)
         if world == 1 and args.render_steps > 0:
@@ -483,9 +532,9 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
     mode = "tight" if _C.get_footprint() == "rect" else "rect"
     prev = set_footprint(mode)
     try:
-        I = _last_num_rendered(cam, g, bg)
-        for _ in range(warmup):
+        for _ in range(max(warmup, 1)):
             one_step()
+        I = num_rendered_seen()
         per, _ = stage_split(one_step, steps)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -497,6 +546,7 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
         set_footprint(prev)
     P, W, H, M = g.xyz.shape[0], cam.image_width, cam.image_height, g.features_rest.shape[1] + 1
     return {"footprint": mode, "value": round(steps / dt, 3), "unit": "train-iters/s",
+            "iter_hbm_frac_measured": measured_frac("unit_" + mode, steps / dt),
             "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps, "num_rendered": I,
             "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "stages_source": STAGES_SOURCE["split"],
             "raster_ms": raster_ms(per), "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
@@ -538,6 +588,59 @@ def glue_rates(cam, g, target, bg, glue: str, steps: int, warmup: int, lambda_ds
     return {"glue": GLUE_NOTE[glue], "value": round(steps / dt, 3), "unit": "train-iters/s",
             "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps,
             "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "raster_ms": raster_ms(per)}
+
+
+def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, lambda_dssim: float) -> dict:
+    """Another training config's unit (B: 100k Gaussians, 800x800, SH3, render -> L1
+    -> backward) at N = 1, the same way as the headline: stage split, timed steps,
+    §8(d)'s iteration roofline, and the host's share (ms_per_step against the
+    rasterizer's own device time, raster_ms)."""
+    import torch
+
+    import synthetic
+    import train_step
+
+    cfg = synthetic.CONFIGS[cfg_name]
+    P, W, H, deg = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
+    M = (deg + 1) ** 2
+    cam = synthetic.make_camera(W, H, view=0).to(dev)
+    g = synthetic.make_gaussians(P, deg, seed=0).to(dev, requires_grad=True)
+    target = synthetic.make_target(W, H, seed=1).to(dev)
+    bg = torch.zeros(3, device=dev)
+    params = g.params()
+
+    def step():
+        for p in params:
+            p.grad = None
+        train_step.train_step(cam, g, target, bg, lambda_dssim=lambda_dssim, glue=glue)
+
+    for _ in range(max(warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    I = num_rendered_seen()
+    per, _ = stage_split(step, steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    host = 0.0
+    for _ in range(steps):
+        h0 = time.perf_counter()
+        step()
+        host += time.perf_counter() - h0
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del g, params
+    ms = 1e3 * dt / steps
+    rms = raster_ms(per)
+    return {"metric": f"train iters/sec (fwd+bwd) + Mpix/sec, {W}x{H}, {P} Gaussians, SH{deg}",
+            "value": round(steps / dt, 3), "unit": "train-iters/s", "ms_per_step": round(ms, 4), "steps": steps,
+            "mpix_per_s": round(steps / dt * W * H / 1e6, 2),
+            "config": {"workload": f"{cfg_name}: {WORKLOADS[cfg_name]}", "gaussians": P, "width": W, "height": H,
+                       "sh_degree": deg, "num_rendered": I, "glue": GLUE_NOTE[glue]},
+            "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "raster_ms": rms,
+            "host_ms_per_step": round(1e3 * host / steps, 4),
+            "ms_per_step_vs_raster_ms": round(ms / rms, 3) if rms else None,
+            "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
+            "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * steps / dt / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmup: int, plain_ms: float,
@@ -633,11 +736,11 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
     cam = synthetic.make_camera(W, H, view=view).to(dev)
     g = synthetic.make_gaussians(P, deg, seed=0).to(dev)
     bg = torch.zeros(3, device=dev)
-    I = _last_num_rendered(cam, g, bg)
     render = train_step.render_fused if glue == "fused" else train_step.render
     with torch.no_grad():
-        for _ in range(warmup):
+        for _ in range(max(warmup, 1)):
             render(cam, g, bg)
+        I = num_rendered_seen()
         # the largest stage by measured time, from a steady-state block of its own
         per, dom = stage_split(lambda: render(cam, g, bg), steps)
         _C.timing_enable([dom])  # only the dominant stage inside the timed region
@@ -653,6 +756,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
     ab = algorithmic_bytes(dom, P, I, W, H, M)
     achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     fps = steps / dt
+    sfx = "" if _C.get_footprint() == "tight" else "_" + _C.get_footprint()
     res = {
         "metric": render_metric(cfg_name), "value": round(fps, 3), "unit": "frames/s", "ms_per_frame": round(1e3 * dt / steps, 4),
         "mpix_per_s": round(fps * W * H / 1e6, 2), "steps": steps, "warmup": warmup,
@@ -662,7 +766,9 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
         "stages_source": STAGES_SOURCE["split"],
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic(f"{dom}_{cfg_name}"),
+                     # PMC bytes of this workload's own pass: keyed by config and footprint
+                     # (the default tight pass is "<stage>_E", upstream's rect "<stage>_E_rect")
+                     "traffic": pmc_traffic(f"{dom}_{cfg_name}{sfx}"),
                      "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(dom_ms, 4)},
     }
     fwd_bytes = sum(algorithmic_bytes(k, P, I, W, H, M) for k in
@@ -672,6 +778,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
     res["raster_ms"] = raster_ms(per)
     res["iter_algorithmic_bytes"] = iter_bytes(P, I, W, H, M, backward=False)  # §8(d)'s forward formula
     res["iter_hbm_frac"] = round(res["iter_algorithmic_bytes"] * fps / 1e9 / HBM_PEAK_GBS, 4)
+    res["iter_hbm_frac_measured"] = measured_frac(f"unit_{cfg_name}{sfx}", fps) if glue == "fused" else None
     del g
     torch.cuda.empty_cache()
     return res
@@ -736,22 +843,6 @@ def full_step_rates(cam, P: int, deg: int, target, bg, steps: int) -> dict:
         out[name] = {"it_per_s": round(steps / dt, 2), "ms_per_step": round(1e3 * dt / steps, 3)}
         del g, st
     return out
-
-
-def _last_num_rendered(cam, g, bg) -> int:
-    """num_rendered of the benchmarked view (forward only, outside the timed region)."""
-    import math
-
-    import torch
-    from diff_gaussian_rasterization import _C
-
-    with torch.no_grad():
-        res = _C.rasterize_gaussians(bg, g.get_xyz, torch.empty(0, device=bg.device), g.get_opacity, g.get_scaling,
-                                     g.get_rotation, 1.0, torch.empty(0, device=bg.device), cam.world_view_transform,
-                                     cam.full_proj_transform, math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5),
-                                     cam.image_height, cam.image_width, g.get_features, g.active_sh_degree,
-                                     cam.camera_center, False, False)
-    return int(res[0])
 
 
 if __name__ == "__main__":

@@ -27,13 +27,18 @@
  * nonzero gsr_status; gsr_last_error() then describes the failure
  * (thread-local string).
  *
- * Forward is two calls because the binning buffer's size depends on
- * num_rendered, which needs one device->host read (upstream does the same
- * cudaMemcpy inside Rasterizer::forward):
- *   1. gsr_forward_preprocess: per-Gaussian projection, SH, tile counts, scan
- *      -> *num_rendered (host), synchronises `stream` once;
- *   2. caller allocates gsr_binning_bytes(num_rendered, W, H) bytes;
- *   3. gsr_forward_render: bucket by tile, per-tile depth sort, blend.
+ * The binning buffer's size depends on num_rendered, which needs one
+ * device->host read (upstream does the same cudaMemcpy inside
+ * Rasterizer::forward).  Two ways to run the forward:
+ *   - gsr_forward (one call): the caller passes a binning buffer of a guessed
+ *     capacity (e.g. the last num_rendered of this scene plus a margin); the
+ *     whole forward is queued before the host waits for the count, so the
+ *     device never idles on the read-back.  If the count exceeds the capacity
+ *     it returns GSR_NEED_BINNING with *num_rendered set, and the caller
+ *     finishes with gsr_forward_render on a buffer of that size;
+ *   - gsr_forward_preprocess -> *num_rendered (synchronises `stream` once), the
+ *     caller allocates gsr_binning_bytes(num_rendered, W, H) bytes, then
+ *     gsr_forward_render: bucket by tile, per-tile depth sort, blend.
  */
 #ifndef GSR_H
 #define GSR_H
@@ -45,14 +50,16 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 9
+#define GSR_ABI_VERSION 10
 
 enum gsr_status {
     GSR_OK = 0,
     GSR_ERR_ARGS = 1,        /* bad sizes / pointer combination (upstream AT_ERROR / Exception) */
     GSR_ERR_HIP = 2,         /* HIP runtime error (launch failure, fault) */
     GSR_ERR_PREFILTERED = 3, /* a point was culled although prefiltered=1 (upstream __trap) */
-    GSR_ERR_CAPACITY = 4     /* image/tile count beyond the supported range */
+    GSR_ERR_CAPACITY = 4,    /* image/tile count beyond the supported range */
+    GSR_NEED_BINNING = 5     /* gsr_forward: num_rendered exceeds the binning buffer's capacity (not an error:
+                                preprocess is done, finish with gsr_forward_render on a bigger buffer) */
 };
 
 /* Tile footprint of a Gaussian (which of its bounding-rect tiles get a list
@@ -70,12 +77,13 @@ enum gsr_status {
 enum gsr_footprint { GSR_FOOTPRINT_RECT = 0, GSR_FOOTPRINT_TIGHT = 1 };
 
 /* gsr_inputs.flags.  GSR_FLAG_PREPARE_BACKWARD (forward calls; not upstream):
- * a backward will follow, so gsr_forward_render also zeroes the backward's
- * gradient accumulator (inside the geom buffer) on the library's second stream
- * while the blend runs, and files the quadrants for the backward's wave order —
- * work the backward then skips (its accum argument NULL: the geom buffer's
- * accumulator; a second backward of the same forward zeroes it again itself).
- * Only a speed hint: every backward is correct with or without it. */
+ * a backward will follow, so the blend kernel also zeroes the backward's
+ * gradient accumulator (inside the geom buffer) and a small launch after it files
+ * the quadrants for the backward's wave order — work the backward then skips
+ * (its accum argument NULL: the geom buffer's accumulator; a second backward of
+ * the same forward zeroes it again itself).  Only a speed hint: every backward
+ * is correct with or without it, and any number of forward renders may follow
+ * one preprocess (each files its own quadrants afresh). */
 enum gsr_flags { GSR_FLAG_PREPARE_BACKWARD = 1, GSR_FLAG_L1_SEED = 2 };
 
 /* GSR_FLAG_L1_SEED (backward calls; not upstream): the image's gradient is that of
@@ -146,7 +154,9 @@ typedef struct gsr_inputs {
 /* Scratch sizes in bytes (all buffers 256-byte aligned internally).
  * geom:    per-Gaussian state + per-tile counting scratch (upstream GeometryState),
  *          and the backward's gradient accumulator (64 B per Gaussian)
- * binning: per-instance keys and the sorted point list (upstream BinningState)
+ * binning: per-instance keys and the sorted point list (upstream BinningState),
+ *          for a capacity of num_rendered instances or more; the point list sits
+ *          at offset 0 whatever the capacity (the backward needs only the pointer)
  * img:     per-pixel final T / contributor counts (ImageState)
  * accum:   a separate backward accumulator (64 B per Gaussian), for callers that
  *          pass one to a backward instead of NULL (the geom buffer's) */
@@ -158,9 +168,7 @@ size_t gsr_accum_bytes(int32_t P);
 /* Replaces the first half of RasterizeGaussiansCUDA -> Rasterizer::forward
  * (preprocess + InclusiveSum + the num_rendered cudaMemcpy).  The device also
  * sorts the P Gaussians by depth (the first half of the binning, see
- * 3dgs_study_amd/csrc/binning.hip), on a second stream of the library's own
- * (one per host thread and device) that forks from and joins back into `stream`
- * inside this call: the caller sees one stream.
+ * 3dgs_study_amd/csrc/binning.hip), in line on `stream` after preprocess.
  * Writes radii [P] int32 and *num_rendered (host pointer). */
 int gsr_forward_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int64_t *num_rendered, void *stream);
 
@@ -182,6 +190,23 @@ int gsr_forward_render(const gsr_inputs *in, void *geom, void *binning, void *im
 int gsr_forward_render_l1(const gsr_inputs *in, void *geom, void *binning, void *img, int64_t num_rendered,
                           const int32_t *radii, float *out_color, const float *gt, float *loss_out,
                           uint8_t *visible_out, void *stream);
+
+/* The whole of Rasterizer::forward in one call (not an upstream entry point; the
+ * Python binding's _C.rasterize_gaussians uses it once it knows a capacity for the
+ * scene): gsr_forward_preprocess + gsr_forward_render(_l1), with emit, the tile
+ * sort, the blend (and with gt the L1 loss, as gsr_forward_render_l1; gt NULL: no
+ * loss, loss_out / visible_out unused) queued BEFORE the host waits for
+ * num_rendered, into `binning`, a buffer of gsr_binning_bytes(capacity, W, H) bytes.
+ * Each binning kernel reads the published count on the device and does nothing
+ * unless it fits.  Returns GSR_OK (*num_rendered <= capacity: every output is
+ * written, as by the two-call form) or GSR_NEED_BINNING (*num_rendered >
+ * capacity: radii and the geom buffer are complete, the rest is not — the caller
+ * allocates gsr_binning_bytes(*num_rendered, W, H) and calls gsr_forward_render /
+ * gsr_forward_render_l1 with it).  Debug mode runs the two-call sequence inside
+ * the call.  Results are bit-identical to the two-call form. */
+int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning, int64_t capacity, void *img,
+                float *out_color, const float *gt, float *loss_out, uint8_t *visible_out, int64_t *num_rendered,
+                void *stream);
 
 /* Replaces RasterizeGaussiansBackwardCUDA -> Rasterizer::backward.
  * accum: NULL = the accumulator inside geom (zeroed by a forward called with
@@ -329,8 +354,8 @@ enum gsr_geom_field {
     GSR_GEOM_NFIELDS
 };
 enum gsr_binning_field {
-    GSR_BIN_KEYS = 0,        /* uint32 [I]  tile index of each point_list entry (sorted) */
-    GSR_BIN_POINT_LIST,      /* uint32 [I]  Gaussian ids in (tile, depth, id) order */
+    GSR_BIN_KEYS = 0,        /* uint32 [cap] tile-sort scratch */
+    GSR_BIN_POINT_LIST,      /* uint32 [I]  Gaussian ids in (tile, depth, id) order: offset 0 */
     GSR_BIN_NFIELDS
 };
 enum gsr_img_field {
@@ -344,7 +369,7 @@ enum gsr_img_field {
 int gsr_point_list_keys(int32_t P, int32_t W, int32_t H, const void *geom, const void *binning,
                         int64_t num_rendered, uint64_t *keys, void *stream);
 int gsr_geom_layout(int32_t P, int32_t W, int32_t H, size_t *offsets, int cap);
-int gsr_binning_layout(int64_t num_rendered, int32_t W, int32_t H, size_t *offsets, int cap);
+int gsr_binning_layout(int64_t capacity, int32_t W, int32_t H, size_t *offsets, int cap);
 int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap);
 
 /* Per-stage device timing (HIP events on the launch stream), for benchmarks.
@@ -356,15 +381,13 @@ int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap);
 enum gsr_stage {
     GSR_STAGE_PREPROCESS = 0, /* FORWARD::preprocessCUDA */
     GSR_STAGE_SCAN,           /* InclusiveSum of tiles_touched: the rects in depth order + emission offsets */
-    GSR_STAGE_DEPTH_SORT,     /* stable sort of the P depths (in line; with the side stream: the wait for it) */
+    GSR_STAGE_DEPTH_SORT,     /* stable sort of the P depths */
     GSR_STAGE_DUPLICATE,      /* duplicateWithKeys in depth order */
     GSR_STAGE_TILE_SORT,      /* stable sort by tile (SortPairs) + identifyTileRanges */
     GSR_STAGE_RENDER_FWD,     /* FORWARD::renderCUDA */
     GSR_STAGE_RENDER_BWD,     /* BACKWARD::renderCUDA */
     GSR_STAGE_PREPROCESS_BWD, /* BACKWARD::computeCov2DCUDA + preprocessCUDA */
     GSR_STAGE_BWD_PREPARE,    /* accumulator zeroing + the render backward's wave order (no upstream kernel) */
-    GSR_STAGE_DSORT_CONCURRENT, /* GSR_SIDE_STREAM=1 only: the depth sort on the library's second stream beside
-                                   preprocess; GSR_STAGE_DEPTH_SORT is then its exposed part (the launch stream's wait) */
     GSR_STAGE_EXCHANGE_WAIT,  /* caller-marked (gsr_timing_begin/end): the view-parallel exchange's wait for its collectives */
     GSR_STAGE_SH_REBUILD,     /* caller-marked: the SH gradients rebuilt from the gathered colour records */
     GSR_STAGE_COUNT

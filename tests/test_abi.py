@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 9
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 10
     assert ctypes.sizeof(_C.GsrL1Seed) == 32  # struct gsr_l1_seed: three pointers and an int64
     # 12 x 4-byte scalars, 11 pointers, then sh_rest and two int32 (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 48 + 12 * 8 + 8
@@ -56,7 +56,11 @@ def test_scratch_layouts_are_aligned_and_disjoint(lib):
         for d in (g, b, im):
             offs = list(d.values())
             assert all(o % 256 == 0 for o in offs)
-            assert offs == sorted(offs) and len(set(offs)) == len(offs)
+            assert len(set(offs)) == len(offs)
+        assert list(g.values()) == sorted(g.values()) and list(im.values()) == sorted(im.values())
+        # the point list sits at offset 0 whatever the capacity (gsr_forward's
+        # buffers are sized before the count is known; the backward needs the pointer)
+        assert b["point_list"] == 0 and b["keys"] >= 4 * I
         assert lib.gsr_geom_bytes(P, W, H) > g["ctrl"]
         assert lib.gsr_binning_bytes(I, W, H) >= I * 12
         assert lib.gsr_img_bytes(W, H) >= W * H * 8
@@ -125,9 +129,9 @@ def test_sh_exchange_entry_points_validate(lib):
 def test_stage_names(lib):
     from diff_gaussian_rasterization import _C
 
-    names = [lib.gsr_stage_name(i).decode() for i in range(12)]
+    names = [lib.gsr_stage_name(i).decode() for i in range(11)]
     assert names == ["preprocess", "scan", "depth_sort", "duplicate", "tile_sort", "render_fwd", "render_bwd",
-                     "preprocess_bwd", "bwd_prepare", "depth_sort_concurrent", "exchange_wait", "sh_rebuild"]
+                     "preprocess_bwd", "bwd_prepare", "exchange_wait", "sh_rebuild"]
     assert lib.gsr_stage_name(99).decode() == ""
     _C.timing_enable(True)
     assert _C.timing_read() == {n: (0.0, 0) for n in names}
@@ -235,3 +239,76 @@ def test_l1_grad_validates(lib):
     # with lambda 0 the loss alone may be asked for (no gradient map), else it is required
     assert lib.gsr_l1_ssim(1, 1, 3, 4, 4, ctypes.c_float(0.5), None, 1, 1, None) != 0
     assert "NULL" in lib.gsr_last_error().decode()
+
+
+def test_forward_one_call_validates(lib):
+    """gsr_forward (the one-call forward, binning sized before the count is known):
+    host-side checks only."""
+    s = _inputs()
+    n = ctypes.c_int64(-1)
+    # (in, geom, radii, binning, capacity, img, out_color, gt, loss_out, visible_out, num_rendered, stream)
+    assert lib.gsr_forward(ctypes.byref(s), 1, 1, 1, 16, 1, 1, None, None, None, None, None) != 0
+    assert "num_rendered is NULL" in lib.gsr_last_error().decode()
+    assert lib.gsr_forward(ctypes.byref(s), 1, 1, 1, -1, 1, 1, None, None, None, ctypes.byref(n), None) != 0
+    assert "capacity out of range" in lib.gsr_last_error().decode()
+    assert lib.gsr_forward(ctypes.byref(s), 1, 1, 1, 1 << 32, 1, 1, None, None, None, ctypes.byref(n), None) != 0
+    assert lib.gsr_forward(ctypes.byref(s), 1, 1, 1, 16, 1, None, None, None, None, ctypes.byref(n), None) != 0
+    assert "out_color is NULL" in lib.gsr_last_error().decode()
+    assert lib.gsr_forward(ctypes.byref(s), 1, 1, 1, 16, 1, 1, 1, None, None, ctypes.byref(n), None) != 0
+    assert "loss_out and img required" in lib.gsr_last_error().decode()
+    assert lib.gsr_forward(ctypes.byref(s), 1, 1, 1, 16, 1, 1, None, None, 1, ctypes.byref(n), None) != 0
+    assert "visible_out needs gt" in lib.gsr_last_error().decode()
+    assert lib.gsr_forward(ctypes.byref(s), None, 1, 1, 16, 1, 1, None, None, None, ctypes.byref(n), None) != 0
+    assert "scratch buffers are NULL" in lib.gsr_last_error().decode()
+    assert n.value == 0
+    bad = _inputs(D=3, M=4)
+    assert lib.gsr_forward(ctypes.byref(bad), 1, 1, 1, 16, 1, 1, None, None, None, ctypes.byref(n), None) != 0
+    assert "degree 3 needs 16" in lib.gsr_last_error().decode()
+
+
+def test_binning_capacity_policy():
+    """The binding's capacity for gsr_forward: none before the first forward of an
+    image size and footprint, then the last count scaled by the Gaussian count with
+    a margin; it grows at once and shrinks by 1/128 per forward."""
+    from diff_gaussian_rasterization import _C
+
+    key = (123, 45, 1)
+    _C._capacity_level.pop(key, None)
+    assert _C._capacity_for(key, 1000) is None
+    _C._note_count(key, 1000, 50_000)
+    cap = _C._capacity_for(key, 1000)
+    assert cap == int(50_000 * _C._CAP_SLACK) + _C._CAP_PAD
+    assert _C._capacity_for(key, 2000) == int(100_000 * _C._CAP_SLACK) + _C._CAP_PAD  # densified: scaled
+    _C._note_count(key, 1000, 10_000)  # a sparse view: the level decays, it does not drop
+    assert _C._capacity_level[key] == (1000, 50_000 - (50_000 >> 7))
+    _C._note_count(key, 1000, 80_000)
+    assert _C._capacity_level[key] == (1000, 80_000)
+    prev = _C.capacity_override
+    try:
+        _C.capacity_override = 7
+        assert _C._capacity_for(key, 1000) == 7
+        _C.capacity_override = 0
+        assert _C._capacity_for(key, 1000) is None
+    finally:
+        _C.capacity_override = prev
+        _C._capacity_level.pop(key, None)
+
+
+def test_bench_measured_roofline_helpers():
+    """bench.py's iteration roofline from PMC bytes: per-unit bytes come
+    from profiles/pmc_summary.json's "units" records (tools/pmc_summary.py), keyed by
+    workload and footprint; a workload without a record reports null, never a guess."""
+    import json as _json
+    import sys as _sys
+
+    _sys.path.insert(0, str(ROOT))
+    import bench
+
+    assert bench.pmc_unit_bytes("unit_no_such_workload") is None
+    assert bench.measured_frac("unit_no_such_workload", 1000.0) is None
+    f = ROOT / "profiles" / "pmc_summary.json"
+    units = _json.loads(f.read_text()).get("units", {})
+    for key, rec in units.items():
+        b = rec["hbm_bytes_per_unit"]
+        assert b > 0 and rec["units"] > 0
+        assert bench.measured_frac(key, 1000.0) == round(b * 1000.0 / 1e9 / bench.HBM_PEAK_GBS, 4)

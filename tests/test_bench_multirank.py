@@ -57,3 +57,27 @@ def test_bench_multirank_line(n, exchange):
     assert ex["bytes_per_rank"] == 4 * floats * P + record
     # the fused leaf gradients survive the exchange: the rasterizer writes them into the bucket
     assert set(ex["fused_leaves"]) >= {"means3D", "opacities", "rotations", "scales"}
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_single_gpu_line_fields():
+    """The N = 1 line carries what VERDICT r4 asked beside the headline: the
+    unmodified drop-in's rate and roofline (``dropin``), the PMC-measured iteration
+    roofline key, the host's time per step, and config B's own sub-line."""
+    cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--full-steps", "0",
+           "--render-steps", "2", "--footprint-steps", "3", "--exchange-steps", "0", "--glue-steps", "3",
+           "--config-b-steps", "3"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["config"]["num_rendered"] > 0
+    assert d["dropin"]["value"] == d["reference_glue"]["value"] > 0
+    assert 0 < d["dropin"]["iter_hbm_frac"] < d["iter_hbm_frac"]
+    assert "iter_hbm_frac_measured" in d and d["host_ms_per_step"] > 0
+    b = d["config_B"]
+    assert b["config"]["gaussians"] == 100_000 and b["config"]["width"] == b["config"]["height"] == 800
+    assert b["value"] > 0 and b["raster_ms"] > 0 and b["iter_hbm_frac"] > 0
+    assert set(b["stages_ms"]) >= {"preprocess", "render_fwd", "render_bwd", "preprocess_bwd"}
+    e = d["config_E_render_rect"]
+    assert e["config"]["footprint"] == "rect" and "iter_hbm_frac_measured" in e

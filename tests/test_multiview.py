@@ -902,3 +902,49 @@ def test_bucket_started_by_the_rasterizer_gloo_world2(views_per_step):
     for a, b, x in zip(g0, g1, p):
         assert torch.equal(a, b)
         torch.testing.assert_close(a, 2 * wsum * x, rtol=1e-6, atol=1e-6)
+
+
+def _late_path_worker(rank, world, port, out, views_per_step):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    xyz, opacity = (torch.randn(s, requires_grad=True) for s in ((7, 3), (7, 1)))
+    ar = GradAllReduce([xyz, opacity], views_per_step=views_per_step)
+    _AllWriter.started = []
+    c = 0.5 * (rank + 1)
+    for v in range(views_per_step):
+        # a regulariser on a reduced leaf, formed before the render: AccumulateGrad(opacity)
+        # waits for both paths, so it runs AFTER the writer started the bucket's all-reduce
+        reg = c * (opacity * opacity).sum()
+        (reg + _AllWriter.apply(xyz, opacity, float(rank + 1) * (v + 1))).backward()
+    started = list(_AllWriter.started)
+    flat = ar()
+    views_ok = all(flat.data_ptr() <= p.grad.data_ptr() < flat.data_ptr() + flat.numel() * 4 for p in (xyz, opacity))
+    out[rank] = ([p.grad.clone() for p in (xyz, opacity)], [p.detach().clone() for p in (xyz, opacity)], started,
+                 views_ok)
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("views_per_step", [1, 2])
+def test_late_gradient_path_after_early_start_gloo_world2(views_per_step):
+    """once the rasterizer has started the bucket's all-reduce, a
+    gradient that another loss term sends into a reduced leaf later in the same
+    backward must neither race with the collective nor be left out of it: it is
+    reduced on its own and added, and every rank ends with the full sum, bit-identical,
+    every .grad a view of the bucket again."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_late_path_worker, args=(2, port, out, views_per_step), nprocs=2, join=True)
+        res = dict(out)
+    (g0, p, s0, v0), (g1, _, s1, v1) = res[0], res[1]
+    assert s0 == s1 == [(0, 0)] * (views_per_step - 1) + [(0, 1)]  # the early start did happen
+    assert v0 and v1
+    wsum = sum(float(r + 1) * (v + 1) for r in (0, 1) for v in range(views_per_step))
+    creg = 2 * views_per_step * (0.5 + 1.0)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(g0[0], 2 * wsum * p[0], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(g0[1], (2 * wsum + creg) * p[1], rtol=1e-6, atol=1e-6)

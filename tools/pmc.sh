@@ -6,7 +6,7 @@ TAG=${1:-pmc}
 OUT=/tmp/$TAG  # raw CSVs stay on the box; the summary returns
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --full-steps 0 --render-steps 0 --footprint-steps 0 --exchange-steps 0 --glue-steps 0 ${PMC_ARGS:-}"
+CMD="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --full-steps 0 --render-steps 0 --footprint-steps 0 --exchange-steps 0 --glue-steps 0 --config-b-steps 0 ${PMC_ARGS:-}"
 i=0
 for SET in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_THREAD_CYCLES_VALU" \

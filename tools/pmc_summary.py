@@ -29,6 +29,7 @@ for k, cs in sorted(vals.items()):
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         hbm = 2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024
         line["hbm_bytes_per_launch"] = hbm
+        line["dispatches"] = len(cs["FETCH_SIZE"])
         for kn, st in STAGE.items():
             if k.startswith(kn):
                 summary["stages"][st + SUFFIX] = {"hbm_bytes_per_launch": hbm, "kernel": k}
@@ -74,9 +75,23 @@ def tile_sort_stage(kernels, titems, suffix=""):
     return None
 
 
-rec = tile_sort_stage(summary["kernels"], "16" if SUFFIX == "_E" else "8")
+rec = tile_sort_stage(summary["kernels"], "16" if SUFFIX.startswith("_E") else "8")
 if rec:
     summary["stages"]["tile_sort" + SUFFIX] = rec
+# One benchmark unit's measured HBM bytes (bench.py iter_hbm_frac_measured): every
+# gsr kernel's per-dispatch bytes times its dispatches, over the units the run made.
+# The run repeats one unit (tools/pmc.sh: warm-up, stage split and timed steps of
+# the same step; bench.py reads num_rendered from the warm-up, no extra forward), so
+# the anchor kernel — once per unit: render_bwd for a training step, render_fwd for
+# a forward-only config — counts the units.
+ks = {k: v for k, v in summary["kernels"].items() if "dispatches" in v}
+anchor = next((k for k in ks if k.startswith("gsr::render_bwd_kernel")), None) or \
+    next((k for k in ks if k.startswith("gsr::render_fwd_kernel")), None)
+if anchor:
+    units = ks[anchor]["dispatches"]
+    total = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in ks.values())
+    summary["units"] = {"unit" + SUFFIX: {"hbm_bytes_per_unit": total / units, "units": units, "anchor": anchor,
+                                          "kernels": sorted(ks)}}
 for st, rec in summary["stages"].items():
     frac = summary["kernels"].get(rec["kernel"], {}).get("valu_issue_frac")
     if frac is not None:
@@ -85,6 +100,7 @@ if out:
     if out.exists() and "--merge" in sys.argv:  # keep the other config's stages
         old = json.loads(out.read_text())
         old.get("stages", {}).update(summary["stages"])
+        old.setdefault("units", {}).update(summary.get("units", {}))
         old.get("kernels", {}).update({k + SUFFIX: v for k, v in summary["kernels"].items()})
         summary = old
     out.write_text(json.dumps(summary, indent=1) + "\n")

@@ -12,6 +12,8 @@ bash tools/prof.sh ${TAG}_C || exit 1
 bash tools/prof.sh ${TAG}_E --config E || exit 1
 bash tools/pmc.sh ${TAG} > /dev/null || exit 1
 PMC_ARGS="--config E" PMC_SUFFIX="_E --merge" PMC_TXT=_E bash tools/pmc.sh ${TAG} > /dev/null || exit 1
+# upstream's rect footprint at E (bench.py keys its PMC traffic by footprint)
+GSR_FOOTPRINT=rect PMC_ARGS="--config E" PMC_SUFFIX="_E_rect --merge" PMC_TXT=_E_rect bash tools/pmc.sh ${TAG} > /dev/null || exit 1
 echo profiles done
 if [ "${2:-}" != "skip-tests" ]; then
   timeout -k 10 1000 python -u -m pytest tests/ -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread \
