@@ -339,15 +339,11 @@ static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t
         return gt ? step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", dbg, s)
                   : GSR_OK;
     }
-    // the L1 loss's partial sums ride in the same launch as the quadrant filing
-    int l1_nb = 0;
+    // the L1 loss (partial sums and finish) rides in the same launch as the quadrant filing
     if (int rc = step(launch_bwd_prepare(*in, geom, img, (float *)acc, n > 0, true, true, s, gt ? out_color : nullptr,
-                                         gt, &l1_nb, radii, visible_out),
+                                         gt, loss_out, radii, visible_out),
                       "backward prepare", dbg, s))
         return rc;
-    if (gt)
-        if (int rc = step(launch_l1_finish(nullptr, nullptr, npix, l1_part, l1_nb, false, loss_out, s), "l1 loss", dbg, s))
-            return rc;
     prepared_set(geom, true);
     return GSR_OK;
 }

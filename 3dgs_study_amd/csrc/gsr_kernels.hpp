@@ -37,12 +37,13 @@ hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binni
                              float *acc_zero, size_t acc_bytes, hipStream_t s);
 
 // render_bwd.hip
-// l1 (forward only, or NULL): {image, gt, n} whose L1 partial sums (gsr_l1.hpp) the
-// same launch writes into img's l1_part; returns their count in *l1_nb.  visible
-// (forward only, or NULL): visible[i] = radii[i] > 0 in the same launch.
+// l1 (forward only, or NULL): the L1 loss mean|l1_x - l1_y| (n = 3 W H) into
+// l1_out [3], its partial sums and finish (gsr_l1.hpp) in the same launch; needs
+// render_fwd_kernel before it (the finish ticket).  visible (forward only, or
+// NULL): visible[i] = radii[i] > 0 in the same launch.
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
                               bool internal, bool forward, hipStream_t s, const float *l1_x = nullptr,
-                              const float *l1_y = nullptr, int *l1_nb = nullptr, const int32_t *radii = nullptr,
+                              const float *l1_y = nullptr, float *l1_out = nullptr, const int32_t *radii = nullptr,
                               uint8_t *visible = nullptr);
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, const void *img,
                              const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s);

@@ -21,8 +21,10 @@ __host__ __device__ inline int l1_blocks(size_t n) {
 // Block blk of nblk (L1_THREADS threads): sum |x - y| over its grid-stride share
 // (16-B loads; block 0 also takes the tail of a length that is not a multiple of 4)
 // into partials[2 blk] (and 0 into partials[2 blk + 1], the SSIM slot).
+// write_through: the two words leave as agent-scope (sc1) stores, for a consumer in
+// the same launch (l1_finish_last_block).
 __device__ __forceinline__ void l1_block_partial(const float *x, const float *y, size_t n, int blk, int nblk,
-                                                 float *partials) {
+                                                 float *partials, bool write_through = false) {
     __shared__ float wsum[L1_THREADS / 64];
     const size_t n4 = n >> 2, stride = (size_t)nblk * L1_THREADS;
     const float4 *x4 = reinterpret_cast<const float4 *>(x), *y4 = reinterpret_cast<const float4 *>(y);
@@ -41,8 +43,56 @@ __device__ __forceinline__ void l1_block_partial(const float *x, const float *y,
         float tot = 0.f;
 #pragma unroll
         for (int k = 0; k < L1_THREADS / 64; k++) tot += wsum[k];
-        partials[2 * blk] = tot;
-        partials[2 * blk + 1] = 0.f;
+        if (write_through) {
+            __hip_atomic_store(&partials[2 * blk], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&partials[2 * blk + 1], 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            partials[2 * blk] = tot;
+            partials[2 * blk + 1] = 0.f;
+        }
+    }
+}
+
+// The L1 loss's finish inside the partial sums' own launch: each block, after its
+// write-through partials, takes a ticket (agent-scope add after its stores drained);
+// the block that draws the last one reads every partial (sc1 loads: MI355X_MICROARCH
+// hand-off table, row 1) and forms the loss exactly as l1_ssim_finish_kernel does
+// with lambda 0 — its 1024 threads' double sums, emulated 4 per thread in the same
+// order, so the same bits — saving the finish launch and its boundary.  The ticket
+// word is zeroed by the launch before (render_fwd_kernel).
+__device__ __forceinline__ void l1_finish_last_block(const float *partials, int nb, uint32_t *ticket, float invN,
+                                                     float *out) {
+    __shared__ int last;
+    __shared__ double ws[16];
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partials have landed
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1u;
+    }
+    __syncthreads();
+    if (!last) return;
+    // virtual thread v = threadIdx.x + 256 j of the finish kernel's 1024: partial v
+    // (nb <= L1_BLOCKS = 1024), reduced per virtual wave by the same xor butterfly
+    static_assert(L1_THREADS == 256, "four virtual finish threads per thread");
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int v = (int)threadIdx.x + 256 * j;
+        double l1 = v < nb ? (double)__hip_atomic_load(&partials[2 * v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.0;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) l1 += __shfl_xor(l1, o);
+        if ((threadIdx.x & 63) == 0) ws[4 * j + w] = l1;  // virtual wave v / 64 = 4 j + w
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0;
+        for (int k = 0; k < 16; k++) a += ws[k];
+        const double lambda = 0.0, b = 0.0;
+        const float lam = 0.0f;
+        (void)lambda;
+        out[0] = (float)((1.0 - lam) * a * invN + lam * (1.0 - b * invN));
+        out[1] = (float)(a * invN);
+        out[2] = (float)(b * invN);
     }
 }
 

@@ -381,6 +381,10 @@ struct BwdPrepArgs {
     const float *l1_x, *l1_y;
     size_t l1_n;
     float *l1_part;
+    // ... and the last of them to finish forms the loss (gsr_l1.hpp l1_finish_last_block)
+    uint32_t *l1_ticket;
+    float l1_invN;
+    float *l1_out;
     // ... and workgroups after those write visible[i] = radii[i] > 0 (render()'s
     // visibility_filter), or NULL
     const int32_t *radii;
@@ -398,7 +402,8 @@ __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a
         return;
     }
     if ((int)blockIdx.x >= a.file_blocks) {  // workgroup-uniform: an L1 partial-sum block
-        l1_block_partial(a.l1_x, a.l1_y, a.l1_n, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_part);
+        l1_block_partial(a.l1_x, a.l1_y, a.l1_n, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_part, true);
+        l1_finish_last_block(a.l1_part, a.l1_nb, a.l1_ticket, a.l1_invN, a.l1_out);
         return;
     }
     const size_t tid = (size_t)blockIdx.x * PREP_THREADS + threadIdx.x;
@@ -441,7 +446,7 @@ __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a
 
 hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img, float *accum, bool file,
                               bool internal, bool forward, hipStream_t s, const float *l1_x, const float *l1_y,
-                              int *l1_nb, const int32_t *radii, uint8_t *visible) {
+                              float *l1_out, const int32_t *radii, uint8_t *visible) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -463,7 +468,9 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
     a.l1_n = (size_t)3 * in.W * in.H;
     a.l1_nb = l1_x ? l1_blocks(a.l1_n) : 0;
     a.l1_part = l1_x ? at<float>(const_cast<void *>(img), Im.l1_part) : nullptr;
-    if (l1_nb) *l1_nb = a.l1_nb;
+    a.l1_ticket = at<uint32_t>(const_cast<void *>(img), Im.l1_ticket);
+    a.l1_invN = 1.0f / (float)(double)a.l1_n;  // launch_l1_finish's invN
+    a.l1_out = l1_out;
     a.radii = radii;
     a.visible = visible;
     a.P = in.P;

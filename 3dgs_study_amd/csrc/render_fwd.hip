@@ -38,6 +38,7 @@ struct RenderFwdArgs {
     // workgroup 0: this forward's quadrants are filed afresh (bwd_prepare_kernel),
     // however many forwards ran on the geom buffer since its preprocess
     uint32_t *order_cnt;
+    uint32_t *l1_ticket;  // img's L1 finish ticket (gsr_l1.hpp), cleared by workgroup 0 for bwd_prepare_kernel
 };
 
 #ifndef GSR_FWD_GROUP
@@ -61,8 +62,10 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     };
     const QuadSlot qs = quad_slot(a.tiles);
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
-    if (blockIdx.x == 0)
+    if (blockIdx.x == 0) {
         for (int i = threadIdx.x; i < ORDER_FILED + 2; i += BLEND_THREADS) a.order_cnt[i] = 0u;
+        if (threadIdx.x == 0) *a.l1_ticket = 0u;
+    }
     if (tile < 0) {
         zero_slice();
         return;
@@ -238,6 +241,7 @@ hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binni
     a.zero4 = reinterpret_cast<float4 *>(acc_zero);
     a.zero_n4 = acc_zero ? acc_bytes / sizeof(float4) : 0;
     a.order_cnt = at<uint32_t>(geom, G.order_cnt);
+    a.l1_ticket = at<uint32_t>(img, Im.l1_ticket);
     hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
