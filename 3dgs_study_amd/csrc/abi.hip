@@ -83,6 +83,11 @@ struct StageTimer {
     size_t used = 0;
     double total_ms[GSR_STAGE_COUNT] = {};
     int64_t launches[GSR_STAGE_COUNT] = {};
+    // gsr_timing_sample: events on every `every`-th launch of a stage only (each
+    // event pair is a marker packet with a ~4 us idle gap behind it)
+    int every = 1;
+    int64_t seen[GSR_STAGE_COUNT] = {};
+    bool sampled[GSR_STAGE_COUNT] = {};
 };
 StageTimer g_timer;  // the ABI is driven from one host thread per process
 size_t g_open[GSR_STAGE_COUNT];  // gsr_timing_begin: the pool slot whose end event is pending, + 1
@@ -116,6 +121,9 @@ hipError_t take_pair(int st, std::pair<hipEvent_t, hipEvent_t> **out) {
 template <typename F>
 hipError_t timed(int st, hipStream_t s, F &&launch) {
     if (!(g_timer.mask & (1 << (st & 0xff)))) return launch();
+    const int k = st & 0xff;
+    if (!(st & TIMED_MORE)) g_timer.sampled[k] = g_timer.seen[k]++ % g_timer.every == 0;
+    if (!g_timer.sampled[k]) return launch();  // (more work of an unsampled launch: unsampled too)
     std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
     hipError_t e = take_pair(st, &ev);
     if (e != hipSuccess) return e;
@@ -647,9 +655,17 @@ int gsr_knn_mean_dist2(int32_t P, const float *points, float *dist2, void *scrat
     return check_hip(launch_knn(P, points, dist2, scratch, g_pinned, (hipStream_t)stream), "knn");
 }
 
+int gsr_timing_sample(int every) {
+    if (every < 1) return fail(GSR_ERR_ARGS, "timing sample period must be >= 1 (got %d)", every);
+    g_timer.every = every;
+    for (auto &n : g_timer.seen) n = 0;
+    return GSR_OK;
+}
+
 int gsr_timing_enable(int mask) {
     g_timer.mask = mask;
     g_timer.used = 0;
+    for (auto &n : g_timer.seen) n = 0;
     for (auto &o : g_open) o = 0;
     for (int k = 0; k < GSR_STAGE_COUNT; k++) {
         g_timer.total_ms[k] = 0;

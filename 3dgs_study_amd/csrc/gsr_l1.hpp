@@ -58,15 +58,26 @@ __device__ __forceinline__ void l1_block_partial(const float *x, const float *y,
 // the block that draws the last one reads every partial (sc1 loads: MI355X_MICROARCH
 // hand-off table, row 1) and forms the loss exactly as l1_ssim_finish_kernel does
 // with lambda 0 — its 1024 threads' double sums, emulated 4 per thread in the same
-// order, so the same bits — saving the finish launch and its boundary.  The ticket
-// word is zeroed by the launch before (render_fwd_kernel).
-__device__ __forceinline__ void l1_finish_last_block(const float *partials, int nb, uint32_t *ticket, float invN,
-                                                     float *out) {
+// order, so the same bits — saving the finish launch and its boundary.  Tickets are
+// two-level: 1024 adds on one word serialise (~88 per us), so block b adds to group
+// b mod 8's word and each group's last block to the top word.  The L1_TICKETS words
+// are zeroed by the launch before (render_fwd_kernel).
+constexpr int L1_TICKET_GROUPS = 8, L1_TICKETS = L1_TICKET_GROUPS + 1;
+constexpr int L1_TICKET_STRIDE = 32;  // words: each ticket on a 128-B line of its own
+__device__ __forceinline__ void l1_finish_last_block(const float *partials, int blk, int nb, uint32_t *tickets,
+                                                     float invN, float *out) {
     __shared__ int last;
     __shared__ double ws[16];
     if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partials have landed
-        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1u;
+        const int g = blk % L1_TICKET_GROUPS, ng = nb < L1_TICKET_GROUPS ? nb : L1_TICKET_GROUPS;
+        const uint32_t in_group = (uint32_t)((nb - g + L1_TICKET_GROUPS - 1) / L1_TICKET_GROUPS);
+        bool l = false;
+        if (__hip_atomic_fetch_add(&tickets[g * L1_TICKET_STRIDE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            in_group - 1u)
+            l = __hip_atomic_fetch_add(&tickets[L1_TICKET_GROUPS * L1_TICKET_STRIDE], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)ng - 1u;
+        last = l;
     }
     __syncthreads();
     if (!last) return;

@@ -403,7 +403,7 @@ __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a
     }
     if ((int)blockIdx.x >= a.file_blocks) {  // workgroup-uniform: an L1 partial-sum block
         l1_block_partial(a.l1_x, a.l1_y, a.l1_n, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_part, true);
-        l1_finish_last_block(a.l1_part, a.l1_nb, a.l1_ticket, a.l1_invN, a.l1_out);
+        l1_finish_last_block(a.l1_part, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_ticket, a.l1_invN, a.l1_out);
         return;
     }
     const size_t tid = (size_t)blockIdx.x * PREP_THREADS + threadIdx.x;

@@ -16,6 +16,7 @@
 // list order with their parameters broadcast from a per-wave LDS image.
 #include "gsr_blend.hpp"
 #include "gsr_kernels.hpp"
+#include "gsr_l1.hpp"
 
 namespace gsr {
 
@@ -64,7 +65,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     const int tile = qs.tile, w = qs.w, lane = threadIdx.x & 63;
     if (blockIdx.x == 0) {
         for (int i = threadIdx.x; i < ORDER_FILED + 2; i += BLEND_THREADS) a.order_cnt[i] = 0u;
-        if (threadIdx.x == 0) *a.l1_ticket = 0u;
+        if (threadIdx.x < L1_TICKETS) a.l1_ticket[threadIdx.x * L1_TICKET_STRIDE] = 0u;
     }
     if (tile < 0) {
         zero_slice();

@@ -64,7 +64,7 @@ EXPORTED = (
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
     "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
-    "gsr_forward_render_l1", "gsr_forward",
+    "gsr_forward_render_l1", "gsr_forward", "gsr_timing_sample",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -222,6 +222,8 @@ def load_library():
     lib.gsr_img_layout.argtypes = [i32, i32, ctypes.POINTER(sz), ctypes.c_int]
     lib.gsr_timing_enable.argtypes = [ctypes.c_int]
     lib.gsr_timing_enable.restype = ctypes.c_int
+    lib.gsr_timing_sample.argtypes = [ctypes.c_int]
+    lib.gsr_timing_sample.restype = ctypes.c_int
     lib.gsr_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
     lib.gsr_timing_read.restype = ctypes.c_int
     lib.gsr_stage_name.argtypes = [ctypes.c_int]
@@ -665,6 +667,11 @@ def timing_begin(name: str, device) -> None:
 def timing_end(name: str, device) -> None:
     lib = load_library()
     _check(lib.gsr_timing_end(_stage_id(name), _stream(device)), "gsr_timing_end")
+
+
+def timing_sample(every: int = 1) -> None:
+    """Events on every `every`-th launch of a stage only (gsr_timing_sample)."""
+    _check(load_library().gsr_timing_sample(int(every)), "gsr_timing_sample")
 
 
 def timing_read() -> dict:

@@ -333,6 +333,9 @@ def main():
     if world > 1 and on is not True:
         on = (on or []) + list(EXCHANGE_STAGES)
     _C.timing_enable(on)
+    # the dominant stage's events on every DOM_EVERY-th step (each event pair's
+    # marker leaves the device idle ~4 us: on every step they cost ~1.3 % at C)
+    _C.timing_sample(DOM_EVERY if args.stage_events == "split" else 1)
     torch.cuda.synchronize()
     if world > 1:
         reducer.reset_stats()
@@ -349,6 +352,7 @@ def main():
     t1 = time.perf_counter()
     stages = _C.timing_read()
     _C.timing_enable(False)
+    _C.timing_sample(1)
     elapsed = t1 - t0
     exchange = None
     if world > 1:
@@ -481,9 +485,12 @@ def main():
         dist.destroy_process_group()
 
 
+DOM_EVERY = 4  # timed region: events around the dominant stage on every 4th step
+
 STAGES_SOURCE = {
     "split": "HIP events around every rasterizer stage over a steady-state block of the same K steps right before "
-             "the timed region (mean per launch); inside the timed region only the dominant stage carries events",
+             "the timed region (mean per launch); inside the timed region only the dominant stage carries events, "
+             "on every 4th step",
     "all": "HIP events around every rasterizer stage inside the timed region (mean per launch)",
     "none": "not measured (--stage-events none)",
 }
@@ -744,6 +751,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
         # the largest stage by measured time, from a steady-state block of its own
         per, dom = stage_split(lambda: render(cam, g, bg), steps)
         _C.timing_enable([dom])  # only the dominant stage inside the timed region
+        _C.timing_sample(DOM_EVERY)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -752,6 +760,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
         dt = time.perf_counter() - t0
         live = _C.timing_read()[dom]
         _C.timing_enable(False)
+        _C.timing_sample(1)
     dom_ms = live[0] / live[1]
     ab = algorithmic_bytes(dom, P, I, W, H, M)
     achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0

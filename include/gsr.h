@@ -394,6 +394,12 @@ enum gsr_stage {
 };
 int gsr_timing_enable(int mask);
 int gsr_timing_read(double *total_ms, int64_t *launches, int cap);
+/* Record the library's stage events on every `every`-th launch of a stage only
+ * (1 = every launch, the default; reset counts restart at gsr_timing_enable): each
+ * event pair is a marker packet that leaves the device idle ~4 us, so a benchmark
+ * that times a stage inside its timed region samples it.  Caller-marked regions
+ * (gsr_timing_begin/end) are always recorded. */
+int gsr_timing_sample(int every);
 const char *gsr_stage_name(int stage);
 /* A caller-marked region of `stage` on `stream` (the same fence-free events as the
  * library's own stages; nothing is recorded unless the stage's bit is enabled):

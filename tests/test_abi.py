@@ -133,6 +133,8 @@ def test_stage_names(lib):
     assert names == ["preprocess", "scan", "depth_sort", "duplicate", "tile_sort", "render_fwd", "render_bwd",
                      "preprocess_bwd", "bwd_prepare", "exchange_wait", "sh_rebuild"]
     assert lib.gsr_stage_name(99).decode() == ""
+    assert lib.gsr_timing_sample(0) != 0 and "sample period" in lib.gsr_last_error().decode()
+    assert lib.gsr_timing_sample(4) == 0 and lib.gsr_timing_sample(1) == 0
     _C.timing_enable(True)
     assert _C.timing_read() == {n: (0.0, 0) for n in names}
     _C.timing_enable(False)
