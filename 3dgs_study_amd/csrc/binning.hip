@@ -15,9 +15,8 @@
 //                   the sort runs right after it, and its first digit scan also
 //                   publishes num_rendered (gsr_publish.hpp).  Gaussians that
 //                   preprocess culls sort anywhere: they emit nothing.
-//  2. rank scan   — the tile rects in rank order (gathered by the final depth
-//                   pass), instances per emit block and their prefix
-//                   (rank_gather_kernel).
+//  2. rank scan   — the tile rects gathered in rank order (rank_gather_kernel),
+//                   instances per emit block, an exclusive scan of those.
 //  3. emit        — each Gaussian, in rank order, writes (tile, id) for every
 //                   tile of its rect (row-major, as upstream) at its offset.
 //  4. tile sort   — stable LSD radix sort of the I instances by tile index
@@ -132,11 +131,6 @@ struct RadixPass {
     // tile sort queued before the host knows num_rendered (gsr_forward): n is the
     // buffer's capacity and every kernel works on the published count instead
     SpecGuard g;
-    // depth sort: the pass that writes the final order also writes each Gaussian's
-    // tile rect at its rank (rects_ranked[pos] = rects[id]), the random 16-B gather
-    // the rank-order emission needs, hidden among the pass's other work (NULL: none)
-    const uint4 *rects;
-    uint4 *rects_ranked;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
@@ -534,31 +528,6 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     __syncthreads();
     // ... written out in order: each digit's run is contiguous in the output too
     const uint32_t nb = span.y - b0;
-    if constexpr (MODE == RXM_KV) {
-        if (a.rects_ranked && (final3 || a.role == RX_DEPTH_FOURTH)) {
-            // the final depth pass: the order, and every item's rect gathered at its
-            // rank — all of a thread's gathers in flight before its stores
-            uint32_t pos[ITEMS], val[ITEMS];
-            uint4 q[ITEMS];
-#pragma unroll
-            for (int r = 0; r < ITEMS; r++) {
-                const uint32_t i = threadIdx.x + (uint32_t)(r * RX_THREADS);
-                const bool ok = i < nb;
-                const uint32_t k = ok ? stage_k[i] : 0u;
-                pos[r] = gshift[(k >> a.shift) & a.dmask] + i;
-                val[r] = ok ? stage_v[i] : 0u;
-                q[r] = ok ? a.rects[val[r]] : make_uint4(0u, 0u, 0u, 0u);
-            }
-#pragma unroll
-            for (int r = 0; r < ITEMS; r++) {
-                if (threadIdx.x + (uint32_t)(r * RX_THREADS) < nb) {
-                    vout[pos[r]] = val[r];
-                    a.rects_ranked[pos[r]] = q[r];
-                }
-            }
-            return;
-        }
-    }
     for (uint32_t i = threadIdx.x; i < nb; i += RX_THREADS) {
         const uint32_t k = stage_k[i];
         const uint32_t d = (k >> a.shift) & a.dmask;
@@ -637,26 +606,34 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t lo, uint32_t hi, uint32
     return base;
 }
 
-// Where each emit block's instances start, from the rects in rank (depth) order
-// (the final depth pass gathered them: coalesced reads here).  A workgroup covers
-// RG_SUPER emit blocks (4,096 ranks, RG_RANKS per thread with every load issued
-// first) and writes each one's instances before it within the workgroup, and its
-// total; emit_kernel adds the totals of the workgroups before its own — so no scan
-// launch sits between this kernel and the emission.
+// The tile rects in rank (depth) order, and where each emit block's instances
+// start: one random 16-B gather per Gaussian (the depth sort's order meets
+// preprocess's rects here, after both streams), the rest coalesced.  A workgroup
+// covers RG_SUPER emit blocks (4,096 ranks, RG_RANKS per thread with every load
+// issued first) and writes each one's instances before it within the workgroup,
+// and its total; emit_kernel adds the totals of the workgroups before its own —
+// so no scan launch sits between this kernel and the emission.
 __global__ void __launch_bounds__(RG_THREADS)
-    rank_gather_kernel(const uint4 *rects_ranked, int P, uint32_t *local, uint32_t *super,
-                       const uint32_t *dsort_ctrl) {
+    rank_gather_kernel(const uint32_t *order, const uint4 *rects, int P, uint4 *rects_ranked, uint32_t *local,
+                       uint32_t *super, const uint32_t *dsort_ctrl) {
     __shared__ uint32_t wsum[RG_RANKS][RG_THREADS / 64];
     // queued before the host knows the pass count: a four-pass sort is not done yet
     // (the host launches its fourth pass and this kernel again)
     if (dsort_ctrl && dsort_ctrl[DCTRL_PASSES] != 3u) return;
     const int r0 = blockIdx.x * RG_THREADS * RG_RANKS + threadIdx.x;
-    uint4 q[RG_RANKS];
-#pragma unroll
-    for (int k = 0; k < RG_RANKS; k++)
-        q[k] = r0 + k * RG_THREADS < P ? rects_ranked[r0 + k * RG_THREADS] : make_uint4(0u, 0u, 0u, 0u);
+    uint32_t id[RG_RANKS];
 #pragma unroll
     for (int k = 0; k < RG_RANKS; k++) {
+        const int r = r0 + k * RG_THREADS;
+        id[k] = r < P ? order[r] : 0u;
+    }
+    uint4 q[RG_RANKS];
+#pragma unroll
+    for (int k = 0; k < RG_RANKS; k++) q[k] = r0 + k * RG_THREADS < P ? rects[id[k]] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < RG_RANKS; k++) {
+        const int r = r0 + k * RG_THREADS;
+        if (r < P) rects_ranked[r] = q[k];
         uint32_t c = rect_count(q[k]);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
@@ -901,10 +878,6 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     a.shift = 8 * p;
     a.nbits = RADIX_BITS;
     a.dmask = RADIX - 1;
-    if (p >= 2) {  // passes 3 and 4 may be the final one (gather the rects)
-        a.rects = at<const uint4>(geom, L.rects);
-        a.rects_ranked = at<uint4>(geom, L.rects_ranked);
-    }
     if (p > 0 && dsort_grouped(P)) {
         a.nsup = dsort_nsup(P);
         a.sup = at<uint32_t>(geom, L.dsort_sup) + (size_t)(p - 1) * a.nsup * RADIX;
@@ -958,7 +931,8 @@ hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hi
     if (P <= 0) return hipSuccess;
     const GeomLayout L = geom_layout(P, W, H);
     hipLaunchKernelGGL(rank_gather_kernel, dim3(rg_blocks(P)), dim3(RG_THREADS), 0, s,
-                       at<const uint4>(geom, L.rects_ranked), P, at<uint32_t>(geom, L.emit_sums),
+                       at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), at<const uint4>(geom, L.rects), P,
+                       at<uint4>(geom, L.rects_ranked), at<uint32_t>(geom, L.emit_sums),
                        at<uint32_t>(geom, L.emit_super), require3 ? at<const uint32_t>(geom, L.dsort_ctrl) : nullptr);
     return hipGetLastError();
 }
