@@ -118,9 +118,9 @@ struct RadixPass {
     // (zeroed by preprocess); no digit-scan launch.  NULL otherwise.
     uint32_t *sup;
     int nsup;
-    // first depth pass: preprocess counted the key digits per block of 256 Gaussians
-    // (pre_hist [RADIX][pre_n]); the digit scan sums each radix block's pre_group of
-    // them.  NULL otherwise.
+    // first depth pass: preprocess counted the key digits per preprocess workgroup
+    // (pre_hist [RADIX][pre_n], column xcd_slot(workgroup, pre_n)); the digit scan
+    // sums each radix block's pre_group of them.  NULL otherwise.
     const uint32_t *pre_hist;
     int pre_n, pre_group;
     // first depth pass after preprocess: one more digit-scan workgroup publishes
@@ -347,17 +347,15 @@ __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPa
     uint32_t *row = a.hist + (size_t)blockIdx.x * a.NB;
     uint32_t tot;
     if (a.pre_hist) {  // radix block b's count = its pre_group preprocess workgroups' counts
-        const uint32_t *pre = a.pre_hist + (size_t)blockIdx.x * pre_hist_stride((int)a.n);
+        const uint32_t *pre = a.pre_hist + (size_t)blockIdx.x * a.pre_n;
         tot = block_exclusive_scan_fn<DSCAN_THREADS, DSCAN_PER>(
             a.NB, wsum,
-            [&](int b) {  // pre_group (4 or 8) consecutive words
-                const int p0 = b * a.pre_group;
-                if (p0 + a.pre_group <= a.pre_n && a.pre_group == 4) {
-                    const uint4 v = *reinterpret_cast<const uint4 *>(pre + p0);
-                    return (v.x + v.y) + (v.z + v.w);
-                }
+            [&](int b) {
                 uint32_t c = 0;
-                for (int j = 0; j < a.pre_group; j++) c += p0 + j < a.pre_n ? pre[p0 + j] : 0u;
+                for (int j = 0; j < a.pre_group; j++) {
+                    const int pb = b * a.pre_group + j;
+                    c += pb < a.pre_n ? pre[xcd_slot((uint32_t)pb, (uint32_t)a.pre_n)] : 0u;
+                }
                 return c;
             },
             [&](int b, uint32_t x) { row[b] = x; });

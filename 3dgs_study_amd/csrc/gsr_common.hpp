@@ -107,8 +107,6 @@ __host__ __device__ inline int dsort_nsup(int P) {
     return dsort_grouped(P) ? (radix_blocks(P, dsort_items(P)) + DSORT_SB - 1) / DSORT_SB : 1;
 }
 __host__ __device__ inline int pre_blocks(int P) { return (P + PRE_THREADS - 1) / PRE_THREADS; }
-// row stride (words) of the depth sort's per-preprocess-block digit counts: 16-B rows
-__host__ __device__ inline int pre_hist_stride(int P) { return (pre_blocks(P > 0 ? P : 1) + 3) & ~3; }
 
 // ---- control words (uint32 [16]) inside the geom buffer (a device copy of what
 // preprocess publishes to the host: num_rendered, the prefiltered error) ----
@@ -163,7 +161,7 @@ struct GeomLayout {
     size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, dsort_items(P))]
     size_t dsort_totals;  // uint32 [RADIX]
     size_t dsort_minmax;  // uint2 [pre_blocks(P)] candidate key range per preprocess workgroup
-    size_t dsort_prehist; // uint32 [RADIX][pre_hist_stride(P)] key low-byte counts per block of 256 Gaussians
+    size_t dsort_prehist; // uint32 [RADIX][pre_blocks(P)] key low-byte counts per preprocess workgroup
     size_t dsort_ctrl;    // uint32 [16] DsortCtrlWord
     size_t dsort_sup;     // uint32 [3][dsort_nsup(P)][RADIX] passes 2-4: digit counts per group of DSORT_SB blocks
     size_t emit_sums;     // uint32 [emit_blocks(P)] instances before each emit block within its rank-gather block
@@ -196,7 +194,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_hist = take((size_t)RADIX * radix_blocks(P, dsort_items(P)) * 4);
     L.dsort_totals = take((size_t)RADIX * 4);
     L.dsort_minmax = take((size_t)pre_blocks(P > 0 ? P : 1) * 8);
-    L.dsort_prehist = take((size_t)RADIX * pre_hist_stride(P) * 4);
+    L.dsort_prehist = take((size_t)RADIX * pre_blocks(P > 0 ? P : 1) * 4);
     L.dsort_ctrl = take(CTRL_WORDS * 4);
     L.dsort_sup = take((size_t)3 * dsort_nsup(P) * RADIX * 4);
     L.off[GSR_GEOM_DSORT_CTRL] = L.dsort_ctrl;

@@ -38,10 +38,9 @@ struct PreArgs {
     uint32_t *ctrl;   // geom control words (CTRL_SHJAC)
     // the depth sort's input (binning.hip): the key of each Gaussian (its view-depth
     // bits when not culled by the near plane, +inf bits otherwise), the key low
-    // byte's counts per workgroup [RADIX][nb] (column: its Gaussians' block), and
+    // byte's counts per workgroup [RADIX][nb] at column xcd_slot(workgroup, nb), and
     // the candidates' key range per workgroup; the grouped passes' counts zeroed
     uint32_t *dkeys, *dprehist;
-    int dpre_stride;
     uint2 *dminmax;
     uint32_t *dzero;
     int dzero_n;
@@ -84,12 +83,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     dh[threadIdx.x] = 0u;  // (first used after block_sum's barriers)
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
     const gsr_inputs &in = a.in;
-    // workgroup -> its 256 Gaussians: each XCD a contiguous run (xcd_slot), so the
-    // ITEMS workgroups whose digit counts form one radix block of the depth sort
-    // write neighbouring columns from one L2, which the first digit scan reads as
-    // one contiguous group
-    const int pb = (int)xcd_slot(blockIdx.x, gridDim.x);
-    const int g0 = pb * PRE_THREADS;
+    const int g0 = blockIdx.x * PRE_THREADS;
     const int idx = g0 + threadIdx.x;
     const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
     const bool use_sh = in.sh != nullptr && in.colors_precomp == nullptr;
@@ -311,7 +305,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     // workgroup stores its sum (bit 31 flags a prefiltered violation)
     const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
     const int berr = __syncthreads_or(perr);
-    if (threadIdx.x == 0) a.block_sums[pb] = make_uint4(tot | (berr ? 0x80000000u : 0u), 0u, 0u, 0u);
+    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), 0u, 0u, 0u);
     // the depth sort's keys and its first pass's digit counts (binning.hip), from the
     // view depth above: the sort needs no key launch of its own
     if (live) {
@@ -330,14 +324,15 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     }
     for (int i = idx; i < a.dzero_n; i += gridDim.x * PRE_THREADS) a.dzero[i] = 0u;
     __syncthreads();
-    a.dprehist[(size_t)threadIdx.x * a.dpre_stride + pb] = dh[threadIdx.x];
+    const uint32_t col = xcd_slot(blockIdx.x, gridDim.x);
+    a.dprehist[(size_t)threadIdx.x * gridDim.x + col] = dh[threadIdx.x];
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int k = 1; k < PRE_THREADS / 64; k++) {
             kmin = min(kmin, dmin[k]);
             kmax = max(kmax, dmax[k]);
         }
-        a.dminmax[pb] = make_uint2(kmin, kmax);
+        a.dminmax[col] = make_uint2(kmin, kmax);
     }
 }
 
@@ -375,7 +370,6 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, h
     a.shjac = (in.flags & GSR_FLAG_PREPARE_BACKWARD) && in.sh && !in.colors_precomp ? at<float>(geom, L.shjac) : nullptr;
     a.dkeys = at<uint32_t>(geom, L.dsort_keys_a);
     a.dprehist = at<uint32_t>(geom, L.dsort_prehist);
-    a.dpre_stride = pre_hist_stride(in.P);
     a.dminmax = at<uint2>(geom, L.dsort_minmax);
     a.dzero = dsort_grouped(in.P) ? at<uint32_t>(geom, L.dsort_sup) : nullptr;
     a.dzero_n = dsort_grouped(in.P) ? 3 * dsort_nsup(in.P) * RADIX : 0;
