@@ -245,7 +245,8 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
     // scan can also publish num_rendered (one launch fewer than a publish kernel)
     if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s,
                             [&] {
-                                return launch_depth_sort(in->P, in->W, in->H, geom, passes, g_pinned, s);
+                                return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom,
+                                                         passes, g_pinned, s);
                             }),
                       "depth sort", dbg, s))
         return rc;

@@ -10,9 +10,9 @@
 //  1. depth sort  — stable LSD radix sort of the P depth bit patterns with the
 //                   index as value (3 passes over P when the keys span < 2^24,
 //                   else 4; not over I): order[rank] = id in (depth_bits, id)
-//                   order.  Preprocess writes the keys and counts the first
-//                   pass's digits per workgroup (the depth it computes anyway);
-//                   the sort runs right after it, and its first digit scan also
+//                   order.  It needs only the view depths (depth_keys_kernel
+//                   computes the keys and the first pass's digit counts itself);
+//                   it runs right after preprocess, and its first digit scan also
 //                   publishes num_rendered (gsr_publish.hpp).  Gaussians that
 //                   preprocess culls sort anywhere: they emit nothing.
 //  2. rank scan   — the tile rects gathered in rank order (rank_gather_kernel),
@@ -115,14 +115,9 @@ struct RadixPass {
     int T;
     // grouped depth passes (dsort_grouped, passes 2-4): hist holds block rows
     // [NB][RADIX], sup the digit counts per group of DSORT_SB blocks [nsup][RADIX]
-    // (zeroed by preprocess); no digit-scan launch.  NULL otherwise.
+    // (zeroed by depth_keys_kernel); no digit-scan launch.  NULL otherwise.
     uint32_t *sup;
     int nsup;
-    // first depth pass: preprocess counted the key digits per preprocess workgroup
-    // (pre_hist [RADIX][pre_n], column xcd_slot(workgroup, pre_n)); the digit scan
-    // sums each radix block's pre_group of them.  NULL otherwise.
-    const uint32_t *pre_hist;
-    int pre_n, pre_group;
     // first depth pass after preprocess: one more digit-scan workgroup publishes
     // num_rendered (gsr_publish.hpp) from preprocess's block sums; NULL otherwise
     const uint4 *pub_sums;
@@ -137,7 +132,7 @@ enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
 
 // First depth pass: key = depth bits - base (base = the smallest candidate key
 // with its low byte cleared, so the key's low byte — this pass's digit, which
-// preprocess counted before the base was known — is the raw bits' own);
+// depth_keys_kernel counted before the base was known — is the raw bits' own);
 // in three-pass mode keys beyond 2^24 (only non-candidates, +inf keys, reach it)
 // saturate their top 16 bits and keep that low byte: every pass then sorts by the
 // digits of one and the same key.
@@ -169,7 +164,11 @@ __device__ __forceinline__ uint32_t key_rel(uint32_t k, uint32_t base, uint32_t 
 // each XCD a contiguous run of blocks: a sector's partial writes (upsweep) and
 // reads (downsweep) then meet in one L2 instead of crossing to HBM once per
 // block.  A bijection on [0, NB); placement is a speed hint only.
-__device__ __forceinline__ uint32_t radix_block(int NB) { return xcd_slot(blockIdx.x, (uint32_t)NB); }
+__device__ __forceinline__ uint32_t radix_block(int NB) {
+    const uint32_t x = blockIdx.x & 7u, j = blockIdx.x >> 3;
+    const uint32_t q = (uint32_t)NB >> 3, r = (uint32_t)NB & 7u;
+    return x * q + min(x, r) + j;
+}
 
 // The second pass's segment table from the first pass's digit totals: segment
 // (low tile digit) s starts at block sfb[s] and item sst[s]; [RADIX] = the totals.
@@ -311,8 +310,7 @@ __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPa
     if (blockIdx.x == RADIX) {  // first depth pass: one more workgroup reduces the candidate key range
         __shared__ uint32_t wmin[DSCAN_THREADS / 64], wmax[DSCAN_THREADS / 64];
         uint32_t kmin = 0xffffffffu, kmax = 0u;
-        const int nmm = a.pre_hist ? a.pre_n : a.NB;  // (per preprocess workgroup)
-        for (int i = threadIdx.x; i < nmm; i += DSCAN_THREADS) {
+        for (int i = threadIdx.x; i < a.NB; i += DSCAN_THREADS) {
             const uint2 m = a.minmax[i];
             kmin = min(kmin, m.x);
             kmax = max(kmax, m.y);
@@ -344,24 +342,8 @@ __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPa
         return;
     }
     if (pass_skipped(a)) return;
-    uint32_t *row = a.hist + (size_t)blockIdx.x * a.NB;
-    uint32_t tot;
-    if (a.pre_hist) {  // radix block b's count = its pre_group preprocess workgroups' counts
-        const uint32_t *pre = a.pre_hist + (size_t)blockIdx.x * a.pre_n;
-        tot = block_exclusive_scan_fn<DSCAN_THREADS, DSCAN_PER>(
-            a.NB, wsum,
-            [&](int b) {
-                uint32_t c = 0;
-                for (int j = 0; j < a.pre_group; j++) {
-                    const int pb = b * a.pre_group + j;
-                    c += pb < a.pre_n ? pre[xcd_slot((uint32_t)pb, (uint32_t)a.pre_n)] : 0u;
-                }
-                return c;
-            },
-            [&](int b, uint32_t x) { row[b] = x; });
-    } else {
-        tot = block_exclusive_scan_inplace<DSCAN_THREADS, DSCAN_PER>(row, a.NB, wsum);
-    }
+    const uint32_t tot =
+        block_exclusive_scan_inplace<DSCAN_THREADS, DSCAN_PER>(a.hist + (size_t)blockIdx.x * a.NB, a.NB, wsum);
     if (threadIdx.x == 0) a.totals[blockIdx.x] = tot;
 }
 
@@ -565,7 +547,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
 template <int ITEMS, int MODE = RXM_KV>
 static hipError_t radix_pass(const RadixPass &a, hipStream_t s, bool counted = false) {
     if (a.n == 0) return hipSuccess;
-    // counted: the digit counts come from preprocess (the first digit scan sums them)
+    // counted: the digit counts are already in a.hist (depth_keys_kernel)
     if (!counted) hipLaunchKernelGGL((radix_upsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     if (!a.sup)  // grouped depth passes: each downsweep block sums its own prefix
         hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(a.pub_sums ? RADIX + 2 : a.minmax ? RADIX + 1 : RADIX),
@@ -842,8 +824,85 @@ hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const v
     return hipGetLastError();
 }
 
+// The depth sort's keys and its first pass's digit counts in one launch (the
+// first pass needs no upsweep of its own): per Gaussian the view-space depth as
+// preprocess computes it (xform_point4x3, the same operations, no contraction),
+// key = its bits for a candidate (z > 0.2: not culled by the near plane), +inf
+// bits otherwise; per radix block the histogram of the keys' low byte (the first
+// digit needs no base: key_of keeps it) and the candidates' key range, which the
+// first digit scan reduces into the base and the pass count.
+struct DepthKeyArgs {
+    const float *means3D;
+    const float *viewmatrix;
+    uint32_t n;
+    int NB;
+    uint32_t *keys;
+    uint32_t *hist;   // [RADIX][NB]
+    uint2 *minmax;    // [NB]
+    uint32_t *zero;   // the grouped passes' group counts, cleared here (every block a slice), or NULL
+    int zero_n;
+};
+template <int ITEMS>
+__global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) {
+    constexpr int TILE_N = RX_THREADS * ITEMS;
+    __shared__ uint32_t h[RX_WAVES][RADIX];
+    __shared__ uint32_t wmin[RX_WAVES], wmax[RX_WAVES];
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
+    const uint32_t blk = radix_block(a.NB);
+    if (a.zero)
+        for (int i = blockIdx.x * RX_THREADS + threadIdx.x; i < a.zero_n; i += gridDim.x * RX_THREADS) a.zero[i] = 0u;
+    const Mat4 V = load_mat4(a.viewmatrix);
+    float z[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {  // every load first
+        const uint32_t idx = blk * (uint32_t)TILE_N + (uint32_t)(r * RX_THREADS) + threadIdx.x;
+        const uint32_t li = idx < a.n ? idx : a.n - 1;
+        const f3 p = {a.means3D[3 * (size_t)li], a.means3D[3 * (size_t)li + 1], a.means3D[3 * (size_t)li + 2]};
+        z[r] = xform_point4x3(p, V).z;
+    }
+    __syncthreads();
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const uint32_t idx = blk * (uint32_t)TILE_N + (uint32_t)(r * RX_THREADS) + threadIdx.x;
+        if (idx < a.n) {
+            const bool cand = z[r] > 0.2f;  // preprocess culls z <= 0.2 (and a NaN depth sorts last)
+            const uint32_t key = cand ? __float_as_uint(z[r]) : 0x7f800000u;
+            a.keys[idx] = key;
+            atomicAdd(&h[w][key & (RADIX - 1)], 1u);
+            if (cand) {
+                kmin = min(kmin, key);
+                kmax = max(kmax, key);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wmin[w] = kmin;
+        wmax[w] = kmax;
+    }
+    __syncthreads();
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < RX_WAVES; k++) c += h[k][threadIdx.x];
+    a.hist[(size_t)threadIdx.x * a.NB + blk] = c;
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < RX_WAVES; k++) {
+            kmin = min(kmin, wmin[k]);
+            kmax = max(kmax, wmax[k]);
+        }
+        a.minmax[blk] = make_uint2(kmin, kmax);
+    }
+}
+
 // ------------------------------------------------------------ launchers
-// The depth sort: preprocess's keys, then passes 1-3; the fourth pass is launched
+// The depth sort: depth_keys_kernel, then passes 1-3; the fourth pass is launched
 // by the host after its sync when the published pass count needs it (in line), or
 // queued with kernels that return at once unless the key range needs it (on the
 // opt-in second stream, GSR_SIDE_STREAM=1).  The order lands in
@@ -858,7 +917,7 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     uint32_t *ka = at<uint32_t>(geom, L.dsort_keys_a), *kb = at<uint32_t>(geom, L.dsort_keys_b);
     uint32_t *va = at<uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), *vb = at<uint32_t>(geom, L.dsort_vals_b);
     uint32_t *vc = at<uint32_t>(geom, L.dsort_vals_c);
-    // keys: a (preprocess) -> b -> a -> b -> -; values: index -> b -> c -> b -> order
+    // keys: a (depth_keys_kernel) -> b -> a -> b -> -; values: index -> b -> c -> b -> order
     const uint32_t *kin[4] = {ka, kb, ka, kb};
     const uint32_t *vin[4] = {nullptr, vb, vc, vb};
     uint32_t *kout[4] = {kb, ka, kb, nullptr};
@@ -885,11 +944,21 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     return a;
 }
 
-// The keys and the first pass's digit counts come from preprocess (preprocess.hip:
-// the view depth it computes anyway; no key launch of the sort's own).
 template <int ITEMS>
-static hipError_t depth_sort_items(int P, int W, int H, void *geom, int passes, uint32_t *host_ctrl, hipStream_t s) {
+static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
+                                   int passes, uint32_t *host_ctrl, hipStream_t s) {
     const GeomLayout L = geom_layout(P, W, H);
+    DepthKeyArgs k;
+    k.means3D = means3D;
+    k.viewmatrix = viewmatrix;
+    k.n = (uint32_t)P;
+    k.NB = radix_blocks(P, ITEMS);
+    k.keys = at<uint32_t>(geom, L.dsort_keys_a);
+    k.hist = at<uint32_t>(geom, L.dsort_hist);
+    k.minmax = at<uint2>(geom, L.dsort_minmax);
+    k.zero = dsort_grouped(P) ? at<uint32_t>(geom, L.dsort_sup) : nullptr;
+    k.zero_n = dsort_grouped(P) ? 3 * dsort_nsup(P) * RADIX : 0;
+    hipLaunchKernelGGL(depth_keys_kernel<ITEMS>, dim3(k.NB), dim3(RX_THREADS), 0, s, k);
     // passes 3: the host reads the published pass count after its sync and launches
     // the fourth (launch_depth_sort_fourth) when the keys need it — three
     // early-returning launches (~14 us at config C) saved in the common case;
@@ -903,9 +972,6 @@ static hipError_t depth_sort_items(int P, int W, int H, void *geom, int passes, 
             a.pub_n = pre_blocks(P);
             a.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
             a.pub_host = host_ctrl;
-            a.pre_hist = at<const uint32_t>(geom, L.dsort_prehist);
-            a.pre_n = pre_blocks(P);
-            a.pre_group = ITEMS;  // RX_THREADS == PRE_THREADS: ITEMS preprocess workgroups per radix block
         }
         hipError_t e = radix_pass<ITEMS>(a, s, p == 0);
         if (e != hipSuccess) return e;
@@ -913,10 +979,12 @@ static hipError_t depth_sort_items(int P, int W, int H, void *geom, int passes, 
     return hipGetLastError();
 }
 
-hipError_t launch_depth_sort(int P, int W, int H, void *geom, int passes, uint32_t *host_ctrl, hipStream_t s) {
+hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
+                             int passes, uint32_t *host_ctrl, hipStream_t s) {
     if (P <= 0) return hipSuccess;
-    return dsort_items(P) == DSORT_ITEMS_BIG ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, geom, passes, host_ctrl, s)
-                                             : depth_sort_items<DSORT_ITEMS>(P, W, H, geom, passes, host_ctrl, s);
+    return dsort_items(P) == DSORT_ITEMS_BIG
+               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, s)
+               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, s);
 }
 
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s) {

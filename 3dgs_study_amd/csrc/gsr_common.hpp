@@ -160,8 +160,7 @@ struct GeomLayout {
     size_t dsort_vals_c;
     size_t dsort_hist;    // uint32 [RADIX][radix_blocks(P, dsort_items(P))]
     size_t dsort_totals;  // uint32 [RADIX]
-    size_t dsort_minmax;  // uint2 [pre_blocks(P)] candidate key range per preprocess workgroup
-    size_t dsort_prehist; // uint32 [RADIX][pre_blocks(P)] key low-byte counts per preprocess workgroup
+    size_t dsort_minmax;  // uint2 [radix_blocks(P, dsort_items(P))] candidate key range per first-pass block
     size_t dsort_ctrl;    // uint32 [16] DsortCtrlWord
     size_t dsort_sup;     // uint32 [3][dsort_nsup(P)][RADIX] passes 2-4: digit counts per group of DSORT_SB blocks
     size_t emit_sums;     // uint32 [emit_blocks(P)] instances before each emit block within its rank-gather block
@@ -193,8 +192,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_vals_c = take((size_t)P * 4);
     L.dsort_hist = take((size_t)RADIX * radix_blocks(P, dsort_items(P)) * 4);
     L.dsort_totals = take((size_t)RADIX * 4);
-    L.dsort_minmax = take((size_t)pre_blocks(P > 0 ? P : 1) * 8);
-    L.dsort_prehist = take((size_t)RADIX * pre_blocks(P > 0 ? P : 1) * 4);
+    L.dsort_minmax = take((size_t)radix_blocks(P, dsort_items(P)) * 8);
     L.dsort_ctrl = take(CTRL_WORDS * 4);
     L.dsort_sup = take((size_t)3 * dsort_nsup(P) * RADIX * 4);
     L.off[GSR_GEOM_DSORT_CTRL] = L.dsort_ctrl;

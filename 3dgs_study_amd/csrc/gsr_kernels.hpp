@@ -17,8 +17,8 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 // count says so) or 4 (queued up front; returns at once when three suffice).
 // host_ctrl: the caller's pinned words, which the first digit scan fills with the
 // pass count and num_rendered (after preprocess, in stream order).
-// (after launch_preprocess, which writes the keys and the first pass's digit counts)
-hipError_t launch_depth_sort(int P, int W, int H, void *geom, int passes, uint32_t *host_ctrl, hipStream_t s);
+hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
+                             int passes, uint32_t *host_ctrl, hipStream_t s);
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s);
 hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hipStream_t s);
 // cap: the binning buffer's instance capacity (its layout); g: speculative guard

@@ -101,8 +101,8 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *wsum) {
 // total, and one exchange of the wave totals places the waves: a block scan
 // (two barriers) per THREADS entries left the 256 digit scans of the config-E
 // tile sort at ~28 us each.
-template <int THREADS, int PER, typename Load, typename Store>
-__device__ __forceinline__ uint32_t block_exclusive_scan_fn(int n, uint32_t *wsum, Load load, Store store) {
+template <int THREADS, int PER>
+__device__ __forceinline__ uint32_t block_exclusive_scan_inplace(uint32_t *v, int n, uint32_t *wsum) {
     constexpr int NW = THREADS / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t carry = 0;
@@ -110,7 +110,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_fn(int n, uint32_t *wsu
         const int wb = base + w * 64 * PER + lane;
         uint32_t x[PER], ex[PER], run = 0;
 #pragma unroll
-        for (int j = 0; j < PER; j++) x[j] = wb + 64 * j < n ? load(wb + 64 * j) : 0u;
+        for (int j = 0; j < PER; j++) x[j] = wb + 64 * j < n ? v[wb + 64 * j] : 0u;
 #pragma unroll
         for (int j = 0; j < PER; j++) {
             const uint32_t s = wave_inclusive_scan(x[j]);
@@ -129,23 +129,10 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_fn(int n, uint32_t *wsu
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < PER; j++)
-            if (wb + 64 * j < n) store(wb + 64 * j, carry + pre + ex[j]);
+            if (wb + 64 * j < n) v[wb + 64 * j] = carry + pre + ex[j];
         carry += tot;
     }
     return carry;
-}
-template <int THREADS, int PER>
-__device__ __forceinline__ uint32_t block_exclusive_scan_inplace(uint32_t *v, int n, uint32_t *wsum) {
-    return block_exclusive_scan_fn<THREADS, PER>(
-        n, wsum, [&](int i) { return v[i]; }, [&](int i, uint32_t x) { v[i] = x; });
-}
-
-// Workgroup b of a grid of n -> slot: each XCD (workgroups are dealt round-robin
-// over the 8, b mod 8) a contiguous run of slots, so the partial-line writes of
-// neighbouring slots meet in one L2.  A bijection on [0, n); a speed hint only.
-__host__ __device__ inline uint32_t xcd_slot(uint32_t b, uint32_t n) {
-    const uint32_t x = b & 7u, j = b >> 3, q = n >> 3, r = n & 7u;
-    return x * q + (x < r ? x : r) + j;
 }
 
 }  // namespace gsr

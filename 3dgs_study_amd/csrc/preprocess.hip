@@ -36,14 +36,6 @@ struct PreArgs {
     uint32_t *order_cnt;
     float *shjac;     // [9][P] the SH direction Jacobian, when a backward will follow (else NULL)
     uint32_t *ctrl;   // geom control words (CTRL_SHJAC)
-    // the depth sort's input (binning.hip): the key of each Gaussian (its view-depth
-    // bits when not culled by the near plane, +inf bits otherwise), the key low
-    // byte's counts per workgroup [RADIX][nb] at column xcd_slot(workgroup, nb), and
-    // the candidates' key range per workgroup; the grouped passes' counts zeroed
-    uint32_t *dkeys, *dprehist;
-    uint2 *dminmax;
-    uint32_t *dzero;
-    int dzero_n;
 };
 
 // SH -> RGB for one Gaussian, per channel (forward.cu computeColorFromSH).
@@ -77,10 +69,7 @@ __device__ inline float sh_channel(const float *sh, int c, int deg, float x, flo
 // instead of their cat.
 template <int RWC, bool SPLIT>
 __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) {
-    static_assert(PRE_THREADS == RADIX, "one digit counter per thread");
     __shared__ uint32_t wsum[PRE_THREADS / 64];
-    __shared__ uint32_t dh[RADIX], dmin[PRE_THREADS / 64], dmax[PRE_THREADS / 64];
-    dh[threadIdx.x] = 0u;  // (first used after block_sum's barriers)
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
     const gsr_inputs &in = a.in;
     const int g0 = blockIdx.x * PRE_THREADS;
@@ -142,8 +131,6 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     }
     uint32_t touched = 0;
     bool perr = false;
-    uint32_t dkey = 0x7f800000u;  // the depth sort's key: +inf bits unless a near-plane candidate
-    bool dcand = false;
     // what the colour stage (after the barrier) needs
     bool emit = false;
     float px = 0.f, py = 0.f, conic_x = 0.f, conic_y = 0.f, conic_z = 0.f, qmax = 0.f, depth = 0.f;
@@ -154,8 +141,6 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         const float p_w = 1.0f / (p_hom.w + 0.0000001f);
         const f3 p_proj = {p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w};
         const f3 p_view = xform_point4x3(p, V);
-        dcand = p_view.z > 0.2f;  // (a NaN depth is no candidate: it sorts last)
-        dkey = dcand ? __float_as_uint(p_view.z) : 0x7f800000u;
         bool ok = true;
         if (p_view.z <= 0.2f) {
             ok = false;
@@ -244,7 +229,8 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 rect_out = make_uint4(rc.x0 | (rc.x1 << 16), rc.y0 | (rc.y1 << 16), (uint32_t)m, (uint32_t)(m >> 32));
             }
         }
-        // depths of invisible Gaussians: +inf (the depth sort's keys are dkey, below)
+        // depths of invisible Gaussians: +inf (the depth sort keys its candidates
+        // itself, binning.hip depth_keys_kernel)
         if (!radius_out) a.depths[idx] = __uint_as_float(0x7f800000u);
         a.radii[idx] = radius_out;
         a.tiles_touched[idx] = touched;
@@ -306,34 +292,6 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
     const int berr = __syncthreads_or(perr);
     if (threadIdx.x == 0) a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), 0u, 0u, 0u);
-    // the depth sort's keys and its first pass's digit counts (binning.hip), from the
-    // view depth above: the sort needs no key launch of its own
-    if (live) {
-        a.dkeys[idx] = dkey;
-        atomicAdd(&dh[dkey & (RADIX - 1)], 1u);
-    }
-    uint32_t kmin = live && dcand ? dkey : 0xffffffffu, kmax = live && dcand ? dkey : 0u;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
-        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        dmin[threadIdx.x >> 6] = kmin;
-        dmax[threadIdx.x >> 6] = kmax;
-    }
-    for (int i = idx; i < a.dzero_n; i += gridDim.x * PRE_THREADS) a.dzero[i] = 0u;
-    __syncthreads();
-    const uint32_t col = xcd_slot(blockIdx.x, gridDim.x);
-    a.dprehist[(size_t)threadIdx.x * gridDim.x + col] = dh[threadIdx.x];
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int k = 1; k < PRE_THREADS / 64; k++) {
-            kmin = min(kmin, dmin[k]);
-            kmax = max(kmax, dmax[k]);
-        }
-        a.dminmax[col] = make_uint2(kmin, kmax);
-    }
 }
 
 // auxiliary.h in_frustum via checkFrustum (markVisible).
@@ -368,11 +326,6 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, h
     a.order_cnt = at<uint32_t>(geom, L.order_cnt);
     a.ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
     a.shjac = (in.flags & GSR_FLAG_PREPARE_BACKWARD) && in.sh && !in.colors_precomp ? at<float>(geom, L.shjac) : nullptr;
-    a.dkeys = at<uint32_t>(geom, L.dsort_keys_a);
-    a.dprehist = at<uint32_t>(geom, L.dsort_prehist);
-    a.dminmax = at<uint2>(geom, L.dsort_minmax);
-    a.dzero = dsort_grouped(in.P) ? at<uint32_t>(geom, L.dsort_sup) : nullptr;
-    a.dzero_n = dsort_grouped(in.P) ? 3 * dsort_nsup(in.P) * RADIX : 0;
     const int nb = pre_blocks(in.P);
     const bool split = in.sh_rest != nullptr;
     // the register prefetch of cat rows reads them as float4: 16-B aligned only

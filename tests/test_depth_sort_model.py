@@ -1,7 +1,8 @@
-"""Host-side model of the depth sort's key transform (preprocess.hip writes the keys,
+"""Host-side model of the depth sort's key transform (binning.hip: depth_keys_kernel,
 key_of, the first digit scan's base / pass count), run in numpy on the CPU.
 
-Preprocess counts the first pass's digits before the key base is known: the base has its low byte cleared (the first digit is
+The sort runs on its own stream beside preprocess, so its first pass counts digits
+before the key base is known: the base has its low byte cleared (the first digit is
 the raw bits' low byte), and in three-pass mode keys beyond 2^24 saturate their top
 16 bits but keep their low byte, so every pass sorts by digits of one and the same
 key.  This model runs the same LSD passes (stable, 8-bit digits) and checks that the
@@ -29,7 +30,7 @@ def depth_order(z):
     else:
         base, passes = 0, 3
     vals = np.arange(z.size)
-    # pass 1 digit: the raw low byte (counted by preprocess before the base exists)
+    # pass 1 digit: the raw low byte (counted by depth_keys_kernel before the base exists)
     order = np.argsort(keys & 0xFF, kind="stable")
     k = key_of(keys[order], base, passes)
     assert np.array_equal(k & 0xFF, keys[order] & 0xFF)  # the digit pass 1 counted is the one it sorted by
