@@ -110,9 +110,11 @@ __global__ void __launch_bounds__(256) colors_from_accum_kernel(int P, const int
     if (i >= P) return;
     const bool vis = radii[i] > 0;
     const uint32_t cl = clamped[i];
-    const float *row = accum + (size_t)i * ACCUM_STRIDE;
+    // one 16-B load of the row's head (the colour sums, floats 0..2)
+    const float4 row = *reinterpret_cast<const float4 *>(accum + (size_t)i * ACCUM_STRIDE);
+    const float c[3] = {row.x, row.y, row.z};
 #pragma unroll
-    for (int c = 0; c < 3; c++) drgb[3 * (size_t)i + c] = vis ? row[c] * ((cl >> c) & 1u ? 0.f : 1.f) : 0.f;
+    for (int k = 0; k < 3; k++) drgb[3 * (size_t)i + k] = vis ? c[k] * ((cl >> k) & 1u ? 0.f : 1.f) : 0.f;
 }
 
 hipError_t launch_colors_from_accum(int P, const int32_t *radii, const uint8_t *clamped, const float *accum,

@@ -246,9 +246,10 @@ def set_grad_exchange(ex):
     """Install (or with None remove) the view-parallel gradient exchange
     (multiview.GradAllReduce); returns the previous one.  The exchange provides
     ``accepts(sh, means3D) -> bool`` (True: it takes this backward's SH gradient as
-    the view's colour gradient), ``record(P)`` (a float32 tensor of
-    ``_C.sh_record_floats(P)`` elements) and ``push(record, campos, sh_degree)`` for
-    that; ``owns_hooks(leaf) -> bool`` (the leaf's post-accumulate hooks are its own,
+    the view's colour gradient), ``record(P, campos, sh_degree)`` (a float32 tensor
+    of ``_C.sh_record_floats(P)`` elements, its [campos, degree] header written) and
+    ``push(record, campos, sh_degree, ready)`` for that (``ready``: an event after
+    which the record's colour gradient is written); ``owns_hooks(leaf) -> bool`` (the leaf's post-accumulate hooks are its own,
     so the fused path may write that leaf's gradient) and
     ``leaf_bucket({name: leaves}) -> {name: views}`` (where the fused leaf gradients
     go: views of its all-reduce bucket, for the names it can take)."""
@@ -351,10 +352,10 @@ class _RasterizeGaussians(torch.autograd.Function):
             leaf, fresh = _leaf_outputs(plan)
             kw["leaf"] = leaf
         if sink_takes_sh:
-            rec = ex.record(means3D.size(0))
-            # the record's exchange starts as soon as the colour gradient is queued,
-            # under the per-Gaussian backward
-            kw["drgb_out"], kw["on_drgb"] = rec[4:], lambda: ex.push(rec, rs.campos, rs.sh_degree)
+            rec = ex.record(means3D.size(0), rs.campos, rs.sh_degree)
+            # the record's exchange starts behind an event right after the colour
+            # gradient is written, under the per-Gaussian backward
+            kw["drgb_out"], kw["on_drgb"] = rec[4:], lambda ready: ex.push(rec, rs.campos, rs.sh_degree, ready)
         else:
             # a dsh that autograd receives is the [P,M,3] view of coefficient planes:
             # the reference's SH cat backward (get_features) then slices an f_dc
@@ -477,8 +478,8 @@ class _RasterizeModel(torch.autograd.Function):
         leaf = _C.LeafGrads(accumulate=acc, **kw)
         bkw = dict(inputs=inputs, leaf=leaf, l1_seed=seed)
         if sink_takes_sh:
-            rec = ex.record(P)
-            bkw["drgb_out"], bkw["on_drgb"] = rec[4:], lambda: ex.push(rec, rs.campos, rs.sh_degree)
+            rec = ex.record(P, rs.campos, rs.sh_degree)
+            bkw["drgb_out"], bkw["on_drgb"] = rec[4:], lambda ready: ex.push(rec, rs.campos, rs.sh_degree, ready)
         args = (rs.bg, means3D, radii, None, scaling, rotation, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
                 rs.tanfovx, rs.tanfovy, grad_out_color, f_dc, rs.sh_degree, rs.campos, geom, ctx.num_rendered, binning,
                 img, rs.debug)

@@ -100,7 +100,8 @@ class GradAllReduce:
         self._cb_queued = False
         self.launched_in_backward = False  # the bucket's all-reduce started from the end-of-backward callback
         self._timing = timing
-        self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0}
+        self.timing_every = 4   # regions recorded on every 4th step (each event pair idles the device ~4 us)
+        self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0, "timed_calls": 0}
         self._prev_ex = None
         self._hdr = None        # push()'s cached record header
         self._installed = False
@@ -233,7 +234,17 @@ class GradAllReduce:
         covered = {id(v) for vs in views.values() for v in vs if v is not None}
         if any(id(v) not in covered for v in self._views):
             return
-        self._work = dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        # The SH rebuild is queued first, right behind the backward's last kernel (it
+        # needs only the gathered records), and the bucket's all-reduce then starts
+        # behind an event marking that kernel: the collective's host-side launch
+        # (tens of us in ProcessGroupNCCL) no longer leaves the device idle before
+        # the rebuild, and the all-reduce runs beside it.
+        done = torch.cuda.Event() if self._bucket.is_cuda else None
+        if done is not None:
+            done.record()
+        self._sh_rebuild()
+        self._work = self._launch(done, lambda: dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM,
+                                                                group=self.group, async_op=True))
         self.launched_in_backward = True
         # The bucket now belongs to the collective.  Another gradient path into a
         # reduced leaf (an extra loss term, a regulariser on _scaling ...) reaches
@@ -246,7 +257,6 @@ class GradAllReduce:
         self._early_version = self._bucket._version
         for p in self._reduced:
             p.grad = None
-        self._sh_rebuild()
 
     # ---- the end of each backward: start the bucket's all-reduce on the step's last
     def _queue_callback(self):
@@ -276,13 +286,17 @@ class GradAllReduce:
             return
         if self._backwards == self.views_per_step and self._work is None and not self._stale():
             bucket = self._pack()
-            self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            self.launched_in_backward = True
+            done = torch.cuda.Event() if bucket.is_cuda else None
+            if done is not None:
+                done.record()
             # the SH rebuild needs only the gathered records: queued here, behind the
-            # backward's last kernel and beside the bucket's all-reduce, instead of
-            # after the host has returned from backward() into the caller's
-            # __call__ (a host round trip the device spent idle: 60-90 us per step)
+            # backward's last kernel, instead of after the host has returned from
+            # backward() into the caller's __call__ (a host round trip the device spent
+            # idle: 60-90 us per step); the bucket's all-reduce behind the pack, beside it
             self._sh_rebuild()
+            self._work = self._launch(done, lambda: dist.all_reduce(bucket, op=dist.ReduceOp.SUM,
+                                                                    group=self.group, async_op=True))
+            self.launched_in_backward = True
 
     # ---- the rasterizer's SH sink
     def accepts(self, sh, means3D: torch.Tensor) -> bool:
@@ -307,11 +321,7 @@ class GradAllReduce:
                                "callables that return the current tensors")
         return ok
 
-    def record(self, P: int) -> torch.Tensor:
-        from diff_gaussian_rasterization import _C
-        return torch.empty(_C.sh_record_floats(P), dtype=torch.float32, device=self._sh[0].device)
-
-    def push(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int) -> None:
+    def _header(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int) -> None:
         # the record's header [campos, degree]: one copy from a cached 4-float tensor
         # (the view's camera is usually the same object step after step)
         h = self._hdr
@@ -320,10 +330,51 @@ class GradAllReduce:
                              torch.cat([campos.reshape(-1)[:3].float(),
                                         torch.full((1,), float(sh_degree), device=rec.device)]))
         rec[0:4].copy_(h[3])
+
+    def record(self, P: int, campos: torch.Tensor = None, sh_degree: int = None) -> torch.Tensor:
+        """A view's record; with the camera given its header is written now, on the
+        compute stream ahead of the backward's kernels (push's ready event then
+        covers it)."""
+        from diff_gaussian_rasterization import _C
+        rec = torch.empty(_C.sh_record_floats(P), dtype=torch.float32, device=self._sh[0].device)
+        if campos is not None:
+            self._header(rec, campos, sh_degree)
+            self._hdr_rec = rec
+        return rec
+
+    def _side(self, device) -> "torch.cuda.Stream":
+        """A stream for the collectives' launches only (no kernel of ours runs on it):
+        a collective started on it behind an event waits for exactly the work that
+        event marks, not for whatever the compute stream has queued since."""
+        st = getattr(self, "_side_stream", None)
+        if st is None or st.device != device:
+            st = self._side_stream = torch.cuda.Stream(device=device)
+        return st
+
+    def _launch(self, ready, fn):
+        """fn() (a collective, async) ordered after `ready` (an event on the compute
+        stream, or None: after everything queued there so far)."""
+        if ready is None:
+            return fn()
+        st = self._side(ready.device if hasattr(ready, "device") and ready.device is not None
+                        else torch.cuda.current_device())
+        with torch.cuda.stream(st):
+            st.wait_event(ready)
+            return fn()
+
+    def push(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int, ready=None) -> None:
+        """Exchange a view's record: with `ready` (an event after which its colour
+        gradient is written; the header written by record()) the all-gather starts
+        behind that event, else behind everything queued so far."""
+        if ready is None or getattr(self, "_hdr_rec", None) is not rec:
+            self._header(rec, campos, sh_degree)
+            ready = None  # the header copy was just queued: gather behind it
+        self._hdr_rec = None
         if self._active():
             world = dist.get_world_size(self.group)
             out = torch.empty(world * rec.numel(), dtype=rec.dtype, device=rec.device)
-            work = dist.all_gather_into_tensor(out, rec, group=self.group, async_op=True)
+            work = self._launch(ready, lambda: dist.all_gather_into_tensor(out, rec, group=self.group,
+                                                                           async_op=True))
             self._gathers.append((out, world, work))
         else:
             self._gathers.append((rec, 1, None))
@@ -390,8 +441,11 @@ class GradAllReduce:
     # ---- timing (bench.py's N > 1 line): on a GPU the regions are the library's
     # fence-free stage events (stages "exchange_wait" / "sh_rebuild", recorded while
     # _C.timing_enable has them on, read with _C.timing_read); on the CPU host clocks
+    def _timed_now(self) -> bool:
+        return self._timing and self._tstats["calls"] % self.timing_every == 0
+
     def _begin(self, name):
-        if not self._timing:
+        if not self._timed_now():
             return
         if self._reduced and self._reduced[0].is_cuda:
             from diff_gaussian_rasterization import _C
@@ -400,7 +454,7 @@ class GradAllReduce:
             self._t0 = time.perf_counter()
 
     def _end(self, name):
-        if not self._timing:
+        if not self._timed_now():
             return
         if self._reduced and self._reduced[0].is_cuda:
             from diff_gaussian_rasterization import _C
@@ -409,16 +463,18 @@ class GradAllReduce:
             self._tstats[name + "_ms"] += 1e3 * (time.perf_counter() - self._t0)
 
     def stats(self) -> dict:
-        """Per-__call__ means since the last reset of the host-clock regions (CPU
+        """Per-step means since the last reset of the host-clock regions (CPU
         tensors; on a GPU the regions are library stages, read by the caller with
-        _C.timing_read), the calls, and the bytes this rank contributes per step."""
-        n = max(self._tstats["calls"], 1)
+        _C.timing_read and divided by timed_calls), the calls, the steps whose regions
+        were recorded (every timing_every-th), and the bytes this rank sends per step."""
+        n = max(self._tstats["timed_calls"], 1)
         return {"exchange_wait_ms": self._tstats["exchange_wait_ms"] / n,
                 "sh_rebuild_ms": self._tstats["sh_rebuild_ms"] / n, "calls": self._tstats["calls"],
+                "timed_calls": self._tstats["timed_calls"],
                 "bytes_per_rank": self.nbytes}
 
     def reset_stats(self) -> None:
-        self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0}
+        self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0, "timed_calls": 0}
 
     def __call__(self):
         """Finish this step's exchange: the bucket's all-reduce (started at the end
@@ -454,6 +510,7 @@ class GradAllReduce:
                 if i in extra:
                     v.add_(extra[i].view_as(v))
                 p.grad = v
+        self._tstats["timed_calls"] += int(self._timed_now())
         self._tstats["calls"] += 1
         self._early = False
         self._extra = None

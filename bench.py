@@ -357,7 +357,7 @@ def main():
     exchange = None
     if world > 1:
         ex = reducer.stats()
-        wait_ms, rebuild_ms = _exchange_split(stages, ex["calls"])
+        wait_ms, rebuild_ms = _exchange_split(stages, ex["timed_calls"])
         t = torch.tensor([elapsed, wait_ms, rebuild_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0].item())
@@ -524,8 +524,9 @@ def _dominant(per: dict) -> str:
 
 
 def _exchange_split(stages: dict, calls: int) -> tuple:
-    """Per-call means (ms) of the exchange's two regions from the library's stage
-    events: the compute stream's wait for the collectives, the SH rebuild."""
+    """Per-step means (ms) of the exchange's two regions from the library's stage
+    events over the `calls` steps that recorded them (GradAllReduce.timing_every):
+    the compute stream's wait for the collectives, the SH rebuild."""
     n = max(calls, 1)
     return tuple(stages.get(k, (0.0, 0))[0] / n for k in EXCHANGE_STAGES)
 
@@ -700,7 +701,7 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
         stages = _C.timing_read()
         _C.timing_enable(False)
         st = ar.stats()
-        st["exchange_wait_ms"], st["sh_rebuild_ms"] = _exchange_split(stages, st["calls"])
+        st["exchange_wait_ms"], st["sh_rebuild_ms"] = _exchange_split(stages, st["timed_calls"])
         plan = list(dgr.last_leaf_plan)
         ar.remove_hooks()
         del g, params

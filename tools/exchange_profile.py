@@ -136,7 +136,7 @@ def main():
                  "sync_wait_ms": round(1e3 * sync["t"] / max(sync["n"], 1), 4),
                  "plan": list(dgr.last_leaf_plan)}
             if ar is not None:
-                n = max(ar.stats()["calls"], 1)
+                n = max(ar.stats()["timed_calls"], 1)
                 r.update(wait_ms=round(stages["exchange_wait"][0] / n, 4),
                          rebuild_ms=round(stages["sh_rebuild"][0] / n, 4))
                 ar.remove_hooks()
