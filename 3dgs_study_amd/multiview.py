@@ -254,7 +254,6 @@ class GradAllReduce:
         # in a fresh tensor, reduced on its own at the end of the backward, and
         # __call__ adds it to the reduced bucket and reinstalls the views.
         self._early = True
-        self._early_version = self._bucket._version
         for p in self._reduced:
             p.grad = None
 
@@ -496,8 +495,6 @@ class GradAllReduce:
         # all-reduce is still in flight (queued at the end of the backward already,
         # unless nothing started there), and the compute stream waits for the bucket last
         self._sh_rebuild()
-        if self._early and self._bucket._version != self._early_version:
-            raise RuntimeError("GradAllReduce: the bucket was written while its all-reduce was in flight")
         self._begin("exchange_wait")
         if self._work is not None:
             self._work.wait()

@@ -919,10 +919,15 @@ def _late_path_worker(rank, world, port, out, views_per_step):
         reg = c * (opacity * opacity).sum()
         (reg + _AllWriter.apply(xyz, opacity, float(rank + 1) * (v + 1))).backward()
     started = list(_AllWriter.started)
+    # the late contribution landed in a tensor of its own, not in the bucket the
+    # collective was reading (the leaves' .grad were cleared at the early start)
+    bucket = ar._bucket
+    late_apart = opacity.grad is not None and not (
+        bucket.data_ptr() <= opacity.grad.data_ptr() < bucket.data_ptr() + bucket.numel() * 4)
     flat = ar()
     views_ok = all(flat.data_ptr() <= p.grad.data_ptr() < flat.data_ptr() + flat.numel() * 4 for p in (xyz, opacity))
     out[rank] = ([p.grad.clone() for p in (xyz, opacity)], [p.detach().clone() for p in (xyz, opacity)], started,
-                 views_ok)
+                 views_ok and late_apart)
     ar.remove_hooks()
     dist.destroy_process_group()
 

@@ -57,18 +57,20 @@ def main():
                                 device_id=dev if args.pg == "eager" else None)
 
     lib = _C.load_library()
-    orig = lib.gsr_forward_preprocess
     sync = {"t": 0.0, "n": 0}
 
-    def wrapped(*a):
-        t0 = time.perf_counter()
-        r = orig(*a)
-        sync["t"] += time.perf_counter() - t0
-        sync["n"] += 1
-        return r
+    def wrapper(orig):
+        def wrapped(*a):
+            t0 = time.perf_counter()
+            r = orig(*a)
+            sync["t"] += time.perf_counter() - t0
+            sync["n"] += 1
+            return r
+        return wrapped
 
-    if not args.no_wrap:
-        lib.gsr_forward_preprocess = wrapped
+    if not args.no_wrap:  # the forward's native call: its one host wait (two-call or one-call form)
+        lib.gsr_forward_preprocess = wrapper(lib.gsr_forward_preprocess)
+        lib.gsr_forward = wrapper(lib.gsr_forward)
     hostt = {}
     if args.host:  # wrap the calls on the step's host path and sum their wall time
         import multiview
