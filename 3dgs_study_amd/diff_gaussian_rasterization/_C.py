@@ -499,10 +499,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     gradient [P,3] there (gsr_backward_colors) and the returned ``dsh`` is None.
     ``dsh_planar`` — dsh is the [P,M,3] view of [M,P,3] coefficient planes
     (strides (3, 3P, 1); gsr_backward_planar), same values.
-    ``on_drgb`` (with ``drgb_out``) — called with a ``torch.cuda.Event`` recorded
-    right after drgb is written (gsr_backward_phase 1), once the per-Gaussian
-    backward (phase 2) is queued too: the caller starts exchanging drgb behind that
-    event, under the per-Gaussian backward.
+    ``on_drgb`` (with ``drgb_out``) — called (with None: no event) between the
+    kernels that write drgb (gsr_backward_phase 1) and the per-Gaussian backward
+    (phase 2): what the caller queues then — the exchange of drgb — follows drgb
+    and runs under the per-Gaussian backward.
     ``leaf`` — a ``LeafGrads``: the library writes the requested leaf gradients of
     the caller's activations itself (gsr_backward_phase) and returns None in place
     of the activation gradients they replace (dsh, dopacity, dscales, drot, and
@@ -580,14 +580,15 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     lg = ctypes.byref(leaf.struct(P, M, device, dsh_planar)) if leaf is not None else None
     tail = (_ptr(dsh), _ptr(drgb_out), _ptr(dscales), _ptr(drot), lg)
     if drgb_out is not None and on_drgb is not None:
-        # both phases are queued first, with an event between them: the caller's
-        # exchange of drgb waits for that event on a stream of its own, so it runs
-        # under the per-Gaussian backward and its host-side cost never delays it
+        # the caller's exchange of drgb starts between the phases: a collective
+        # launched then waits for exactly what the stream holds so far (drgb
+        # written), and runs under the per-Gaussian backward.  The device has the
+        # rest of the forward and the render backward queued at this point, so the
+        # launch's host time delays nothing (an event and a second stream for it
+        # cost the host ~25 us a step, and the exchange path is host-bound)
         _check(lib.gsr_backward_phase(*head, *tail, 1, stream), "rasterize_gaussians_backward")
-        ready = torch.cuda.Event()
-        ready.record(torch.cuda.current_stream(device))
+        on_drgb(None)
         _check(lib.gsr_backward_phase(*head, *tail, 2, stream), "rasterize_gaussians_backward")
-        on_drgb(ready)
     else:
         _check(lib.gsr_backward_phase(*head, *tail, 3, stream), "rasterize_gaussians_backward")
     return ret

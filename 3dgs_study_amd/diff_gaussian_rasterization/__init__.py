@@ -365,11 +365,13 @@ class _RasterizeGaussians(torch.autograd.Function):
         (d_means2D, d_colors, d_opacities, d_means3D, d_cov3D, d_sh, d_scales, d_rotations) = _call_native(
             lambda *a: _C.rasterize_gaussians_backward(*a, **kw), args, rs.debug, "snapshot_bw.dump", "backward")
         if plan:
-            for p, g in fresh:
-                p.grad = g
             views = {k: v[3] for k, v in plan.items() if v[3] is not None}
-            if views and ex is not None and hasattr(ex, "rasterizer_done"):  # the exchange may start right away
-                ex.rasterizer_done(views)
+            # the exchange may start right away; when it does, the bucket is its own
+            # and the leaves get their .grad back from it (multiview.GradAllReduce)
+            took = views and ex is not None and hasattr(ex, "rasterizer_done") and ex.rasterizer_done(views)
+            for p, g in fresh:
+                if not (took and any(g is v for vs in views.values() for v in vs)):
+                    p.grad = g
         return (d_means3D, d_means2D, d_sh, d_colors, d_opacities, d_scales, d_rotations, d_cov3D, None, None)
 
 
@@ -485,10 +487,12 @@ class _RasterizeModel(torch.autograd.Function):
                 img, rs.debug)
         d_means2D = _call_native(lambda *a: _C.rasterize_gaussians_backward(*a, **bkw), args, rs.debug,
                                  "snapshot_bw.dump", "backward")[0]
-        for p, g in fresh:
-            p.grad = g
-        if views and hasattr(ex, "rasterizer_done"):  # the exchange may start right away
-            ex.rasterizer_done(views)
+        # the exchange may start right away; when it does, the bucket is its own and
+        # the leaves get their .grad back from it (multiview.GradAllReduce)
+        took = views and hasattr(ex, "rasterizer_done") and ex.rasterizer_done(views)
+        if not took:
+            for p, g in fresh:
+                p.grad = g
         global last_leaf_plan
         last_leaf_plan = tuple(sorted(["means3D", "opacities", "rotations", "scales"] +
                                       ([] if sink_takes_sh else ["sh"])))

@@ -103,7 +103,10 @@ class GradAllReduce:
         self.timing_every = 4   # regions recorded on every 4th step (each event pair idles the device ~4 us)
         self._tstats = {"exchange_wait_ms": 0.0, "sh_rebuild_ms": 0.0, "calls": 0, "timed_calls": 0}
         self._prev_ex = None
-        self._hdr = None        # push()'s cached record header
+        self._hdr = None        # the record header's cached 4-float source
+        self._recs = []         # per view slot of a step: [record, header key] (reused step to step)
+        self._gouts = []        # per view slot: the all-gather's output (reused step to step)
+        self._sh_out = None     # (dc, rest, event): the SH rebuild queued beside the backward
         self._installed = False
         self._sh_on = sh is not None and (sh_force or self._active())
         self._bind()
@@ -130,6 +133,7 @@ class GradAllReduce:
         self.params, self._sh = self._resolve()
         self.numel = sum(p.numel() for p in self.params)
         self._reduced = [p for p in self.params if self._sh is None or not any(p is q for q in self._sh[1:])]
+        self._index = {id(p): i for i, p in enumerate(self._reduced)}  # (strong refs: ids are unique)
         self._bucket = self._views = None
         # hooks only while there is something to exchange: with one rank the leaves
         # carry none, and the rasterizer's fused leaf gradients apply as without us
@@ -172,10 +176,8 @@ class GradAllReduce:
         if self._bucket is None:
             ref = self._reduced[0]
             self._bucket = torch.empty(sum(p.numel() for p in self._reduced), dtype=torch.float32, device=ref.device)
-            self._views, off = [], 0
-            for p in self._reduced:
-                self._views.append(self._bucket[off:off + p.numel()].view_as(p))
-                off += p.numel()
+            parts = self._bucket.split([p.numel() for p in self._reduced])
+            self._views = [v.view(p.shape) for v, p in zip(parts, self._reduced)]
         return self._bucket
 
     @staticmethod
@@ -215,47 +217,48 @@ class GradAllReduce:
         self._queue_callback()
         out = {}
         for name, ls in leaves.items():
-            idx = [next((i for i, p in enumerate(self._reduced) if p is leaf), -1) for leaf in ls]
+            idx = [self._index.get(id(leaf), -1) for leaf in ls]
             if all(i >= 0 and (ls[j].grad is None or self._is_view(ls[j].grad, self._views[i]))
                    for j, i in enumerate(idx)):
                 out[name] = tuple(self._views[i] for i in idx)
         return out
 
-    def rasterizer_done(self, views: dict) -> None:
+    def rasterizer_done(self, views: dict) -> bool:
         """Called by the rasterizer's backward right after its kernels are queued, with
-        the bucket views it wrote (``leaf_bucket``'s answer).  On the step's last
-        backward, when those views cover every reduced parameter, the bucket is
-        complete already: its all-reduce starts here and the SH rebuild is queued
-        behind the backward's last kernel.  Done from the end-of-backward callback
-        instead, the host's round trip through the autograd engine left the device
-        idle for ~65 us per step (``tools/exchange_profile.py`` traces)."""
+        the bucket views it wrote (``leaf_bucket``'s answer), before it installs them
+        as the leaves' ``.grad``.  On the step's last backward, when those views cover
+        every reduced parameter, the bucket is complete already: its all-reduce
+        starts here, the SH rebuild is queued behind the backward's last kernel, and
+        True tells the rasterizer to leave the leaves' ``.grad`` unset (below).  Done
+        from the end-of-backward callback instead, the host's round trip through the
+        autograd engine left the device idle for ~65 us per step
+        (``tools/exchange_profile.py`` traces)."""
         if self._work is not None or self._bucket is None or self._backwards + 1 != self.views_per_step:
-            return
+            return False
         covered = {id(v) for vs in views.values() for v in vs if v is not None}
         if any(id(v) not in covered for v in self._views):
-            return
-        # The SH rebuild is queued first, right behind the backward's last kernel (it
-        # needs only the gathered records), and the bucket's all-reduce then starts
-        # behind an event marking that kernel: the collective's host-side launch
-        # (tens of us in ProcessGroupNCCL) no longer leaves the device idle before
-        # the rebuild, and the all-reduce runs beside it.
-        done = torch.cuda.Event() if self._bucket.is_cuda else None
-        if done is not None:
-            done.record()
+            return False
+        # The all-reduce is launched first, on the compute stream as it stands (RCCL's
+        # stream waits for the backward's kernels queued so far, not for what
+        # follows), then the SH rebuild.  The device is still a render or more behind
+        # the host here, so the launch order costs it nothing; what the exchange path
+        # costs is host time (each event / stream switch ~5-10 us on the step's
+        # critical host path, which the device waited for: exchange_profile traces).
+        self._work = dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._sh_rebuild()
-        self._work = self._launch(done, lambda: dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM,
-                                                                group=self.group, async_op=True))
         self.launched_in_backward = True
         # The bucket now belongs to the collective.  Another gradient path into a
         # reduced leaf (an extra loss term, a regulariser on _scaling ...) reaches
         # its AccumulateGrad after this backward — and would add in place into the
         # .grad it finds, i.e. into the bucket RCCL is reading, never to be reduced
-        # (ADVICE r4).  So the leaves' .grad are cleared: such a contribution lands
-        # in a fresh tensor, reduced on its own at the end of the backward, and
-        # __call__ adds it to the reduced bucket and reinstalls the views.
+        # (ADVICE r4).  So the leaves hold no .grad until __call__: such a
+        # contribution lands in a fresh tensor, reduced on its own at the end of the
+        # backward, and __call__ adds it to the reduced bucket and installs the views.
         self._early = True
         for p in self._reduced:
-            p.grad = None
+            if p.grad is not None:  # a view installed by an earlier backward of the step
+                p.grad = None
+        return True
 
     # ---- the end of each backward: start the bucket's all-reduce on the step's last
     def _queue_callback(self):
@@ -285,16 +288,12 @@ class GradAllReduce:
             return
         if self._backwards == self.views_per_step and self._work is None and not self._stale():
             bucket = self._pack()
-            done = torch.cuda.Event() if bucket.is_cuda else None
-            if done is not None:
-                done.record()
-            # the SH rebuild needs only the gathered records: queued here, behind the
-            # backward's last kernel, instead of after the host has returned from
-            # backward() into the caller's __call__ (a host round trip the device spent
-            # idle: 60-90 us per step); the bucket's all-reduce behind the pack, beside it
+            # the bucket's all-reduce behind the pack; the SH rebuild (it needs only the
+            # gathered records) queued here too, behind the backward's last kernel,
+            # instead of after the host has returned from backward() into the caller's
+            # __call__ (a host round trip the device spent idle: 60-90 us per step)
+            self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self._sh_rebuild()
-            self._work = self._launch(done, lambda: dist.all_reduce(bucket, op=dist.ReduceOp.SUM,
-                                                                    group=self.group, async_op=True))
             self.launched_in_backward = True
 
     # ---- the rasterizer's SH sink
@@ -320,31 +319,44 @@ class GradAllReduce:
                                "callables that return the current tensors")
         return ok
 
-    def _header(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int) -> None:
-        # the record's header [campos, degree]: one copy from a cached 4-float tensor
-        # (the view's camera is usually the same object step after step)
+    def _header(self, slot: list, campos: torch.Tensor, sh_degree: int) -> None:
+        """The record's header [campos, degree], written when it differs from what the
+        slot's record holds: one copy from a cached 4-float tensor (the view's camera
+        is usually the same tensor step after step, and then nothing is queued)."""
+        key = (campos, campos._version, int(sh_degree))
+        if slot[1] is not None and slot[1][0] is campos and slot[1][1:] == key[1:]:
+            return
         h = self._hdr
-        if h is None or h[0] is not campos or h[1] != campos._version or h[2] != int(sh_degree):
-            h = self._hdr = (campos, campos._version, int(sh_degree),
-                             torch.cat([campos.reshape(-1)[:3].float(),
-                                        torch.full((1,), float(sh_degree), device=rec.device)]))
-        rec[0:4].copy_(h[3])
+        if h is None or h[0] is not campos or h[1:3] != key[1:]:
+            h = self._hdr = key + (torch.cat([campos.reshape(-1)[:3].float(),
+                                              torch.full((1,), float(sh_degree), device=slot[0].device)]),)
+        slot[0][0:4].copy_(h[3])
+        slot[1] = key
+
+    def _slot(self, P: int) -> list:
+        # the record of this step's next view; a slot's record is reused the next step
+        # (stream order makes that safe: its gather and its rebuild are done before
+        # the next step's backward writes it, and the compute stream waited for both)
+        from diff_gaussian_rasterization import _C
+        i, n, dev = len(self._gathers), _C.sh_record_floats(P), self._sh[0].device
+        while len(self._recs) <= i:
+            self._recs.append(None)
+        slot = self._recs[i]
+        if slot is None or slot[0].numel() != n or slot[0].device != dev:
+            slot = self._recs[i] = [torch.empty(n, dtype=torch.float32, device=dev), None]
+        return slot
 
     def record(self, P: int, campos: torch.Tensor = None, sh_degree: int = None) -> torch.Tensor:
-        """A view's record; with the camera given its header is written now, on the
-        compute stream ahead of the backward's kernels (push's ready event then
-        covers it)."""
-        from diff_gaussian_rasterization import _C
-        rec = torch.empty(_C.sh_record_floats(P), dtype=torch.float32, device=self._sh[0].device)
+        """A view's record; with the camera given its header is written now (when it
+        changed), on the compute stream ahead of the backward's kernels."""
+        slot = self._slot(P)
         if campos is not None:
-            self._header(rec, campos, sh_degree)
-            self._hdr_rec = rec
-        return rec
+            self._header(slot, campos, sh_degree)
+        else:
+            slot[1] = None
+        return slot[0]
 
     def _side(self, device) -> "torch.cuda.Stream":
-        """A stream for the collectives' launches only (no kernel of ours runs on it):
-        a collective started on it behind an event waits for exactly the work that
-        event marks, not for whatever the compute stream has queued since."""
         st = getattr(self, "_side_stream", None)
         if st is None or st.device != device:
             st = self._side_stream = torch.cuda.Stream(device=device)
@@ -352,7 +364,8 @@ class GradAllReduce:
 
     def _launch(self, ready, fn):
         """fn() (a collective, async) ordered after `ready` (an event on the compute
-        stream, or None: after everything queued there so far)."""
+        stream: started from a stream of its own that waits for it), or with None
+        after everything queued so far."""
         if ready is None:
             return fn()
         st = self._side(ready.device if hasattr(ready, "device") and ready.device is not None
@@ -362,21 +375,55 @@ class GradAllReduce:
             return fn()
 
     def push(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int, ready=None) -> None:
-        """Exchange a view's record: with `ready` (an event after which its colour
-        gradient is written; the header written by record()) the all-gather starts
-        behind that event, else behind everything queued so far."""
-        if ready is None or getattr(self, "_hdr_rec", None) is not rec:
-            self._header(rec, campos, sh_degree)
-            ready = None  # the header copy was just queued: gather behind it
-        self._hdr_rec = None
+        """Exchange a view's record (from ``record``): the all-gather starts behind
+        everything queued on the compute stream so far (the rasterizer calls this
+        right after the kernels that write the colour gradient), or behind `ready`,
+        an event after which it is written."""
+        i = len(self._gathers)
+        slot = self._recs[i] if i < len(self._recs) else None
+        if slot is None or slot[0] is not rec:  # a record not made by record(): header now, gather behind it
+            slot = [rec, None]
+            ready = None
+        if slot[1] is None:
+            self._header(slot, campos, sh_degree)
         if self._active():
             world = dist.get_world_size(self.group)
-            out = torch.empty(world * rec.numel(), dtype=rec.dtype, device=rec.device)
+            while len(self._gouts) <= i:
+                self._gouts.append(None)
+            out = self._gouts[i]
+            if out is None or out.numel() != world * rec.numel() or out.device != rec.device:
+                out = self._gouts[i] = torch.empty(world * rec.numel(), dtype=rec.dtype, device=rec.device)
             work = self._launch(ready, lambda: dist.all_gather_into_tensor(out, rec, group=self.group,
                                                                            async_op=True))
             self._gathers.append((out, world, work))
+            if len(self._gathers) == self.views_per_step and rec.is_cuda:
+                self._rebuild_beside()
         else:
             self._gathers.append((rec, 1, None))
+
+    def _rebuild_beside(self) -> None:
+        """The step's last record is out: the SH rebuild goes on the exchange's own
+        stream right behind the gathers, beside the compute stream's per-Gaussian
+        backward (both HBM-bound, but the rebuild no longer waits for preprocess_bwd
+        and the compute stream no longer waits for the gathers).  ``__call__`` makes
+        the compute stream wait for it and installs the gradients.  The outputs come
+        from the compute stream's pool: their block was last used by compute-stream
+        work ordered before this step's colour gradient, which the gathers (and so
+        the rebuild) follow; record_stream keeps a later reuse behind the rebuild."""
+        xyz, f_dc, f_rest = self._sh
+        dc, rest = torch.empty_like(f_dc), torch.empty_like(f_rest)
+        side = self._side(xyz.device)
+        with torch.cuda.stream(side):
+            for _, _, w in self._gathers:
+                w.wait()
+            self._begin("sh_rebuild")
+            self._rebuild_into(dc, rest)
+            self._end("sh_rebuild")
+            done = torch.cuda.Event()
+            done.record(side)
+        dc.record_stream(side)
+        rest.record_stream(side)
+        self._sh_out = (dc, rest, done)
 
     def _sh_rebuild(self) -> None:
         """The compute stream waits for the records' all-gather, then rebuilds the SH
@@ -392,30 +439,35 @@ class GradAllReduce:
         self._finish_sh()
         self._end("sh_rebuild")
 
-    def _finish_sh(self) -> None:
-        xyz, f_dc, f_rest = self._sh
-        if not self._gathers:
-            return
-        for _, _, w in self._gathers:
-            if w is not None:
-                w.wait()
+    def _rebuild_into(self, dc: torch.Tensor, rest: torch.Tensor) -> None:
         # gathered buffers hold [rank 0 .. world-1] per push; with several views per
         # rank the sum runs push by push (identical order on every rank)
+        xyz = self._sh[0]
         recs = torch.cat([o for o, _, _ in self._gathers]) if len(self._gathers) > 1 else self._gathers[0][0]
         nviews = sum(n for _, n, _ in self._gathers)
         self._gathers = []
-        dc = torch.empty_like(f_dc)
-        rest = torch.empty_like(f_rest)
         if self._rebuild is not None:
             self._rebuild(xyz.detach(), recs, nviews, dc, rest)
         else:
             from diff_gaussian_rasterization import _C
             _C.sh_grad_from_colors(xyz.detach(), recs, nviews, dc, rest if rest.numel() else None)
-        for p, g in ((f_dc, dc), (f_rest, rest)):
+
+    def _install_sh(self, dc: torch.Tensor, rest: torch.Tensor) -> None:
+        for p, g in ((self._sh[1], dc), (self._sh[2], rest)):
             if p.grad is None:
                 p.grad = g
             else:
                 p.grad.add_(g)
+
+    def _finish_sh(self) -> None:
+        if not self._gathers:
+            return
+        for _, _, w in self._gathers:
+            if w is not None:
+                w.wait()
+        dc, rest = torch.empty_like(self._sh[1]), torch.empty_like(self._sh[2])
+        self._rebuild_into(dc, rest)
+        self._install_sh(dc, rest)
 
     def _split(self, flat, idx):
         out, off = [], 0
@@ -496,11 +548,16 @@ class GradAllReduce:
         # unless nothing started there), and the compute stream waits for the bucket last
         self._sh_rebuild()
         self._begin("exchange_wait")
+        sh_out, self._sh_out = self._sh_out, None
+        if sh_out is not None:
+            torch.cuda.current_stream(sh_out[0].device).wait_event(sh_out[2])
         if self._work is not None:
             self._work.wait()
         if self._extra is not None:
             self._extra[2].wait()
         self._end("exchange_wait")
+        if sh_out is not None:
+            self._install_sh(sh_out[0], sh_out[1])
         if self._early:  # the views become the leaves' .grad again, plus what came after the start
             extra = dict(zip(self._extra[0], self._split(self._extra[1], self._extra[0]))) if self._extra else {}
             for i, (p, v) in enumerate(zip(self._reduced, self._views)):

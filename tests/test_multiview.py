@@ -201,12 +201,17 @@ def _gpu_worker(rank, world, port, out, sh_exchange=False):
     reducer = GradAllReduce(params, sh=(params[0], params[1], params[2]) if sh_exchange else None)
     train_step.train_step(cam, g, target, torch.zeros(3, device=dev))
     assert reducer.pending == 1 and reducer.launched_in_backward
-    # the SH records' gather was consumed inside backward: the rebuild is queued
-    # behind the rasterizer's kernels (GradAllReduce.rasterizer_done)
+    # the SH records' gather was consumed inside backward: the rebuild is queued on
+    # the exchange's stream right behind it (GradAllReduce._rebuild_beside), and the
+    # SH gradients reach the leaves when the reducer is called
     assert not reducer._gathers
     if sh_exchange:
-        assert params[1].grad is not None and params[2].grad is not None
+        assert reducer._sh_out is not None
+        assert params[1].grad is None and params[2].grad is None
     reducer()
+    if sh_exchange:
+        assert reducer._sh_out is None
+        assert params[1].grad is not None and params[2].grad is not None
     out[rank] = [p.grad.detach().cpu() for p in g.params()]
     dist.destroy_process_group()
 
@@ -339,6 +344,43 @@ def test_sh_grad_from_colors_kernel_vs_oracle(dev, oracle):
         got = dc.cpu().numpy() if rest is None else np.concatenate([dc.cpu().numpy(), rest.cpu().numpy()], axis=1)
         err = np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30)
         assert err <= 1e-6, (M, err)
+
+
+@pytest.mark.gpu
+def test_sh_grad_from_colors_one_view_form_bit_identical(dev):
+    """One record takes the one-view kernel (products formed at write-out); the
+    same record followed by an all-zero one takes the general kernel (the zero
+    view is skipped).  The two agree bit for bit — signed zeros included — for
+    every degree, ragged sizes, zero and signed-zero rows, and a Gaussian at the
+    camera centre."""
+    from diff_gaussian_rasterization import _C
+
+    rng = np.random.default_rng(21)
+    for P in (1, 7, 256, 4_099):
+        for deg in (3, 2, 1, 0):
+            means = rng.normal(size=(P, 3)).astype(np.float32)
+            campos = (rng.normal(size=3) * 6).astype(np.float32)
+            means[P // 2] = campos  # zero-length direction
+            drgb = rng.normal(size=(P, 3)).astype(np.float32)
+            drgb[::5] = 0
+            drgb[P // 2] = 0
+            drgb[1::7, 1] = -0.0
+            stride = _C.sh_record_floats(P)
+            rec = np.zeros((2, stride), np.float32)
+            rec[:, :3], rec[:, 3], rec[0, 4:4 + 3 * P] = campos, deg, drgb.reshape(-1)
+            m = torch.from_numpy(means).to(dev)
+            r = torch.from_numpy(rec).to(dev)
+            out = []
+            for V in (1, 2):
+                dc = torch.full((P, 1, 3), 7.0, device=dev)
+                rest = torch.full((P, 15, 3), 7.0, device=dev)
+                _C.sh_grad_from_colors(m, r, V, dc, rest)
+                out.append(torch.cat([dc, rest], dim=1).cpu())
+            a, b = out
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32)), (P, deg)
+            assert not torch.isnan(a).any()
+            if deg < 3:
+                assert (a[:, (deg + 1) ** 2:] == 0).all()
 
 
 # ---------------------------------------------------------------- several views per rank, re-binding, training
