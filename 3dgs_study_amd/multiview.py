@@ -58,6 +58,17 @@ import torch.distributed as dist
 ParamSource = Union[Sequence[torch.Tensor], Callable[[], Sequence[torch.Tensor]]]
 
 
+class _Queued:
+    """A collective queued in line on the compute stream: nothing left to wait for."""
+
+    @staticmethod
+    def wait():
+        return True
+
+
+_QUEUED = _Queued()
+
+
 def views_for_rank(rank: int, world: int, num_views: int) -> list:
     """Round-robin view assignment: rank r renders views r, r+world, ..."""
     return list(range(rank, num_views, world))
@@ -107,6 +118,8 @@ class GradAllReduce:
         self._recs = []         # per view slot of a step: [record, header key] (reused step to step)
         self._gouts = []        # per view slot: the all-gather's output (reused step to step)
         self._sh_out = None     # (dc, rest, event): the SH rebuild queued beside the backward
+        self._gather_done = None  # event after this step's in-stream record gathers
+        self._nccl = None       # the group's backend is RCCL (collectives in stream order, below)
         self._installed = False
         self._sh_on = sh is not None and (sh_force or self._active())
         self._bind()
@@ -244,7 +257,7 @@ class GradAllReduce:
         # the host here, so the launch order costs it nothing; what the exchange path
         # costs is host time (each event / stream switch ~5-10 us on the step's
         # critical host path, which the device waited for: exchange_profile traces).
-        self._work = dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._work = self._reduce(self._bucket)
         self._sh_rebuild()
         self.launched_in_backward = True
         # The bucket now belongs to the collective.  Another gradient path into a
@@ -259,6 +272,31 @@ class GradAllReduce:
             if p.grad is not None:  # a view installed by an earlier backward of the step
                 p.grad = None
         return True
+
+    def _in_stream(self, t: torch.Tensor) -> bool:
+        """RCCL on device tensors: collectives are issued as non-async ops, which
+        torch (>= 2.7) runs on the caller's current stream — no event recorded on
+        the compute stream for RCCL's own stream to wait on, and no wait back (each
+        such cross-queue step idled the compute stream 5-7 us, two hops ~21 us:
+        exchange_profile traces); the host is not blocked (tools/pg_stream_probe.py).
+        gloo keeps async work objects."""
+        if not t.is_cuda:
+            return False
+        if self._nccl is None:
+            self._nccl = dist.get_backend(self.group) == "nccl"
+        return self._nccl
+
+    def _reduce(self, bucket: torch.Tensor):
+        """The bucket's all-reduce, started now (behind everything queued on the
+        compute stream).  In stream order it runs on the compute stream itself,
+        after the records' gather on the exchange stream has completed (one
+        collective of a communicator at a time)."""
+        if self._in_stream(bucket):
+            if self._gather_done is not None:
+                torch.cuda.current_stream(bucket.device).wait_event(self._gather_done)
+            dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group)
+            return _QUEUED
+        return dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     # ---- the end of each backward: start the bucket's all-reduce on the step's last
     def _queue_callback(self):
@@ -292,7 +330,7 @@ class GradAllReduce:
             # gathered records) queued here too, behind the backward's last kernel,
             # instead of after the host has returned from backward() into the caller's
             # __call__ (a host round trip the device spent idle: 60-90 us per step)
-            self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self._work = self._reduce(bucket)
             self._sh_rebuild()
             self.launched_in_backward = True
 
@@ -393,8 +431,23 @@ class GradAllReduce:
             out = self._gouts[i]
             if out is None or out.numel() != world * rec.numel() or out.device != rec.device:
                 out = self._gouts[i] = torch.empty(world * rec.numel(), dtype=rec.dtype, device=rec.device)
-            work = self._launch(ready, lambda: dist.all_gather_into_tensor(out, rec, group=self.group,
-                                                                           async_op=True))
+            if self._in_stream(rec):
+                # in stream order on the exchange stream, behind the colour gradient
+                # (or `ready`); the SH rebuild follows it there, and the bucket's
+                # all-reduce waits for this event
+                side = self._side(rec.device)
+                if ready is None:
+                    side.wait_stream(torch.cuda.current_stream(rec.device))
+                else:
+                    side.wait_event(ready)
+                with torch.cuda.stream(side):
+                    dist.all_gather_into_tensor(out, rec, group=self.group)
+                    self._gather_done = torch.cuda.Event()
+                    self._gather_done.record(side)
+                work = None
+            else:
+                work = self._launch(ready, lambda: dist.all_gather_into_tensor(out, rec, group=self.group,
+                                                                               async_op=True))
             self._gathers.append((out, world, work))
             if len(self._gathers) == self.views_per_step and rec.is_cuda:
                 self._rebuild_beside()
@@ -415,7 +468,8 @@ class GradAllReduce:
         side = self._side(xyz.device)
         with torch.cuda.stream(side):
             for _, _, w in self._gathers:
-                w.wait()
+                if w is not None:
+                    w.wait()
             self._begin("sh_rebuild")
             self._rebuild_into(dc, rest)
             self._end("sh_rebuild")
@@ -465,6 +519,8 @@ class GradAllReduce:
         for _, _, w in self._gathers:
             if w is not None:
                 w.wait()
+        if self._gather_done is not None:  # gathered in stream order on the exchange stream
+            torch.cuda.current_stream(self._sh[0].device).wait_event(self._gather_done)
         dc, rest = torch.empty_like(self._sh[1]), torch.empty_like(self._sh[2])
         self._rebuild_into(dc, rest)
         self._install_sh(dc, rest)
@@ -541,7 +597,7 @@ class GradAllReduce:
         if self._work is None:
             bucket = self._pack()
             if self._active():
-                self._work = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                self._work = self._reduce(bucket)
         bucket = self._bucket
         # the SH rebuild needs only the gathered records: it runs while the bucket's
         # all-reduce is still in flight (queued at the end of the backward already,
@@ -567,6 +623,7 @@ class GradAllReduce:
         self._tstats["timed_calls"] += int(self._timed_now())
         self._tstats["calls"] += 1
         self._early = False
+        self._gather_done = None
         self._extra = None
         self._work = None
         self._bucket = self._views = None  # the grads keep the storage; next step gets a fresh bucket
