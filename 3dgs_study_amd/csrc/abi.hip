@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <unordered_set>
 #include <utility>
 #include <vector>
@@ -48,6 +49,26 @@ void prepared_set(const void *geom, bool on) {
 bool prepared_take(const void *geom) {
     std::lock_guard<std::mutex> lk(g_prep_mu);
     return g_prepared.erase(geom) != 0;
+}
+// binning buffers whose last forward recorded its chunk cull masks for the backward
+// (render_fwd with GSR_FLAG_PREPARE_BACKWARD), with the buffer's capacity (the
+// masks' place in it): every forward into a buffer records or forgets it, and a
+// backward finds the masks only for the buffer its forward wrote.  Without a
+// record the backward culls itself (same entries, same pairs).
+std::unordered_map<const void *, int64_t> g_qmask;
+void qmask_set(const void *binning, int64_t cap) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    if (cap <= 0) {
+        g_qmask.erase(binning);
+        return;
+    }
+    if (g_qmask.size() > 4096) g_qmask.clear();
+    g_qmask[binning] = cap;
+}
+int64_t qmask_get(const void *binning) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    const auto it = g_qmask.find(binning);
+    return it == g_qmask.end() ? 0 : it->second;
 }
 // the num_rendered read-back's event (per host thread, like g_pinned): timing off
 // and no system-scope fence — the pinned words are written with system-scope stores
@@ -338,10 +359,12 @@ static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t
     if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s,
                             [&] {
                                 return launch_render_fwd(*in, geom, n > 0 ? binning : nullptr, img, out_color,
-                                                         prep ? (float *)acc : nullptr, acc_bytes, s);
+                                                         prep ? (float *)acc : nullptr, acc_bytes, s,
+                                                         prep && n > 0 ? cap : 0);
                             }),
                       "render", dbg, s))
         return rc;
+    if (binning) qmask_set(binning, prep && n > 0 ? cap : 0);
     if (!prep) {  // the L1 loss, if asked for, on its own
         prepared_set(geom, false);
         return gt ? step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", dbg, s)
@@ -482,7 +505,10 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
                               "backward prepare", dbg, s))
                 return rc;
         if (num_rendered > 0) {
-            if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] { return launch_render_bwd(*in, geom, binning, img, seed ? nullptr : dL_dout_color, seed, acc, s); }),
+            if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] {
+                                  return launch_render_bwd(*in, geom, binning, img, seed ? nullptr : dL_dout_color,
+                                                           seed, acc, s, qmask_get(binning));
+                              }),
                               "render backward", dbg, s))
                 return rc;
         }

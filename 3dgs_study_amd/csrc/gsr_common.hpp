@@ -218,8 +218,18 @@ struct BinningLayout {
     size_t totals;  // uint32 [RADIX]
     size_t totals1; // uint32 [RADIX] the first tile pass's digit totals (the second pass's segments)
     size_t seg_table; // uint32 [2][RADIX + 1] the second pass's segment table: first block, first item
+    size_t qmask;   // uint64 [4][qmask_stride] per quadrant, per 64-entry chunk of its tile's list: the
+                    // entries that reach the quadrant (render_fwd's cull), for render_bwd (qmask_index)
+    size_t qmask_stride;
     size_t bytes;
 };
+// The chunk-mask slot of quadrant w's chunk j of tile t (list range r): (r.x >> 6) + t + j
+// is distinct for every (tile, chunk) of a sorted list whose tile ranges follow each
+// other (tile t + 1 starts at r.y: (r.y >> 6) + 1 >= (r.x >> 6) + ceil((r.y - r.x) / 64)),
+// and below cap / 64 + tiles + 1.
+__host__ __device__ inline size_t qmask_index(uint32_t rx, int tile, int j) {
+    return (size_t)(rx >> 6) + (size_t)tile + (size_t)j;
+}
 __host__ __device__ inline BinningLayout binning_layout(int64_t cap, int W, int H) {
     BinningLayout L;
     size_t n = (size_t)(cap > 0 ? cap : 1);
@@ -233,6 +243,8 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t cap, int W, int 
     L.totals = take((size_t)RADIX * 4);
     L.totals1 = take((size_t)RADIX * 4);
     L.seg_table = take((size_t)2 * (RADIX + 1) * 4);
+    L.qmask_stride = n / 64 + (size_t)grid_dims(W, H).tiles + 2;
+    L.qmask = take(4 * L.qmask_stride * 8);
     L.bytes = o;
     return L;
 }

@@ -27,7 +27,8 @@ namespace gsr {
 
 // Ablation switches for timing builds (results are wrong with any of them on):
 // GSR_XB_NOSWZ: the exchanges read the lane's own value (no ds_swizzle),
-// GSR_XB_NOTRANS: exp and rcp replaced by multiplies.
+// GSR_XB_NOTRANS: exp and rcp replaced by multiplies,
+// GSR_XB_NOPAIRS: no pair loop (the chunk stream, cull and staging alone).
 #ifdef GSR_XB_NOSWZ
 #define GSR_SWZ(v, pat) (v)
 #else
@@ -54,6 +55,9 @@ struct RenderBwdArgs {
     const float *l1_image, *l1_gt, *l1_dloss;
     float l1_n;
     float *accum;
+    // the forward's chunk cull masks (render_fwd.hip; binning's qmask region), or NULL
+    const uint64_t *qmask;
+    size_t qmask_stride;
 };
 __device__ __forceinline__ float l1_sign(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }  // torch.sign
 
@@ -89,6 +93,9 @@ __device__ __forceinline__ float swz_fold(float c) {
 }
 
 
+// MASKS: the forward's chunk cull masks are in a.qmask (a separate instantiation:
+// one kernel carrying both the mask and the cull path ran out of VGPRs)
+template <bool MASKS>
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(6))) render_bwd_kernel(RenderBwdArgs a) {
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
     // workgroup 8 r + x: XCD x's r-th quadrant in bucket order (gsr_blend.hpp)
@@ -266,8 +273,16 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // fused reduce-scatter of their 18 sums.  The survivors sit in records 1..ns
     // (record 0 is the odd pair's dummy b), so pair (a, b) = records (s + 1, s) and
     // both are read from ONE VGPR address with immediate offsets.
-    auto replay_chunk = [&](int lo, float4 A, float4 B, float4 C) {
-        const bool rel = (lo + lane >= 0) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
+    // the forward's cull masks of this quadrant (chunk j of the tile's list at qm[j]), or NULL
+    const uint64_t *qm = MASKS ? a.qmask + (size_t)w * a.qmask_stride + qmask_index(r.x, tile, 0) : nullptr;
+    auto replay_chunk = [&](int lo, float4 A, float4 B, float4 C, uint64_t m) {
+        // the chunk's entries that reach the quadrant: the forward's mask, or the
+        // same exact cull on the same records; none at or past `end`
+        bool rel;
+        if constexpr (MASKS)
+            rel = ((m >> lane) & 1ull) != 0 && lo + lane < end;  // (clearing the bits past end in m spilled VGPRs)
+        else
+            rel = (lo + lane < end) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
         const uint64_t mask = __ballot(rel);
         if (rel) stage_quad(st.rec[survivor_slot(mask, 1)], A, B, C, lane);
         const int ns = __builtin_popcountll(mask);
@@ -318,6 +333,9 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         };
         // (no early-out for pairs without a contributing pixel: 98.6% of the
         // walked pairs have one at config C, the test cost more than it saved)
+#ifdef GSR_XB_NOPAIRS
+        if (ns < 0)  // timing build: the chunk stream and cull alone
+#endif
         for (int k = ns - 1; k >= 0; k -= 2) {
             const bool two = k >= 1;  // wave-uniform
             Cur c;
@@ -329,30 +347,48 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             emit(reduce_sum(qa, qb), gida, gidb, two);
         }
     };
-    // Double-buffered backwards stream, unrolled by two so the buffers swap roles
-    // instead of being copied (see render_fwd.hip).  Indices are clamped so every
-    // load is unconditional; the one wait per chunk also drains the previous
-    // chunk's accumulator atomics, none are waited for inside the Gaussian loop.
-    const float4 *sp = a.splats + 3 * (size_t)list[max(end - 64 + lane, 0)];
+    // Double-buffered backwards stream over the forward's chunks (list positions
+    // [64 j, 64 j + 64), from the one holding entry end - 1 down to 0: the chunks the
+    // forward culled, so its masks apply and every backward pairs the survivors
+    // alike), unrolled by two so the buffers swap roles instead of being copied (see
+    // render_fwd.hip).  Indices are clamped so every load is unconditional; with the
+    // forward's masks a lane whose entry misses the quadrant loads the chunk's first
+    // survivor's record instead (one line for all of them).  The one wait per chunk
+    // also drains the previous chunk's accumulator atomics, none are waited for
+    // inside the Gaussian loop.
+    const int jend = (end - 1) >> 6, e1 = end - 1;
+    auto cmask = [&](int j) -> uint64_t { return !MASKS || j < 0 ? ~0ull : qm[j]; };
+    auto pick = [&](uint32_t idx, uint64_t m) -> uint32_t {
+        if constexpr (!MASKS) return idx;
+        const uint32_t first = __builtin_amdgcn_readlane(idx, m ? __builtin_ctzll(m) : 0);
+        return ((m >> lane) & 1ull) ? idx : first;
+    };
+    auto at_list = [&](int j) { return list[min(max(64 * j + lane, 0), e1)]; };
+    uint64_t mj = cmask(jend), mb = cmask(jend - 1), ma, mc;
+    const float4 *sp = a.splats + 3 * (size_t)pick(at_list(jend), mj);
     float4 A0 = sp[0], B0 = sp[1], C0 = sp[2], A1, B1, C1;
-    uint32_t idx_a, idx_b = list[max(end - 128 + lane, 0)];
-    for (int lo = end - 64;;) {
-        idx_a = list[max(lo - 128 + lane, 0)];
-        sp = a.splats + 3 * (size_t)idx_b;
+    uint32_t idx_a, idx_b = at_list(jend - 1);
+    for (int j = jend;;) {
+        idx_a = at_list(j - 2);
+        ma = cmask(j - 2);
+        sp = a.splats + 3 * (size_t)pick(idx_b, mb);
         A1 = sp[0];
         B1 = sp[1];
         C1 = sp[2];
         wait_vmcnt_4();
-        replay_chunk(lo, A0, B0, C0);
-        if ((lo -= 64) + 64 <= 0) break;
-        idx_b = list[max(lo - 128 + lane, 0)];
-        sp = a.splats + 3 * (size_t)idx_a;
+        replay_chunk(64 * j, A0, B0, C0, mj);
+        if (--j < 0) break;
+        idx_b = at_list(j - 2);
+        mc = cmask(j - 2);
+        sp = a.splats + 3 * (size_t)pick(idx_a, ma);
         A0 = sp[0];
         B0 = sp[1];
         C0 = sp[2];
         wait_vmcnt_4();
-        replay_chunk(lo, A1, B1, C1);
-        if ((lo -= 64) + 64 <= 0) break;
+        replay_chunk(64 * j, A1, B1, C1, mb);
+        if (--j < 0) break;
+        mj = ma;
+        mb = mc;
     }
 }
 
@@ -480,7 +516,8 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
 }
 
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, const void *img,
-                             const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s) {
+                             const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s,
+                             int64_t qmask_cap) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -505,7 +542,17 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.flags = at<uint32_t>(const_cast<void *>(geom), G.order_cnt) + ORDER_FILED;
     a.qlist = at<uint32_t>(img, Im.qlist);
     a.maxc = order_max_per_xcd(4 * g.tiles);
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);
+    a.qmask = nullptr;
+    a.qmask_stride = 0;
+    if (qmask_cap > 0) {
+        const BinningLayout B = binning_layout(qmask_cap, in.W, in.H);
+        a.qmask = at<uint64_t>(binning, B.qmask);
+        a.qmask_stride = B.qmask_stride;
+    }
+    if (a.qmask)
+        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);
+    else
+        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

@@ -40,6 +40,10 @@ struct RenderFwdArgs {
     // however many forwards ran on the geom buffer since its preprocess
     uint32_t *order_cnt;
     uint32_t *l1_ticket;  // img's L1 finish ticket (gsr_l1.hpp), cleared by workgroup 0 for bwd_prepare_kernel
+    // GSR_FLAG_PREPARE_BACKWARD: each chunk's cull mask, for render_bwd (binning's
+    // qmask: quadrant w at w * qmask_stride, chunk slot qmask_index), or NULL
+    uint64_t *qmask;
+    size_t qmask_stride;
 };
 
 #ifndef GSR_FWD_GROUP
@@ -90,11 +94,16 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     if (__any(inside) && n > 0) {
         const uint32_t *list = a.point_list + r.x;
         const int nm1 = n - 1;
+        uint64_t *qm = a.qmask ? a.qmask + (size_t)w * a.qmask_stride + qmask_index(r.x, tile, 0) : nullptr;
         // Blend one 64-entry chunk starting at list position pos (lane l <-> entry
         // pos + l); returns true once every pixel of the quadrant is saturated.
         auto blend_chunk = [&](int pos, float4 A, float4 B, float4 C) -> bool {
             const bool rel = (pos + lane < n) && quad_hit(A.x, A.y, A.z, A.w, B.x, C.z, (float)qx0, (float)qy0);
             const uint64_t mask = __ballot(rel);
+            // the backward replays exactly these entries (the same cull on the same
+            // records): one 8-B store per chunk spares it the cull and the gathers of
+            // the entries that miss the quadrant
+            if (qm && lane == 0) qm[pos >> 6] = mask;
             if (rel) stage_quad(st.rec[survivor_slot(mask, 0)], A, B, C, pos + lane + 1);
             const int ns = __builtin_popcountll(mask);
             stage_zero(st.rec[ns], lane);
@@ -222,7 +231,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
 }
 
 hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binning, void *img, float *out_color,
-                             float *acc_zero, size_t acc_bytes, hipStream_t s) {
+                             float *acc_zero, size_t acc_bytes, hipStream_t s, int64_t qmask_cap) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -243,6 +252,13 @@ hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binni
     a.zero_n4 = acc_zero ? acc_bytes / sizeof(float4) : 0;
     a.order_cnt = at<uint32_t>(geom, G.order_cnt);
     a.l1_ticket = at<uint32_t>(img, Im.l1_ticket);
+    a.qmask = nullptr;
+    a.qmask_stride = 0;
+    if (binning && qmask_cap > 0) {
+        const BinningLayout B = binning_layout(qmask_cap, in.W, in.H);
+        a.qmask = at<uint64_t>(const_cast<void *>(binning), B.qmask);
+        a.qmask_stride = B.qmask_stride;
+    }
     hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
