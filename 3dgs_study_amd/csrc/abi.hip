@@ -465,8 +465,9 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
                          float *drgb, float *dscales, float *drot, void *stream, int dsh_planar = 0,
                          int phases = 3, const gsr_leaf_grads *leaf = nullptr) {
     // phases: bit 0 = accumulator zeroing + render_bwd (+ the colour gradient into
-    // drgb), bit 1 = preprocess_bwd.  The view-parallel exchange runs them as two
-    // calls and starts its all-gather of drgb in between.
+    // drgb), bit 1 = preprocess_bwd, bit 2 = the colour gradient apart (below).  The
+    // view-parallel exchange runs them as separate calls and starts its all-gather of
+    // drgb in between.
     if (int rc = validate(in, false)) return rc;
     if (in->P == 0) return GSR_OK;
     if (!radii || !geom || !img || !dL_dout_color || (num_rendered > 0 && !binning))
@@ -512,13 +513,16 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
                               "render backward", dbg, s))
                 return rc;
         }
-        if (colors) {
-            const GeomLayout G = geom_layout(in->P, in->W, in->H);
-            if (int rc = step(launch_colors_from_accum(in->P, radii, at<uint8_t>(const_cast<void *>(geom), G.off[GSR_GEOM_CLAMPED]),
-                                                       acc, drgb, s),
-                              "colour gradient", dbg, s))
-                return rc;
-        }
+    }
+    // the colour gradient: with the render half, unless GSR_PHASE_COLOURS_APART asks
+    // for it in a call of its own (on the caller's exchange stream, beside the
+    // per-Gaussian half); that bit without the render half is that call
+    if (colors && ((phases & 1) != 0) == ((phases & 4) == 0)) {
+        const GeomLayout G = geom_layout(in->P, in->W, in->H);
+        if (int rc = step(launch_colors_from_accum(in->P, radii, at<uint8_t>(const_cast<void *>(geom), G.off[GSR_GEOM_CLAMPED]),
+                                                   acc, drgb, s),
+                          "colour gradient", dbg, s))
+            return rc;
     }
     if (!(phases & 2)) return GSR_OK;
     // with the colour gradient taken by the exchange, preprocess_bwd still reads the
@@ -571,7 +575,7 @@ int gsr_backward_phase(const gsr_inputs *in, const int32_t *radii, const void *g
                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,
                        float *drgb, float *dscales, float *drot, const gsr_leaf_grads *leaf, int32_t phases,
                        void *stream) {
-    if (phases < 1 || phases > 3) return fail(GSR_ERR_ARGS, "phases must be 1, 2 or 3 (got %d)", phases);
+    if (phases < 1 || phases > 7) return fail(GSR_ERR_ARGS, "phases must be 1 .. 7 (got %d)", phases);
     if (in && in->P > 0 && drgb && in->sh && in->D > 3) return fail(GSR_ERR_ARGS, "sh_degree > 3 is not supported");
     return backward_impl(in, radii, geom, binning, img, num_rendered, dL_dout_color, accum, dmeans2D, dcolors,
                          dopacity, dmeans3D, dcov3D, dsh, drgb, dscales, drot, stream, leaf ? leaf->dsh_planar : 0,

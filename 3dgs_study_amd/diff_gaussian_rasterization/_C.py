@@ -301,6 +301,7 @@ def _stream(device):
 FLAG_PREPARE_BACKWARD = 1  # gsr.h gsr_flags
 FLAG_L1_SEED = 2
 NEED_BINNING = 5  # gsr.h gsr_status: gsr_forward's binning capacity was too small
+PHASE_COLOURS_APART = 4  # gsr.h gsr_backward_phase: the colour gradient in a call of its own
 
 
 # ------------------------------------------------------------------ binning capacity
@@ -490,7 +491,7 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                  viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
                                  geomBuffer, R, binningBuffer, imageBuffer, debug, drgb_out=None, dsh_planar=False,
-                                 on_drgb=None, leaf=None, opacities=None, inputs=None, l1_seed=None):
+                                 on_drgb=None, leaf=None, opacities=None, inputs=None, l1_seed=None, drgb_apart=False):
     """-> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot)
 
     Not upstream (keyword-only extensions; the defaults are upstream's behaviour):
@@ -502,7 +503,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     ``on_drgb`` (with ``drgb_out``) — called (with None: no event) between the
     kernels that write drgb (gsr_backward_phase 1) and the per-Gaussian backward
     (phase 2): what the caller queues then — the exchange of drgb — follows drgb
-    and runs under the per-Gaussian backward.
+    and runs under the per-Gaussian backward.  With ``drgb_apart`` the render half
+    leaves drgb out (GSR_PHASE_COLOURS_APART) and ``on_drgb`` gets a function that
+    queues drgb's kernel on the current stream: the caller runs it on its exchange
+    stream (after the render half), beside the per-Gaussian backward.
     ``leaf`` — a ``LeafGrads``: the library writes the requested leaf gradients of
     the caller's activations itself (gsr_backward_phase) and returns None in place
     of the activation gradients they replace (dsh, dopacity, dscales, drot, and
@@ -586,8 +590,17 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         # rest of the forward and the render backward queued at this point, so the
         # launch's host time delays nothing (an event and a second stream for it
         # cost the host ~25 us a step, and the exchange path is host-bound)
-        _check(lib.gsr_backward_phase(*head, *tail, 1, stream), "rasterize_gaussians_backward")
-        on_drgb(None)
+        if drgb_apart:
+            _check(lib.gsr_backward_phase(*head, *tail, 1 | PHASE_COLOURS_APART, stream),
+                   "rasterize_gaussians_backward")
+
+            def write_drgb():
+                _check(lib.gsr_backward_phase(*head, *tail, PHASE_COLOURS_APART, _stream(device)),
+                       "rasterize_gaussians_backward (colour gradient)")
+            on_drgb(write_drgb)
+        else:
+            _check(lib.gsr_backward_phase(*head, *tail, 1, stream), "rasterize_gaussians_backward")
+            on_drgb(None)
         _check(lib.gsr_backward_phase(*head, *tail, 2, stream), "rasterize_gaussians_backward")
     else:
         _check(lib.gsr_backward_phase(*head, *tail, 3, stream), "rasterize_gaussians_backward")

@@ -261,6 +261,17 @@ def set_grad_exchange(ex):
 set_sh_grad_sink = set_grad_exchange  # the round-1 name
 
 
+def _drgb_hooks(ex, rec, rs) -> dict:
+    """The backward's keywords that hand the view's colour-gradient record to the
+    exchange: with ``colours_apart`` the exchange queues the colour kernel itself (on
+    its own stream, beside the per-Gaussian backward) and then its all-gather
+    (``push(..., write=)``); otherwise the gather starts after the library wrote it."""
+    if getattr(ex, "colours_apart", False):
+        return {"drgb_apart": True,
+                "on_drgb": lambda write: ex.push(rec, rs.campos, rs.sh_degree, write=write)}
+    return {"on_drgb": lambda ready: ex.push(rec, rs.campos, rs.sh_degree, ready)}
+
+
 def _cpu_snapshot(args):
     return tuple(a.detach().cpu().clone() if isinstance(a, torch.Tensor) else a for a in args)
 
@@ -353,9 +364,11 @@ class _RasterizeGaussians(torch.autograd.Function):
             kw["leaf"] = leaf
         if sink_takes_sh:
             rec = ex.record(means3D.size(0), rs.campos, rs.sh_degree)
-            # the record's exchange starts behind an event right after the colour
-            # gradient is written, under the per-Gaussian backward
-            kw["drgb_out"], kw["on_drgb"] = rec[4:], lambda ready: ex.push(rec, rs.campos, rs.sh_degree, ready)
+            # the record's exchange starts right after the colour gradient is written,
+            # under the per-Gaussian backward (an exchange that runs the colour kernel
+            # on its own stream gets it as a function: colours_apart)
+            kw["drgb_out"] = rec[4:]
+            kw.update(_drgb_hooks(ex, rec, rs))
         else:
             # a dsh that autograd receives is the [P,M,3] view of coefficient planes:
             # the reference's SH cat backward (get_features) then slices an f_dc
@@ -481,7 +494,8 @@ class _RasterizeModel(torch.autograd.Function):
         bkw = dict(inputs=inputs, leaf=leaf, l1_seed=seed)
         if sink_takes_sh:
             rec = ex.record(P, rs.campos, rs.sh_degree)
-            bkw["drgb_out"], bkw["on_drgb"] = rec[4:], lambda ready: ex.push(rec, rs.campos, rs.sh_degree, ready)
+            bkw["drgb_out"] = rec[4:]
+            bkw.update(_drgb_hooks(ex, rec, rs))
         args = (rs.bg, means3D, radii, None, scaling, rotation, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
                 rs.tanfovx, rs.tanfovy, grad_out_color, f_dc, rs.sh_degree, rs.campos, geom, ctx.num_rendered, binning,
                 img, rs.debug)

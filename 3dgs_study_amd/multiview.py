@@ -412,11 +412,18 @@ class GradAllReduce:
             st.wait_event(ready)
             return fn()
 
-    def push(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int, ready=None) -> None:
+    # the rasterizer hands over the colour kernel itself (push's `write`): with RCCL
+    # it runs on the exchange stream, beside the per-Gaussian backward
+    colours_apart = True
+
+    def push(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int, ready=None, write=None) -> None:
         """Exchange a view's record (from ``record``): the all-gather starts behind
         everything queued on the compute stream so far (the rasterizer calls this
         right after the kernels that write the colour gradient), or behind `ready`,
-        an event after which it is written."""
+        an event after which it is written.  `write` (``colours_apart``): a function
+        that queues the colour gradient's kernel on the current stream — called here
+        first, on the exchange stream when the collectives run in stream order (the
+        render backward is what the compute stream holds so far), else in line."""
         i = len(self._gathers)
         slot = self._recs[i] if i < len(self._recs) else None
         if slot is None or slot[0] is not rec:  # a record not made by record(): header now, gather behind it
@@ -441,17 +448,24 @@ class GradAllReduce:
                 else:
                     side.wait_event(ready)
                 with torch.cuda.stream(side):
+                    if write is not None:
+                        write()
                     dist.all_gather_into_tensor(out, rec, group=self.group)
                     self._gather_done = torch.cuda.Event()
                     self._gather_done.record(side)
                 work = None
             else:
+                if write is not None:
+                    write()
+                    ready = None
                 work = self._launch(ready, lambda: dist.all_gather_into_tensor(out, rec, group=self.group,
                                                                                async_op=True))
             self._gathers.append((out, world, work))
             if len(self._gathers) == self.views_per_step and rec.is_cuda:
                 self._rebuild_beside()
         else:
+            if write is not None:
+                write()
             self._gathers.append((rec, 1, None))
 
     def _rebuild_beside(self) -> None:

@@ -282,12 +282,16 @@ int gsr_backward_leaves(const gsr_inputs *in, const int32_t *radii, const void *
  * above and below are special cases of it).  phases: 1 = accumulator zeroing +
  * render backward (+ drgb, below), 2 = the per-Gaussian backward, 3 = both; a
  * caller splitting them issues 1 then 2 with the same arguments on the same
- * stream, and may start exchanging drgb in between.  drgb (instead of dsh, and
+ * stream, and may start exchanging drgb in between.  GSR_PHASE_COLOURS_APART (4)
+ * takes drgb out of the render half: 1 | 4 = the render half without it, 4 alone =
+ * drgb only (after the render half; the caller may issue it on another stream,
+ * ordered after the render half, beside the per-Gaussian half).  drgb (instead of dsh, and
  * instead of leaf dsh_dc / dsh_rest): the clamp-masked colour gradient of the
  * view-parallel SH exchange (gsr_backward_colors); leaf: as gsr_backward_leaves
  * (NULL = none) — so one backward can hand the SH gradient to the exchange and
  * write the scaling / opacity / rotation leaf gradients and dmeans3D straight into
  * the caller's all-reduce bucket (3dgs_study_amd/multiview.py). */
+#define GSR_PHASE_COLOURS_APART 4
 int gsr_backward_phase(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,
                        const void *img, int64_t num_rendered, const float *dL_dout_color, void *accum,
                        float *dmeans2D, float *dcolors, float *dopacity, float *dmeans3D, float *dcov3D, float *dsh,

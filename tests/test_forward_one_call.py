@@ -119,3 +119,38 @@ def test_default_binding_switches_to_one_call(dev):
     _C._capacity_level.pop((208, 160, 1), None)
     paths = [_run(cam, g, dev, "tight", None)["path"]["path"] for _ in range(3)]
     assert paths == ["two calls", "one call", "one call"]
+
+
+def test_backward_with_forward_chunk_masks_bit_identical(dev):
+    """render_bwd replays the forward's chunks with the forward's cull masks when the
+    forward prepared the backward (GSR_FLAG_PREPARE_BACKWARD), and
+    culls the same chunks itself when it did not: on the isolated scene (one atomic
+    per accumulator row: a deterministic backward) every gradient is the same bits."""
+    from diff_gaussian_rasterization import _C
+    from test_leaf_grads import _isolated_scene
+
+    cam, g = _isolated_scene()
+    cam, g = cam.to(dev), g.to(dev)
+    H, W = cam.image_height, cam.image_width
+    bg = torch.zeros(3, device=dev)
+    e = torch.empty(0, device=dev)
+    tx, ty = float(np.tan(cam.FoVx * 0.5)), float(np.tan(cam.FoVy * 0.5))
+    sh = g.get_features.contiguous()
+    dL = torch.from_numpy(random_dL(H, W)).to(dev) * 1e4
+    outs = []
+    for prep in (True, False):
+        fw = (bg, g.get_xyz, e, g.get_opacity, g.get_scaling, g.get_rotation, 1.0, e, cam.world_view_transform,
+              cam.full_proj_transform, tx, ty, H, W, sh, 3, cam.camera_center, False, False)
+        R, color, radii, geom, binning, img = _C.rasterize_gaussians(*fw, prepare_backward=prep)
+        bw = (bg, g.get_xyz, radii, e, g.get_scaling, g.get_rotation, 1.0, e, cam.world_view_transform,
+              cam.full_proj_transform, tx, ty, dL, sh, 3, cam.camera_center, geom, R, binning, img, False)
+        grads = _C.rasterize_gaussians_backward(*bw)
+        torch.cuda.synchronize()
+        outs.append((color.cpu(), [t.cpu() if t is not None else None for t in grads]))
+    (c0, g0), (c1, g1) = outs
+    assert torch.equal(c0, c1)
+    for i, (a, b) in enumerate(zip(g0, g1)):
+        if a is None or a.numel() == 0:
+            continue
+        assert float(a.abs().max()) > 0 or i == 1, i
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), i
