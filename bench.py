@@ -321,12 +321,16 @@ def main():
     if world > 1:
         dist.barrier()
     # Stage split (HIP events on the launch stream around every rasterizer stage,
-    # gsr_timing_*): a steady-state block of K steps after the warm-up.  Recording
-    # 14 events per step costs ~5 % of the step, so the timed region below carries
-    # events only around the dominant stage.
+    # gsr_timing_*): a steady-state block of at least SPLIT_MIN_STEPS steps after the
+    # warm-up.  Recording 14 events per step costs ~5 % of the step, so the timed
+    # region below carries events only around the dominant stage.  In a fresh
+    # process the device reaches its steady rate only after ~50 steps of this unit
+    # (tools/warmup_probe.py: 0.729 ms/step over steps 10-19, 0.691 over 30-39,
+    # 0.676 from 50 on — the clocks ramping under sustained load), so a short
+    # warm-up (the driver's --warmup 5) would time the ramp, not the kernels.
     per_stage, dom = {}, "render_bwd"
     if args.stage_events == "split":
-        per_stage, dom = stage_split(one_step, args.steps)
+        per_stage, dom = stage_split(one_step, max(args.steps, SPLIT_MIN_STEPS))
     # Timed region: K steps; events around the dominant stage give its live
     # average launch time (the roofline).
     on = {"split": [dom], "all": True, "none": False}[args.stage_events]
@@ -486,6 +490,7 @@ def main():
 
 
 DOM_EVERY = 4  # timed region: events around the dominant stage on every 4th step
+SPLIT_MIN_STEPS = 60  # the stage-split block before the timed region: past the device's ramp
 
 STAGES_SOURCE = {
     "split": "HIP events around every rasterizer stage over a steady-state block of the same K steps right before "
