@@ -148,6 +148,7 @@ class GradAllReduce:
         self._reduced = [p for p in self.params if self._sh is None or not any(p is q for q in self._sh[1:])]
         self._index = {id(p): i for i, p in enumerate(self._reduced)}  # (strong refs: ids are unique)
         self._bucket = self._views = None
+        self._bucket_cache = None
         # hooks only while there is something to exchange: with one rank the leaves
         # carry none, and the rasterizer's fused leaf gradients apply as without us
         if self.overlap and self._active():
@@ -186,6 +187,14 @@ class GradAllReduce:
 
     # ---- the bucket
     def _ensure_bucket(self):
+        if self._bucket is None and self._bucket_cache is not None:
+            # last step's bucket again when the caller let go of its views (.grad set
+            # to None, or still the view itself: zero_grad(set_to_none=False)) — as
+            # DDP's gradient_as_bucket_view; its allocation and views cost the step's
+            # critical host path ~15 us
+            b, vs = self._bucket_cache
+            if all(p.grad is None or self._is_view(p.grad, v) for p, v in zip(self._reduced, vs)):
+                self._bucket, self._views = b, vs
         if self._bucket is None:
             ref = self._reduced[0]
             self._bucket = torch.empty(sum(p.numel() for p in self._reduced), dtype=torch.float32, device=ref.device)
@@ -286,6 +295,38 @@ class GradAllReduce:
             self._nccl = dist.get_backend(self.group) == "nccl"
         return self._nccl
 
+    def _pg(self):
+        g = getattr(self, "_pg_obj", None)
+        if g is None:
+            g = self._pg_obj = self.group or dist.distributed_c10d._get_default_group()
+        return g
+
+    def _gather_now(self, out: torch.Tensor, rec: torch.Tensor) -> None:
+        """all_gather_into_tensor as a non-async op on the current stream, straight
+        through the process group (torch's Python wrapper costs ~15 us of host time
+        per call, on the step's critical host path in this exchange)."""
+        try:
+            opts = dist.distributed_c10d.AllgatherOptions()
+            opts.asyncOp = False
+            work = self._pg()._allgather_base(out, rec, opts)
+        except (AttributeError, TypeError):  # another torch: the public call
+            dist.all_gather_into_tensor(out, rec, group=self.group)
+            return
+        if work is not None:
+            work.wait()
+
+    def _all_reduce_now(self, t: torch.Tensor) -> None:
+        try:
+            opts = dist.distributed_c10d.AllreduceOptions()
+            opts.reduceOp = dist.ReduceOp.SUM
+            opts.asyncOp = False
+            work = self._pg().allreduce([t], opts)
+        except (AttributeError, TypeError):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            return
+        if work is not None:
+            work.wait()
+
     def _reduce(self, bucket: torch.Tensor):
         """The bucket's all-reduce, started now (behind everything queued on the
         compute stream).  In stream order it runs on the compute stream itself,
@@ -294,7 +335,7 @@ class GradAllReduce:
         if self._in_stream(bucket):
             if self._gather_done is not None:
                 torch.cuda.current_stream(bucket.device).wait_event(self._gather_done)
-            dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group)
+            self._all_reduce_now(bucket)
             return _QUEUED
         return dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
@@ -447,13 +488,20 @@ class GradAllReduce:
                     side.wait_stream(torch.cuda.current_stream(rec.device))
                 else:
                     side.wait_event(ready)
+                last = len(self._gathers) + 1 == self.views_per_step
+                if last:  # the rebuild's outputs from the compute stream's pool (see _rebuild_beside)
+                    _, f_dc, f_rest = self._sh
+                    dc, rest = torch.empty_like(f_dc), torch.empty_like(f_rest)
                 with torch.cuda.stream(side):
                     if write is not None:
                         write()
-                    dist.all_gather_into_tensor(out, rec, group=self.group)
+                    self._gather_now(out, rec)
                     self._gather_done = torch.cuda.Event()
                     self._gather_done.record(side)
-                work = None
+                    self._gathers.append((out, world, None))
+                    if last:
+                        self._rebuild_on_side(side, dc, rest)
+                return
             else:
                 if write is not None:
                     write()
@@ -467,6 +515,18 @@ class GradAllReduce:
             if write is not None:
                 write()
             self._gathers.append((rec, 1, None))
+
+    def _rebuild_on_side(self, side, dc: torch.Tensor, rest: torch.Tensor) -> None:
+        """The SH rebuild on the exchange stream (current), right behind the gathers:
+        _rebuild_beside's work inside push's stream block."""
+        self._begin("sh_rebuild")
+        self._rebuild_into(dc, rest)
+        self._end("sh_rebuild")
+        done = torch.cuda.Event()
+        done.record(side)
+        dc.record_stream(side)
+        rest.record_stream(side)
+        self._sh_out = (dc, rest, done)
 
     def _rebuild_beside(self) -> None:
         """The step's last record is out: the SH rebuild goes on the exchange's own
@@ -640,7 +700,9 @@ class GradAllReduce:
         self._gather_done = None
         self._extra = None
         self._work = None
-        self._bucket = self._views = None  # the grads keep the storage; next step gets a fresh bucket
+        # the grads keep the storage; the next step reuses it only if they were let go
+        self._bucket_cache = (self._bucket, self._views) if self._views is not None else None
+        self._bucket = self._views = None
         self._backwards = 0
         self.launched_in_backward = False
         return bucket
