@@ -995,3 +995,54 @@ def test_late_gradient_path_after_early_start_gloo_world2(views_per_step):
         assert torch.equal(a, b)
     torch.testing.assert_close(g0[0], 2 * wsum * p[0], rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(g0[1], (2 * wsum + creg) * p[1], rtol=1e-6, atol=1e-6)
+
+
+def _reuse_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    xyz, opacity = (torch.randn(s, requires_grad=True) for s in ((7, 3), (7, 1)))
+    ar = GradAllReduce([xyz, opacity])
+    res = []
+    for step in range(3):
+        _AllWriter.apply(xyz, opacity, float(rank + 1) * (step + 1)).backward()
+        bucket = ar()
+        res.append((bucket.data_ptr(), [p.grad.clone() for p in (xyz, opacity)]))
+        if step == 0:
+            for p in (xyz, opacity):
+                p.grad = None               # released: step 1 reuses the bucket
+        elif step == 1:
+            for p in (xyz, opacity):
+                p.grad.zero_()              # still the views (zero_grad(set_to_none=False)): reused
+    # a tensor of the caller's own in one leaf: the next bucket is a fresh one
+    xyz.grad = xyz.grad.clone()
+    opacity.grad = None
+    ar.leaf_bucket({"opacity": (opacity,)})
+    fresh = ar._bucket.data_ptr()
+    ar()
+    out[rank] = (res, [p.detach().clone() for p in (xyz, opacity)], fresh)
+    ar.remove_hooks()
+    dist.destroy_process_group()
+
+
+def test_bucket_reused_only_when_released_gloo_world2():
+    """The all-reduce bucket is reused step to step when every reduced leaf's .grad
+    was set to None or is still its bucket view (as DDP's gradient_as_bucket_view),
+    and not when the caller installed a tensor of its own; the reduced gradients are
+    the ranks' sums either way (a kept view accumulates, as autograd would)."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_reuse_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    (r0, prm, fresh), (r1, _, _) = res[0], res[1]
+    b = [x[0] for x in r0]
+    assert b[1] == b[0] and b[2] == b[0] and fresh != b[0], (b, fresh)
+    for step in range(3):
+        for a, c in zip(r0[step][1], r1[step][1]):
+            assert torch.equal(a, c)
+    for step in (0, 1, 2):
+        wsum = sum(float(r + 1) * (step + 1) for r in (0, 1))
+        for g, x in zip(r0[step][1], prm):
+            torch.testing.assert_close(g, 2 * wsum * x, rtol=1e-6, atol=1e-6)
