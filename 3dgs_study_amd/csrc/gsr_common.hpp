@@ -44,7 +44,10 @@ constexpr int TSORT_ITEMS = GSR_TSORT_ITEMS;
 // contiguous per-digit output runs and half the blocks for the digit scan
 // (tile sort 875 -> 730 us at E); short ones (config C: 4.9M) keep more
 // workgroups in flight (8 items: 85 us vs 91 us with 16).
-constexpr int TSORT_ITEMS_BIG = 16;
+#ifndef GSR_TSORT_ITEMS_BIG
+#define GSR_TSORT_ITEMS_BIG 16
+#endif
+constexpr int TSORT_ITEMS_BIG = GSR_TSORT_ITEMS_BIG;
 constexpr int64_t TSORT_BIG_N = 16 << 20;
 __host__ __device__ inline int tsort_items(int64_t n) { return n > TSORT_BIG_N ? TSORT_ITEMS_BIG : TSORT_ITEMS; }
 #ifndef GSR_EMIT_BLOCK

@@ -314,3 +314,17 @@ def test_bench_measured_roofline_helpers():
         b = rec["hbm_bytes_per_unit"]
         assert b > 0 and rec["units"] > 0
         assert bench.measured_frac(key, 1000.0) == round(b * 1000.0 / 1e9 / bench.HBM_PEAK_GBS, 4)
+
+
+def test_backward_phase_validates(lib):
+    """gsr_backward_phase: phases 1 .. 7 (GSR_PHASE_COLOURS_APART = 4: the colour
+    gradient in a call of its own); anything else is refused before any work."""
+    from diff_gaussian_rasterization import _C
+
+    assert _C.PHASE_COLOURS_APART == 4
+    s = _inputs(P=0)
+    for bad in (0, 8, -1):
+        rc = lib.gsr_backward_phase(ctypes.byref(s), None, None, None, None, 0, *([None] * 12), bad, None)
+        assert rc != 0 and "phases must be 1 .. 7" in lib.gsr_last_error().decode(), bad
+    for ok in (1, 2, 3, 4, 5, 6, 7):  # P = 0: accepted, nothing to do
+        assert lib.gsr_backward_phase(ctypes.byref(s), None, None, None, None, 0, *([None] * 12), ok, None) == 0, ok
