@@ -70,6 +70,25 @@ int64_t qmask_get(const void *binning) {
     const auto it = g_qmask.find(binning);
     return it == g_qmask.end() ? 0 : it->second;
 }
+// img buffers whose last forward wrote sign(image - gt) beside the L1 loss's partial
+// sums (gsr_forward_render_l1 with GSR_FLAG_PREPARE_BACKWARD), with the image and
+// target it compared: an L1-seeded backward of that pair reads the signs (3 B per
+// pixel) instead of both images (24 B).
+std::unordered_map<const void *, std::pair<const float *, const float *>> g_l1sign;
+void l1sign_set(const void *img, const float *image, const float *gt) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    if (!image) {
+        g_l1sign.erase(img);
+        return;
+    }
+    if (g_l1sign.size() > 4096) g_l1sign.clear();
+    g_l1sign[img] = {image, gt};
+}
+bool l1sign_has(const void *img, const float *image, const float *gt) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    const auto it = g_l1sign.find(img);
+    return it != g_l1sign.end() && it->second.first == image && it->second.second == gt;
+}
 // the num_rendered read-back's event (per host thread, like g_pinned): timing off
 // and no system-scope fence — the pinned words are written with system-scope stores
 // already, and a fenced event's cache writeback / invalidate opened a ~6 us idle gap
@@ -365,6 +384,7 @@ static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t
                       "render", dbg, s))
         return rc;
     if (binning) qmask_set(binning, prep && n > 0 ? cap : 0);
+    l1sign_set(img, prep && gt ? out_color : nullptr, gt);
     if (!prep) {  // the L1 loss, if asked for, on its own
         prepared_set(geom, false);
         return gt ? step(launch_l1_finish(out_color, gt, npix, l1_part, 0, true, loss_out, s), "l1 loss", dbg, s)
@@ -508,7 +528,8 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
         if (num_rendered > 0) {
             if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] {
                                   return launch_render_bwd(*in, geom, binning, img, seed ? nullptr : dL_dout_color,
-                                                           seed, acc, s, qmask_get(binning));
+                                                           seed, acc, s, qmask_get(binning),
+                                                           seed && l1sign_has(img, seed->image, seed->gt));
                               }),
                               "render backward", dbg, s))
                 return rc;

@@ -258,6 +258,7 @@ struct ImgLayout {
     size_t qbucket; // uint8 [4 * tiles] each quadrant's forward work bucket (render_fwd.hip)
     size_t l1_part; // float [L1_BLOCKS][2] the L1 loss's partial sums (gsr_forward_render_l1, gsr_l1.hpp)
     size_t l1_ticket; // uint32 [L1_TICKETS] the partial-sum blocks' finish tickets (zeroed by render_fwd_kernel)
+    size_t l1_sign; // int8 [3][H][W] sign(image - gt), written beside the partial sums for the L1-seeded backward
     size_t bytes;
 };
 __host__ __device__ inline ImgLayout img_layout(int W, int H) {
@@ -272,6 +273,7 @@ __host__ __device__ inline ImgLayout img_layout(int W, int H) {
     L.qbucket = take((size_t)g.tiles * 4);
     L.l1_part = take((size_t)1024 * 2 * 4);
     L.l1_ticket = take(9 * 128);  // gsr_l1.hpp: L1_TICKETS words, 128 B apart
+    L.l1_sign = take((size_t)3 * W * H);
     L.bytes = o;
     return L;
 }

@@ -51,7 +51,7 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
 // capacity (launch_render_fwd); the replay then skips the cull
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, const void *img,
                              const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s,
-                             int64_t qmask_cap = 0);
+                             int64_t qmask_cap = 0, bool l1_signs = false);
 
 // preprocess_bwd.hip
 struct BwdOutputs {

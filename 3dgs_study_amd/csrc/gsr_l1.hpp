@@ -23,8 +23,12 @@ __host__ __device__ inline int l1_blocks(size_t n) {
 // into partials[2 blk] (and 0 into partials[2 blk + 1], the SSIM slot).
 // write_through: the two words leave as agent-scope (sc1) stores, for a consumer in
 // the same launch (l1_finish_last_block).
+__device__ __forceinline__ float l1_sign_of(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }  // torch.sign
+// sign (or NULL): sign(x - y) per element as an int8 (the L1 loss's pixel gradient
+// up to its scale, for the seeded backward: 1 B instead of the 8 B of both inputs)
 __device__ __forceinline__ void l1_block_partial(const float *x, const float *y, size_t n, int blk, int nblk,
-                                                 float *partials, bool write_through = false) {
+                                                 float *partials, bool write_through = false,
+                                                 int8_t *sign = nullptr) {
     __shared__ float wsum[L1_THREADS / 64];
     const size_t n4 = n >> 2, stride = (size_t)nblk * L1_THREADS;
     const float4 *x4 = reinterpret_cast<const float4 *>(x), *y4 = reinterpret_cast<const float4 *>(y);
@@ -32,9 +36,19 @@ __device__ __forceinline__ void l1_block_partial(const float *x, const float *y,
     for (size_t i = (size_t)blk * L1_THREADS + threadIdx.x; i < n4; i += stride) {
         const float4 a = x4[i], b = y4[i];
         acc += (fabsf(a.x - b.x) + fabsf(a.y - b.y)) + (fabsf(a.z - b.z) + fabsf(a.w - b.w));
+        if (sign) {
+            const uint32_t s = (uint32_t)(uint8_t)(int8_t)l1_sign_of(a.x - b.x) |
+                               (uint32_t)(uint8_t)(int8_t)l1_sign_of(a.y - b.y) << 8 |
+                               (uint32_t)(uint8_t)(int8_t)l1_sign_of(a.z - b.z) << 16 |
+                               (uint32_t)(uint8_t)(int8_t)l1_sign_of(a.w - b.w) << 24;
+            reinterpret_cast<uint32_t *>(sign)[i] = s;
+        }
     }
     if (blk == 0)
-        for (size_t i = (n4 << 2) + threadIdx.x; i < n; i += L1_THREADS) acc += fabsf(x[i] - y[i]);
+        for (size_t i = (n4 << 2) + threadIdx.x; i < n; i += L1_THREADS) {
+            acc += fabsf(x[i] - y[i]);
+            if (sign) sign[i] = (int8_t)l1_sign_of(x[i] - y[i]);
+        }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;

@@ -54,6 +54,7 @@ struct RenderBwdArgs {
     const float *dL_dpix;       // [3][H][W], or NULL: the L1 loss's gradient from l1_* (GSR_FLAG_L1_SEED)
     const float *l1_image, *l1_gt, *l1_dloss;
     float l1_n;
+    const int8_t *l1_signmap;  // the forward's sign(image - gt) (gsr_l1.hpp), or NULL: formed here from both
     float *accum;
     // the forward's chunk cull masks (render_fwd.hip; binning's qmask region), or NULL
     const uint64_t *qmask;
@@ -126,9 +127,15 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             dpx2 = a.dL_dpix[2 * HW + pix];
         } else {  // L1 seed: gsr_l1_grad's (dloss / n) * sign(image - gt), the same operations
             const float q = a.l1_dloss[0] / a.l1_n;
-            dpx0 = q * l1_sign(a.l1_image[pix] - a.l1_gt[pix]);
-            dpx1 = q * l1_sign(a.l1_image[HW + pix] - a.l1_gt[HW + pix]);
-            dpx2 = q * l1_sign(a.l1_image[2 * HW + pix] - a.l1_gt[2 * HW + pix]);
+            if (a.l1_signmap) {  // 3 B per pixel instead of 24 (the same signs: l1_sign_of)
+                dpx0 = q * (float)a.l1_signmap[pix];
+                dpx1 = q * (float)a.l1_signmap[HW + pix];
+                dpx2 = q * (float)a.l1_signmap[2 * HW + pix];
+            } else {
+                dpx0 = q * l1_sign(a.l1_image[pix] - a.l1_gt[pix]);
+                dpx1 = q * l1_sign(a.l1_image[HW + pix] - a.l1_gt[HW + pix]);
+                dpx2 = q * l1_sign(a.l1_image[2 * HW + pix] - a.l1_gt[2 * HW + pix]);
+            }
         }
     }
     const float bg_dot = a.bg[0] * dpx0 + a.bg[1] * dpx1 + a.bg[2] * dpx2;
@@ -421,6 +428,7 @@ struct BwdPrepArgs {
     uint32_t *l1_ticket;
     float l1_invN;
     float *l1_out;
+    int8_t *l1_sign;  // ... and the signs of image - gt for the seeded backward (img's l1_sign)
     // ... and workgroups after those write visible[i] = radii[i] > 0 (render()'s
     // visibility_filter), or NULL
     const int32_t *radii;
@@ -438,7 +446,8 @@ __global__ void __launch_bounds__(PREP_THREADS) bwd_prepare_kernel(BwdPrepArgs a
         return;
     }
     if ((int)blockIdx.x >= a.file_blocks) {  // workgroup-uniform: an L1 partial-sum block
-        l1_block_partial(a.l1_x, a.l1_y, a.l1_n, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_part, true);
+        l1_block_partial(a.l1_x, a.l1_y, a.l1_n, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_part, true,
+                         a.l1_sign);
         l1_finish_last_block(a.l1_part, (int)blockIdx.x - a.file_blocks, a.l1_nb, a.l1_ticket, a.l1_invN, a.l1_out);
         return;
     }
@@ -507,6 +516,7 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
     a.l1_ticket = at<uint32_t>(const_cast<void *>(img), Im.l1_ticket);
     a.l1_invN = 1.0f / (float)(double)a.l1_n;  // launch_l1_finish's invN
     a.l1_out = l1_out;
+    a.l1_sign = l1_x ? at<int8_t>(const_cast<void *>(img), Im.l1_sign) : nullptr;
     a.radii = radii;
     a.visible = visible;
     a.P = in.P;
@@ -517,7 +527,7 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
 
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, const void *img,
                              const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s,
-                             int64_t qmask_cap) {
+                             int64_t qmask_cap, bool l1_signs) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -537,6 +547,7 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.l1_gt = l1 ? l1->gt : nullptr;
     a.l1_dloss = l1 ? l1->dloss : nullptr;
     a.l1_n = l1 ? (float)(double)l1->n : 0.f;  // gsr_l1_grad's fN
+    a.l1_signmap = l1 && l1_signs ? at<int8_t>(img, Im.l1_sign) : nullptr;
     a.accum = accum;
     a.order_cnt = at<uint32_t>(geom, G.order_cnt);
     a.flags = at<uint32_t>(const_cast<void *>(geom), G.order_cnt) + ORDER_FILED;
