@@ -422,7 +422,16 @@ class GradAllReduce:
             self._recs.append(None)
         slot = self._recs[i]
         if slot is None or slot[0].numel() != n or slot[0].device != dev:
-            slot = self._recs[i] = [torch.empty(n, dtype=torch.float32, device=dev), None]
+            if dev.type == "cuda" and self._active() and dist.get_backend(self.group) == "nccl":
+                # RCCL: the record is this rank's slice of the all-gather's output, so
+                # the gather runs in place (no local copy; at one rank no kernel at all)
+                world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
+                while len(self._gouts) <= i:
+                    self._gouts.append(None)
+                out = self._gouts[i] = torch.empty(world * n, dtype=torch.float32, device=dev)
+                slot = self._recs[i] = [out.narrow(0, rank * n, n), None]
+            else:
+                slot = self._recs[i] = [torch.empty(n, dtype=torch.float32, device=dev), None]
         return slot
 
     def record(self, P: int, campos: torch.Tensor = None, sh_degree: int = None) -> torch.Tensor:
@@ -468,6 +477,8 @@ class GradAllReduce:
         i = len(self._gathers)
         slot = self._recs[i] if i < len(self._recs) else None
         if slot is None or slot[0] is not rec:  # a record not made by record(): header now, gather behind it
+            if slot is not None:
+                slot[1] = None  # the gather may overwrite the slot's record (in place: a slice of its output)
             slot = [rec, None]
             ready = None
         if slot[1] is None:

@@ -154,3 +154,4 @@ def test_backward_with_forward_chunk_masks_bit_identical(dev):
             continue
         assert float(a.abs().max()) > 0 or i == 1, i
         assert torch.equal(a.view(torch.int32), b.view(torch.int32)), i
+
