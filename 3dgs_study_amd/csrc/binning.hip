@@ -903,10 +903,9 @@ __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) 
 
 // ------------------------------------------------------------ launchers
 // The depth sort: depth_keys_kernel, then passes 1-3; the fourth pass is launched
-// by the host after its sync when the published pass count needs it (in line), or
-// queued with kernels that return at once unless the key range needs it (on the
-// opt-in second stream, GSR_SIDE_STREAM=1).  The order lands in
-// GSR_GEOM_DEPTH_ORDER either way.
+// by the host after its sync when the published pass count needs it, or queued up
+// front (the last forward needed four) as a kernel that returns at once unless the
+// key range needs it.  The order lands in GSR_GEOM_DEPTH_ORDER either way.
 static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     const GeomLayout L = geom_layout(P, W, H);
     RadixPass a = {};
