@@ -32,13 +32,28 @@ struct PreBwdArgs {
 // by the forward, or computed here from the SH row): dsh (b[k] * dRGB[c] for the
 // active coefficients, zeros for the rest of the M) and the direction term of
 // dL/dmean3D.  `dsh` may be the row the Jacobian was computed from.
+// the direction term of dL/dmean3D from d colour / d direction (auxiliary.h dnormvdv)
+__device__ __forceinline__ void sh_dir_term(const float J[9], float ox, float oy, float oz, const float dRGB[3],
+                                            f3 &dmean) {
+    const float ddx = (J[0] * dRGB[0] + J[1] * dRGB[1]) + J[2] * dRGB[2];
+    const float ddy = (J[3] * dRGB[0] + J[4] * dRGB[1]) + J[5] * dRGB[2];
+    const float ddz = (J[6] * dRGB[0] + J[7] * dRGB[1]) + J[8] * dRGB[2];
+    const float sum2 = ox * ox + oy * oy + oz * oz;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    dmean.x += ((+sum2 - ox * ox) * ddx - oy * ox * ddy - oz * ox * ddz) * invsum32;
+    dmean.y += (-ox * oy * ddx + (sum2 - oy * oy) * ddy - oz * oy * ddz) * invsum32;
+    dmean.z += (-ox * oz * ddx - oy * oz * ddy + (sum2 - oz * oz) * ddz) * invsum32;
+}
+// the basis of the view direction o / |o| (sh_basis: the products dsh = b[k] * dRGB[c])
+__device__ __forceinline__ void sh_dir_basis(int deg, float ox, float oy, float oz, float b[16]) {
+    const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
+    sh_basis(deg, ox / len, oy / len, oz / len, b);
+}
 __device__ __forceinline__ void sh_backward_j(const float J[9], float *dsh, int deg, int M, float ox, float oy,
                                               float oz, const float dRGB[3], f3 &dmean) {
-    const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
-    const float x = ox / len, y = oy / len, z = oz / len;
     const int ncoef = (deg + 1) * (deg + 1);
     float b[16];
-    sh_basis(deg, x, y, z, b);
+    sh_dir_basis(deg, ox, oy, oz, b);
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         const float d = dRGB[c];
@@ -50,15 +65,7 @@ __device__ __forceinline__ void sh_backward_j(const float J[9], float *dsh, int 
     for (int k = 0; k < 16; k++)
         if (k >= ncoef && k < M) dsh[3 * k + 0] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
     for (int k = max(ncoef, 16); k < M; k++) dsh[3 * k + 0] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
-    const float ddx = (J[0] * dRGB[0] + J[1] * dRGB[1]) + J[2] * dRGB[2];
-    const float ddy = (J[3] * dRGB[0] + J[4] * dRGB[1]) + J[5] * dRGB[2];
-    const float ddz = (J[6] * dRGB[0] + J[7] * dRGB[1]) + J[8] * dRGB[2];
-    // auxiliary.h dnormvdv
-    const float sum2 = ox * ox + oy * oy + oz * oz;
-    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-    dmean.x += ((+sum2 - ox * ox) * ddx - oy * ox * ddy - oz * ox * ddz) * invsum32;
-    dmean.y += (-ox * oy * ddx + (sum2 - oy * oy) * ddy - oz * oy * ddz) * invsum32;
-    dmean.z += (-ox * oz * ddx - oy * oz * ddy + (sum2 - oz * oz) * ddz) * invsum32;
+    sh_dir_term(J, ox, oy, oz, dRGB, dmean);
 }
 // The same from the SH row itself (no stored Jacobian): every coefficient is read
 // (into J) before any gradient is written, so `sh` and `dsh` may alias.
@@ -124,6 +131,61 @@ __device__ __forceinline__ void leaf_sh_store_direct(const gsr_leaf_grads &L, in
     }
 }
 
+// The same leaves from each Gaussian's basis and colour gradient instead of its
+// 48-float dsh row (preprocess_bwd_kernel<48, *, true>): leaf_sh_store_direct's
+// half-wave LDS image and coalesced 16-B stores, with each lane's 45 rest floats
+// formed as b[k] * dRGB[c] — the products sh_backward_j forms, so the same bits —
+// as they go into LDS, so no row is held in registers (77 instead of 125 VGPRs: 6
+// waves per SIMD, not 4).  Every thread of the workgroup calls it (barriers).
+__device__ __forceinline__ void leaf_sh_store_basis(const gsr_leaf_grads &L, int P, int idx, bool live, bool vis,
+                                                    int ncoef, const float b[16], const float dRGB[3]) {
+    __shared__ __attribute__((aligned(16))) float stage[PB_THREADS / 64][32 * 45];
+    const bool add = (L.accumulate & 1) != 0;
+    auto coef = [&](int k, int c) { return vis && k < ncoef ? b[k] * dRGB[c] : 0.f; };
+    if (live)
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            float *p = L.dsh_dc + 3 * (size_t)idx + c;
+            *p = add ? *p + coef(0, c) : coef(0, c);
+        }
+    const int lane = threadIdx.x & 63;
+    float *buf = stage[threadIdx.x >> 6];
+    const size_t wave_g0 = (size_t)blockIdx.x * PB_THREADS + (threadIdx.x & ~63u);
+    const size_t limit = (size_t)45 * P;  // floats in dsh_rest
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        if ((lane >> 5) == h)
+#pragma unroll
+            for (int k = 1; k < 16; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) buf[(lane & 31) * 45 + 3 * (k - 1) + c] = coef(k, c);
+        __syncthreads();
+        const size_t f0 = (wave_g0 + 32 * h) * 45;  // the half's first float in dsh_rest
+#pragma unroll
+        for (int m = 0; m < 6; m++) {
+            const int i = lane + 64 * m;  // float4 of the half's 32 x 45 floats
+            if (i < 360) {
+                const size_t f = f0 + 4 * (size_t)i;
+                const float4 v = *reinterpret_cast<const float4 *>(buf + 4 * i);
+                if (f + 4 <= limit) {
+                    float4 *d = reinterpret_cast<float4 *>(L.dsh_rest + f);
+                    if (add) {
+                        const float4 o = *d;
+                        *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+                    } else {
+                        *d = v;
+                    }
+                } else {
+                    const float vv[4] = {v.x, v.y, v.z, v.w};
+                    for (int c = 0; c < 4; c++)
+                        if (f + c < limit) L.dsh_rest[f + c] = add ? L.dsh_rest[f + c] + vv[c] : vv[c];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // What the SH stage (after the rows reach LDS) needs from the geometry stage.
 struct ShStage {
     f3 dmean;      // dL/dmean3D so far
@@ -144,7 +206,10 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
 // C); forcing 5 or 6 spilled (160 us).  Other degrees stage the workgroup's rows
 // through LDS and stream them back out coalesced.
 // SPLIT: the SH rows come from GaussianModel's two leaves (gsr_inputs.sh_rest).
-template <int RWC, bool SPLIT>
+// LB (degree-3 rows, no dsh output: the leaves, or the exchange's colour gradient
+// only): no 48-float row in registers — the Jacobian from the forward's planes (or
+// from the row, loaded only to form it), the leaves through leaf_sh_store_basis.
+template <int RWC, bool SPLIT, bool LB = false>
 __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PB_THREADS][3M + 1]
     const gsr_inputs &in = a.in;
@@ -190,8 +255,9 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
     const float opac_in = in.opacities ? in.opacities[li] : a.splat_f[12 * (size_t)li + 5];
     const int32_t rad = a.radii[li];
     const uint32_t cl = a.clamped[li];
-    float rowv[DIRECT ? 48 : 1];
-    auto load_row = [&]() {  // launched only with staged (stage == true) SH rows: 16-B aligned cat rows, or split
+    static_assert(!LB || RWC == 48, "the basis-staged leaves are built for degree-3 rows");
+    float rowv[DIRECT && !LB ? 48 : 1];
+    auto load_row = [&](float *rowv) {  // launched only with staged (stage == true) SH rows: 16-B aligned cat rows, or split
         if constexpr (SPLIT) {
             load_sh_row_split(in.sh, in.sh_rest, (size_t)li, rowv);
         } else {
@@ -237,13 +303,28 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
         if (live && st.vis)
 #pragma unroll
             for (int k = 0; k < 9; k++) J[k] = a.shjac[(size_t)k * in.P + li];
+    } else if constexpr (LB) {  // the row only to form J (its registers end here)
+        if (live && st.vis) {
+            float r[48];
+            load_row(r);
+            const float ox = mean.x - in.campos[0], oy = mean.y - in.campos[1], oz = mean.z - in.campos[2];
+            const float len = sqrtf((ox * ox + oy * oy) + oz * oz);
+            sh_dir_jacobian(r, in.D, ox / len, oy / len, oz / len, J);
+        }
     } else if constexpr (DIRECT) {  // after the geometry (its registers are not held through it); culled: zeros
-        if (live && st.vis) load_row();
+        if (live && st.vis) load_row(rowv);
     }
     if (stage && !DIRECT) __syncthreads();
+    float b[LB ? 16 : 1];
     if (live) {
         f3 dmean = st.dmean;
-        if (stage) {
+        if constexpr (LB) {
+            if (stage && st.vis) {
+                const float ox = mean.x - in.campos[0], oy = mean.y - in.campos[1], oz = mean.z - in.campos[2];
+                if (a.o.leaf.dsh_dc) sh_dir_basis(in.D, ox, oy, oz, b);
+                sh_dir_term(J, ox, oy, oz, st.dRGB, dmean);
+            }
+        } else if (stage) {
             float *row = DIRECT ? rowv : sh_lds + threadIdx.x * (RW + 1);
             const float ox = mean.x - in.campos[0], oy = mean.y - in.campos[1], oz = mean.z - in.campos[2];
             if (!st.vis)
@@ -264,7 +345,11 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
             dm[2] = dmean.z;
         }
     }
-    if constexpr (DIRECT) {
+    if constexpr (LB) {
+        if (a.o.leaf.dsh_dc)
+            leaf_sh_store_basis(a.o.leaf, in.P, idx, live, live && st.vis, (in.D + 1) * (in.D + 1), b, st.dRGB);
+        return;
+    } else if constexpr (DIRECT) {
         if (live && a.o.dsh) {
             if (a.o.dsh_planar) {
 #pragma unroll
@@ -580,6 +665,8 @@ hipError_t launch_preprocess_bwd(const gsr_inputs &in, const int32_t *radii, con
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(PB_THREADS), lds, s, a); };
     if (3 * in.M == 3)  // (M = 1 has no rest coefficients: never split)
         go(preprocess_bwd_kernel<3, false>);
+    else if (3 * in.M == 48 && direct && !o.dsh)  // the leaves or the colour gradient: no dsh row
+        split ? go(preprocess_bwd_kernel<48, true, true>) : go(preprocess_bwd_kernel<48, false, true>);
     else if (3 * in.M == 48 && direct)
         split ? go(preprocess_bwd_kernel<48, true>) : go(preprocess_bwd_kernel<48, false>);
     else
