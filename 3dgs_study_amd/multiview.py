@@ -465,6 +465,9 @@ class GradAllReduce:
     # the rasterizer hands over the colour kernel itself (push's `write`): with RCCL
     # it runs on the exchange stream, beside the per-Gaussian backward
     colours_apart = True
+    # the SH rebuild on the exchange stream right behind the gather (beside
+    # preprocess_bwd), or (False) on the compute stream after preprocess_bwd
+    rebuild_on_side = True
 
     def push(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int, ready=None, write=None) -> None:
         """Exchange a view's record (from ``record``): the all-gather starts behind
@@ -499,7 +502,7 @@ class GradAllReduce:
                     side.wait_stream(torch.cuda.current_stream(rec.device))
                 else:
                     side.wait_event(ready)
-                last = len(self._gathers) + 1 == self.views_per_step
+                last = len(self._gathers) + 1 == self.views_per_step and self.rebuild_on_side
                 if last:  # the rebuild's outputs from the compute stream's pool (see _rebuild_beside)
                     _, f_dc, f_rest = self._sh
                     dc, rest = torch.empty_like(f_dc), torch.empty_like(f_rest)

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--only", default="plain,local,rccl", help="comma-separated variants to run")
     ap.add_argument("--no-wrap", action="store_true", help="do not time the forward's host sync")
     ap.add_argument("--glue", default="fused", choices=["fused", "reference"])
+    ap.add_argument("--rebuild-on-side", type=int, default=None, choices=[0, 1],
+                    help="override GradAllReduce.rebuild_on_side (the SH rebuild on the exchange stream)")
     ap.add_argument("--colours-apart", type=int, default=None, choices=[0, 1],
                     help="override GradAllReduce.colours_apart (the colour kernel on the exchange stream)")
     ap.add_argument("--host", action="store_true", help="host-side time of the exchange's calls (perf_counter)")
@@ -100,6 +102,8 @@ def main():
         wrap(torch.Tensor, "backward", "loss.backward")
     if args.colours_apart is not None:
         GradAllReduce.colours_apart = bool(args.colours_apart)
+    if args.rebuild_on_side is not None:
+        GradAllReduce.rebuild_on_side = bool(args.rebuild_on_side)
     res = {}
     for rnd in range(args.rounds):
         for name in args.only.split(","):
