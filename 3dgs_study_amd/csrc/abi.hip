@@ -7,6 +7,7 @@
 // here: every buffer belongs to the caller (torch's caching allocator on the
 // Python side).  The only host synchronisation is the num_rendered read-back
 // in gsr_forward_preprocess, as upstream.
+#include <atomic>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -88,6 +89,23 @@ bool l1sign_has(const void *img, const float *image, const float *gt) {
     std::lock_guard<std::mutex> lk(g_prep_mu);
     const auto it = g_l1sign.find(img);
     return it != g_l1sign.end() && it->second.first == image && it->second.second == gt;
+}
+// Binning form (gsr_binning_mode): 0 = the row-span binning (rowspan.hip) wherever
+// the tile grid allows it (at most 256 x 256 tiles), 1 = the LSD tile sort of
+// binning.hip everywhere.  The form of each geom buffer's last preprocess is
+// recorded, so its render uses the rank gather's matching outputs.
+std::atomic<int> g_binning_mode{0};
+std::unordered_map<const void *, bool> g_rowspan;
+bool rowspan_wanted(const gsr_inputs *in) { return g_binning_mode.load() == 0 && rowspan_grid(in->W, in->H); }
+void rowspan_set(const void *geom, bool on) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    if (g_rowspan.size() > 4096) g_rowspan.clear();
+    g_rowspan[geom] = on;
+}
+bool rowspan_get(const void *geom, const gsr_inputs *in) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    const auto it = g_rowspan.find(geom);
+    return it == g_rowspan.end() ? rowspan_wanted(in) : it->second;
 }
 // the num_rendered read-back's event (per host thread, like g_pinned): timing off
 // and no system-scope fence — the pinned words are written with system-scope stores
@@ -253,6 +271,14 @@ int gsr_point_list_keys(int32_t P, int32_t W, int32_t H, const void *geom, const
                      "point_list_keys");
 }
 
+int gsr_binning_mode(int mode) {
+    if (mode < -1 || mode > 1) {
+        fail(GSR_ERR_ARGS, "binning mode %d: 0 (row spans where possible), 1 (LSD tile sort) or -1 (query)", mode);
+        return -1;
+    }
+    return mode < 0 ? g_binning_mode.load() : g_binning_mode.exchange(mode);
+}
+
 const char *gsr_last_error(void) { return g_err.c_str(); }
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 
@@ -275,6 +301,8 @@ static int ensure_pinned() {
 // queued, not waited for.  passes: the depth passes queued (3, or 4 up front).
 static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int passes, hipStream_t s, bool dbg) {
     prepared_set(geom, false);  // preprocess resets the device's flag words too
+    const bool rowspan = rowspan_wanted(in);
+    rowspan_set(geom, rowspan);
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
     g_pinned[CTRL_DSORT_PASSES] = 0;
@@ -294,7 +322,8 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
     // the rects in rank order and the emission offsets (upstream's InclusiveSum of
     // tiles_touched, in depth order), queued before the host waits: the device stays
     // busy (with three passes queued it returns at once if the keys need four)
-    return step(timed(GSR_STAGE_SCAN, s, [&] { return launch_rank_gather(in->P, in->W, in->H, geom, passes == 3, s); }),
+    return step(timed(GSR_STAGE_SCAN, s,
+                      [&] { return launch_rank_gather(in->P, in->W, in->H, geom, passes == 3, rowspan, s); }),
                 "rank gather", dbg, s);
 }
 
@@ -317,7 +346,10 @@ static int finish_preprocess(const gsr_inputs *in, void *geom, int passes, hipSt
                           "depth sort (fourth pass)", dbg, s))
             return rc;
         if (int rc = step(timed(GSR_STAGE_SCAN | TIMED_MORE, s,
-                                [&] { return launch_rank_gather(in->P, in->W, in->H, geom, false, s); }),
+                                [&] {
+                                    return launch_rank_gather(in->P, in->W, in->H, geom, false,
+                                                              rowspan_get(geom, in), s);
+                                }),
                           "rank gather", dbg, s))
             return rc;
     }
@@ -358,7 +390,17 @@ static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t
                         uint8_t *visible_out, hipStream_t s, bool dbg) {
     const size_t npix = (size_t)3 * in->W * in->H;
     float *l1_part = gt ? at<float>(img, img_layout(in->W, in->H).l1_part) : nullptr;
-    if (n > 0) {
+    if (n > 0 && rowspan_get(geom, in)) {
+        // row-span binning: pass A (spans by tile row), pass B (tiles by column)
+        if (int rc = step(timed(GSR_STAGE_DUPLICATE, s,
+                                [&] { return launch_rowspan_a(in->P, in->W, in->H, geom, binning, cap, g, s); }),
+                          "row spans", dbg, s))
+            return rc;
+        if (int rc = step(timed(GSR_STAGE_TILE_SORT, s,
+                                [&] { return launch_rowspan_b(in->P, in->W, in->H, geom, binning, cap, g, s); }),
+                          "tile columns", dbg, s))
+            return rc;
+    } else if (n > 0) {
         if (int rc = step(timed(GSR_STAGE_DUPLICATE, s,
                                 [&] { return launch_emit(in->P, in->W, in->H, geom, binning, cap, g, s); }),
                           "duplicateWithKeys", dbg, s))

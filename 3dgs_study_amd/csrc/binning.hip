@@ -46,6 +46,8 @@
 #include "gsr_kernels.hpp"
 #include "gsr_math.hpp"
 #include "gsr_publish.hpp"
+#include "gsr_radix.hpp"
+#include "gsr_spans.hpp"
 #include "gsr_wave.hpp"
 
 #include <type_traits>
@@ -54,32 +56,6 @@ namespace gsr {
 
 constexpr int RX_WAVES = RX_THREADS / 64;
 static_assert(RX_THREADS == RADIX, "one thread per digit in the per-block digit loops");
-
-// Lanes of the wave whose digit equals this lane's (restricted to `live`),
-// comparing the NB low digit bits (the digit is masked, so comparing more bits
-// than the pass has is harmless).  Per bit: s = the sign-extended bit (0 or ~0,
-// one v_bfe_i32), one ballot of s, and per mask half m &= ~(ballot ^ s) as ONE
-// v_bitop3_b32 (truth table 0x90: m & (ballot == s)): 4 VALU per bit.  (A runtime
-// bit count with a per-lane select of ballot / ~ballot compiled to ~11.)
-__device__ __forceinline__ uint32_t and_xnor(uint32_t m, uint32_t bal, uint32_t s) {
-    return __builtin_amdgcn_bitop3_b32(m, bal, s, 0x90);  // the builtin: the compiler pads its hazards
-}
-template <int NB>
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t live) {
-    uint32_t lo = (uint32_t)live, hi = (uint32_t)(live >> 32);
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-        const uint32_t s = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);  // feeds the ballot too
-        const uint64_t bal = __ballot(s != 0u);
-        lo = and_xnor(lo, (uint32_t)bal, s);
-        hi = and_xnor(hi, (uint32_t)(bal >> 32), s);
-    }
-    return ((uint64_t)hi << 32) | lo;
-}
-// number of set bits of m below this lane
-__device__ __forceinline__ uint32_t count_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 
 struct RadixPass {
     const uint32_t *kin;   // keys (the digit source)
@@ -126,6 +102,10 @@ struct RadixPass {
     // tile sort queued before the host knows num_rendered (gsr_forward): n is the
     // buffer's capacity and every kernel works on the published count instead
     SpecGuard g;
+    // digit scan over a block count the device computed (row-span pass B): NB is
+    // then the hist stride and *nb_dev (<= NB) the blocks to scan; the scan does
+    // nothing unless the speculative guard holds
+    const uint32_t *nb_dev;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
@@ -156,18 +136,6 @@ __device__ __forceinline__ uint2 dsort_base_passes(uint32_t kmin, uint32_t kmax)
 __device__ __forceinline__ uint32_t key_rel(uint32_t k, uint32_t base, uint32_t passes) {
     const uint32_t d = k - base;
     return passes == 3 && d > 0xffffffu ? (0xffff00u | (d & 0xffu)) : d;
-}
-
-// Workgroup -> radix block.  The per-block digit counts live column-major
-// (hist[digit][block], so the digit scan reads rows); neighbouring blocks share
-// their 32-B sectors.  Workgroups are dealt round-robin over the 8 XCDs, so give
-// each XCD a contiguous run of blocks: a sector's partial writes (upsweep) and
-// reads (downsweep) then meet in one L2 instead of crossing to HBM once per
-// block.  A bijection on [0, NB); placement is a speed hint only.
-__device__ __forceinline__ uint32_t radix_block(int NB) {
-    const uint32_t x = blockIdx.x & 7u, j = blockIdx.x >> 3;
-    const uint32_t q = (uint32_t)NB >> 3, r = (uint32_t)NB & 7u;
-    return x * q + min(x, r) + j;
 }
 
 // The second pass's segment table from the first pass's digit totals: segment
@@ -342,9 +310,27 @@ __global__ void __launch_bounds__(DSCAN_THREADS) radix_digit_scan_kernel(RadixPa
         return;
     }
     if (pass_skipped(a)) return;
+    if (a.nb_dev && !spec_ok(a.g)) return;
+    const int n = a.nb_dev ? (int)min(*a.nb_dev, (uint32_t)a.NB) : a.NB;
     const uint32_t tot =
-        block_exclusive_scan_inplace<DSCAN_THREADS, DSCAN_PER>(a.hist + (size_t)blockIdx.x * a.NB, a.NB, wsum);
+        block_exclusive_scan_inplace<DSCAN_THREADS, DSCAN_PER>(a.hist + (size_t)blockIdx.x * a.NB, n, wsum);
     if (threadIdx.x == 0) a.totals[blockIdx.x] = tot;
+}
+
+// Exclusive scan of each of `digits` count rows hist[d][0, n) in place (stride
+// NB; n = *nb_dev when given), totals[d] = the row's sum: the digit scan of the
+// row-span passes (rowspan.hip).
+hipError_t launch_count_scan(uint32_t *hist, int NB, const uint32_t *nb_dev, uint32_t *totals, int digits,
+                             const SpecGuard &g, hipStream_t s) {
+    RadixPass a = {};
+    a.hist = hist;
+    a.NB = NB;
+    a.nb_dev = nb_dev;
+    a.totals = totals;
+    a.role = RX_PLAIN;
+    a.g = g;
+    hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(digits), dim3(DSCAN_THREADS), 0, s, a);
+    return hipGetLastError();
 }
 
 template <int ITEMS, int MODE>
@@ -595,14 +581,20 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t lo, uint32_t hi, uint32
 // issued first) and writes each one's instances before it within the workgroup,
 // and its total; emit_kernel adds the totals of the workgroups before its own —
 // so no scan launch sits between this kernel and the emission.
+// Row-span binning (rs_gy > 0, rowspan.hip) instead: the spans of each pass-A
+// block (RSA_GAUSS ranks) per tile row, rs_ahist[row][block] (one LDS add per span).
 __global__ void __launch_bounds__(RG_THREADS)
     rank_gather_kernel(const uint32_t *order, const uint4 *rects, int P, uint4 *rects_ranked, uint32_t *local,
-                       uint32_t *super, const uint32_t *dsort_ctrl) {
+                       uint32_t *super, const uint32_t *dsort_ctrl, uint32_t *rs_ahist, int rs_nA, int rs_gy) {
+    constexpr int AB = RG_THREADS * RG_RANKS / RSA_GAUSS;  // pass-A blocks per workgroup
     __shared__ uint32_t wsum[RG_RANKS][RG_THREADS / 64];
+    __shared__ uint32_t rows[AB][RADIX];
     // queued before the host knows the pass count: a four-pass sort is not done yet
     // (the host launches its fourth pass and this kernel again)
     if (dsort_ctrl && dsort_ctrl[DCTRL_PASSES] != 3u) return;
     const int r0 = blockIdx.x * RG_THREADS * RG_RANKS + threadIdx.x;
+    if (rs_gy)
+        for (int i = threadIdx.x; i < AB * RADIX; i += RG_THREADS) (&rows[0][0])[i] = 0u;
     uint32_t id[RG_RANKS];
 #pragma unroll
     for (int k = 0; k < RG_RANKS; k++) {
@@ -612,6 +604,26 @@ __global__ void __launch_bounds__(RG_THREADS)
     uint4 q[RG_RANKS];
 #pragma unroll
     for (int k = 0; k < RG_RANKS; k++) q[k] = r0 + k * RG_THREADS < P ? rects[id[k]] : make_uint4(0u, 0u, 0u, 0u);
+    if (rs_gy) {
+        __syncthreads();  // the row counts are zeroed
+#pragma unroll
+        for (int k = 0; k < RG_RANKS; k++) {
+            const int r = r0 + k * RG_THREADS;
+            if (r < P) rects_ranked[r] = q[k];
+            const Foot f = foot_of(q[k]);
+            uint32_t *h = rows[(k * RG_THREADS + threadIdx.x) / RSA_GAUSS];
+            for (uint32_t y = f.y0; y < f.y1; y++)
+                if (foot_row_kept(f, y - f.y0)) atomicAdd(&h[y], 1u);
+        }
+        __syncthreads();
+        // rows[j][y] -> rs_ahist[y][block]: eight consecutive threads write one row's
+        // 32-B run of this workgroup's eight blocks
+        for (int i = threadIdx.x; i < AB * rs_gy; i += RG_THREADS) {
+            const int y = i / AB, j = i % AB, blk = blockIdx.x * AB + j;
+            if (blk < rs_nA) rs_ahist[(size_t)y * rs_nA + blk] = rows[j][y];
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < RG_RANKS; k++) {
         const int r = r0 + k * RG_THREADS;
@@ -994,14 +1006,20 @@ hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t
 
 // After the depth sort: the rects in rank order and the rank-order instance offsets
 // of the emit blocks.
-hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hipStream_t s) {
+// rowspan: the row-span binning follows (rowspan.hip): the pass-A row counts
+// instead of the emission offsets, and their per-row scan
+hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, bool rowspan, hipStream_t s) {
     if (P <= 0) return hipSuccess;
     const GeomLayout L = geom_layout(P, W, H);
+    const int gy = rowspan ? grid_dims(W, H).gy : 0, nA = rsa_blocks(P);
+    uint32_t *ahist = at<uint32_t>(geom, L.rs_ahist);
     hipLaunchKernelGGL(rank_gather_kernel, dim3(rg_blocks(P)), dim3(RG_THREADS), 0, s,
                        at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), at<const uint4>(geom, L.rects), P,
                        at<uint4>(geom, L.rects_ranked), at<uint32_t>(geom, L.emit_sums),
-                       at<uint32_t>(geom, L.emit_super), require3 ? at<const uint32_t>(geom, L.dsort_ctrl) : nullptr);
-    return hipGetLastError();
+                       at<uint32_t>(geom, L.emit_super), require3 ? at<const uint32_t>(geom, L.dsort_ctrl) : nullptr,
+                       ahist, nA, gy);
+    if (!rowspan) return hipGetLastError();
+    return launch_count_scan(ahist, nA, nullptr, at<uint32_t>(geom, L.rs_atot), gy, SpecGuard{}, s);
 }
 
 hipError_t launch_emit(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &guard,

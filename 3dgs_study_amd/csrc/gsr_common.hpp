@@ -111,6 +111,24 @@ __host__ __device__ inline int dsort_nsup(int P) {
 }
 __host__ __device__ inline int pre_blocks(int P) { return (P + PRE_THREADS - 1) / PRE_THREADS; }
 
+// Row-span binning (rowspan.hip), the default for grids of at most RADIX x RADIX
+// tiles (a tile row and a tile column are each one 8-bit digit): pass A sorts the
+// footprints' row spans by tile row in blocks of RSA_GAUSS ranks, pass B their
+// tiles by column in blocks of RSB_SPANS spans of one row.  Each workgroup expands
+// and scatters its items in rounds of RS_THREADS * ITEMS.
+constexpr int RS_THREADS = 256;
+constexpr int RSA_GAUSS = 512, RSA_ITEMS = 8;
+constexpr int RSB_SPANS = 1024, RSB_ITEMS = 16;
+static_assert(RS_THREADS == RADIX, "one thread per digit in the per-block digit loops");
+static_assert(RG_THREADS % RSA_GAUSS == 0, "rank_gather_kernel counts whole A blocks");
+__host__ __device__ inline bool rowspan_grid(int W, int H) {
+    const GridDims g = grid_dims(W, H);
+    return g.gx <= RADIX && g.gy <= RADIX;
+}
+__host__ __device__ inline int rsa_blocks(int P) { return P > 0 ? (P + RSA_GAUSS - 1) / RSA_GAUSS : 1; }
+// pass B's blocks: ceil(spans of row r / RSB_SPANS) per row, spans <= instances <= cap
+__host__ __device__ inline int rsb_blocks_max(int64_t cap, int gy) { return (int)(cap / RSB_SPANS) + gy + 1; }
+
 // ---- control words (uint32 [16]) inside the geom buffer (a device copy of what
 // preprocess publishes to the host: num_rendered, the prefiltered error) ----
 enum CtrlWord {
@@ -168,7 +186,9 @@ struct GeomLayout {
     size_t dsort_sup;     // uint32 [3][dsort_nsup(P)][RADIX] passes 2-4: digit counts per group of DSORT_SB blocks
     size_t emit_sums;     // uint32 [emit_blocks(P)] instances before each emit block within its rank-gather block
     size_t emit_super;    // uint32 [rg_blocks(P)] instances per rank-gather block (RG_SUPER emit blocks)
-    size_t order_cnt;     // uint32 [8][32] backward wave-order bucket counts + the ORDER_FLAGS words (zeroed by preprocess)
+    size_t rs_ahist;      // uint32 [gy][rsa_blocks(P)] row-span pass A: spans per (tile row, block) -> block offsets
+    size_t rs_atot;       // uint32 [RADIX] spans per tile row
+    size_t order_cnt;    // uint32 [8][32] backward wave-order bucket counts + the ORDER_FLAGS words (zeroed by preprocess)
     size_t accum;         // float [P][ACCUM_STRIDE] the backward's gradient accumulator (gsr.h GSR_FLAG_PREPARE_BACKWARD)
     size_t shjac;         // float [9][P] d colour / d view direction (GSR_FLAG_PREPARE_BACKWARD with SH colours)
     size_t bytes;
@@ -201,6 +221,8 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.off[GSR_GEOM_DSORT_CTRL] = L.dsort_ctrl;
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
     L.emit_super = take((size_t)rg_blocks(P) * 4 + 4);
+    L.rs_ahist = take(rowspan_grid(W, H) ? (size_t)g.gy * rsa_blocks(P) * 4 : 4);
+    L.rs_atot = take((size_t)RADIX * 4);
     L.order_cnt = take((8 * 32 + 2) * 4);
     L.accum = take((size_t)(P > 0 ? P : 1) * 16 * 4);
     L.shjac = take((size_t)9 * (P > 0 ? P : 1) * 4);
@@ -215,12 +237,15 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
 // the forward was given.
 struct BinningLayout {
     size_t off[GSR_BIN_NFIELDS];
-    size_t keys_b;  // uint32 [cap] tile-sort ping-pong
-    size_t vals_b;  // uint32 [cap]
-    size_t hist;    // uint32 [RADIX][radix_blocks(cap, tsort_items(cap)) + RADIX] (+ RADIX: segment-aligned blocks)
+    size_t keys_b;  // uint32 [cap] tile-sort ping-pong; row-span binning: the spans' columns x0 | x1 << 16
+    size_t vals_b;  // uint32 [cap]; row-span binning: the spans' Gaussian ids (spans <= instances)
+    size_t hist;    // uint32 [RADIX][radix_blocks(cap, tsort_items(cap)) + RADIX] (+ RADIX: segment-aligned blocks);
+                    // row-span pass B: [RADIX][rsb_blocks_max(cap, gy)] column counts per block
+    size_t hist_stride;  // row-span pass B's block stride in hist (rsb_blocks_max)
     size_t totals;  // uint32 [RADIX]
     size_t totals1; // uint32 [RADIX] the first tile pass's digit totals (the second pass's segments)
     size_t seg_table; // uint32 [2][RADIX + 1] the second pass's segment table: first block, first item
+                      // (row-span pass B: per tile row; [RADIX] = blocks, [2 RADIX + 1] = spans)
     size_t qmask;   // uint64 [4][qmask_stride] per quadrant, per 64-entry chunk of its tile's list: the
                     // entries that reach the quadrant (render_fwd's cull), for render_bwd (qmask_index)
     size_t qmask_stride;
@@ -242,10 +267,14 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t cap, int W, int 
     L.off[GSR_BIN_KEYS] = take(n * 4);
     L.keys_b = take(n * 4);
     L.vals_b = take(n * 4);
-    L.hist = take((size_t)RADIX * (radix_blocks((int64_t)n, tsort_items((int64_t)n)) + RADIX) * 4);
+    const GridDims gd = grid_dims(W, H);
+    const size_t lsd = (size_t)radix_blocks((int64_t)n, tsort_items((int64_t)n)) + RADIX;
+    L.hist_stride = (size_t)rsb_blocks_max((int64_t)n, gd.gy);
+    L.hist = take((size_t)RADIX * (lsd > L.hist_stride ? lsd : L.hist_stride) * 4);
     L.totals = take((size_t)RADIX * 4);
     L.totals1 = take((size_t)RADIX * 4);
     L.seg_table = take((size_t)2 * (RADIX + 1) * 4);
+    L.off[GSR_BIN_ROWSPAN] = L.seg_table;
     L.qmask_stride = n / 64 + (size_t)grid_dims(W, H).tiles + 2;
     L.qmask = take(4 * L.qmask_stride * 8);
     L.bytes = o;

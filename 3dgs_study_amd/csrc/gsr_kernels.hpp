@@ -20,7 +20,10 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
                              int passes, uint32_t *host_ctrl, hipStream_t s);
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s);
-hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, hipStream_t s);
+// rowspan: the row-span binning follows (pass A's row counts and their scan)
+hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, bool rowspan, hipStream_t s);
+hipError_t launch_count_scan(uint32_t *hist, int NB, const uint32_t *nb_dev, uint32_t *totals, int digits,
+                             const SpecGuard &g, hipStream_t s);
 // cap: the binning buffer's instance capacity (its layout); g: speculative guard
 // (gsr_common.hpp SpecGuard; ctrl NULL = the count is exact, cap == num_rendered
 // or larger)
@@ -28,6 +31,13 @@ hipError_t launch_emit(int P, int W, int H, void *geom, void *binning, int64_t c
                        hipStream_t s);
 hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int64_t n, int64_t cap,
                             const SpecGuard &g, hipStream_t s);
+// rowspan.hip: the row-span binning (grids of at most 256 x 256 tiles), after
+// launch_rank_gather(..., rowspan = true): pass A (spans by tile row), pass B
+// (tiles by column into point_list, and the tile ranges)
+hipError_t launch_rowspan_a(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g,
+                            hipStream_t s);
+hipError_t launch_rowspan_b(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g,
+                            hipStream_t s);
 hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const void *binning, int64_t I,
                                   uint64_t *keys, hipStream_t s);
 

@@ -64,16 +64,17 @@ EXPORTED = (
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
     "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
-    "gsr_forward_render_l1", "gsr_forward", "gsr_timing_sample",
+    "gsr_forward_render_l1", "gsr_forward", "gsr_timing_sample", "gsr_binning_mode",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
 FOOTPRINTS = {"rect": 0, "tight": 1}
-# The package default is "tight" (DESIGN.md §2): image, radii, final_T and every
-# gradient are upstream's either way, and of upstream's outputs only the
-# num_rendered integer differs; GSR_FOOTPRINT=rect (or set_footprint("rect"))
-# gives upstream's lists bit for bit.  (The C struct's zero value is RECT.)
-_footprint = os.environ.get("GSR_FOOTPRINT", "tight")
+# The package default is "rect" (DESIGN.md §2): upstream's getRect footprint, so
+# num_rendered, point_list, ranges and n_contrib are upstream's bit for bit.
+# GSR_FOOTPRINT=tight (or set_footprint("tight")) bins only the rect tiles the
+# alpha >= 1/255 ellipse reaches: the same image, radii, final_T and gradients with
+# shorter lists (num_rendered counts those).  (The C struct's zero value is RECT.)
+_footprint = os.environ.get("GSR_FOOTPRINT", "rect")
 if _footprint not in FOOTPRINTS:
     raise ImportError(f"GSR_FOOTPRINT={_footprint!r}: expected one of {sorted(FOOTPRINTS)}")
 
@@ -81,8 +82,8 @@ if _footprint not in FOOTPRINTS:
 def set_footprint(mode: str) -> str:
     """Select the tile footprint of later forwards; returns the previous mode.
 
-    "rect": upstream's getRect footprint — num_rendered, the sorted keys, point_list,
-    ranges and n_contrib are upstream's.  "tight" (default): only the rect tiles the
+    "rect" (default): upstream's getRect footprint — num_rendered, the sorted keys,
+    point_list, ranges and n_contrib are upstream's.  "tight": only the rect tiles the
     Gaussian's alpha >= 1/255 ellipse reaches (same image, radii and gradients, ~40 %
     fewer list entries at config C; num_rendered counts the shorter lists)."""
     global _footprint
@@ -94,6 +95,29 @@ def set_footprint(mode: str) -> str:
 
 def get_footprint() -> str:
     return _footprint
+
+
+# gsr_binning_mode (include/gsr.h): how the (tile, Gaussian) lists are sorted.  Both
+# forms give upstream's point_list and ranges bit for bit.
+BINNING_MODES = {"rowspan": 0, "lsd": 1}
+
+
+def set_binning_mode(mode: str) -> str:
+    """Select the binning of later forwards; returns the previous mode.  "rowspan"
+    (default): the footprints' row spans sorted by tile row, then their tiles by
+    column (grids of at most 256 x 256 tiles; larger grids take the LSD sort);
+    "lsd": an emission in depth order and a stable LSD radix sort by tile index."""
+    if mode not in BINNING_MODES:
+        raise ValueError(f"binning mode must be one of {sorted(BINNING_MODES)} (got {mode!r})")
+    lib = load_library()
+    prev = lib.gsr_binning_mode(BINNING_MODES[mode])
+    if prev < 0:
+        raise RuntimeError(lib.gsr_last_error().decode())
+    return {v: k for k, v in BINNING_MODES.items()}[prev]
+
+
+def get_binning_mode() -> str:
+    return {v: k for k, v in BINNING_MODES.items()}[load_library().gsr_binning_mode(-1)]
 
 
 class GsrLeafGrads(ctypes.Structure):
@@ -157,7 +181,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lib = None
 
@@ -222,6 +246,8 @@ def load_library():
     lib.gsr_img_layout.argtypes = [i32, i32, ctypes.POINTER(sz), ctypes.c_int]
     lib.gsr_timing_enable.argtypes = [ctypes.c_int]
     lib.gsr_timing_enable.restype = ctypes.c_int
+    lib.gsr_binning_mode.argtypes = [ctypes.c_int]
+    lib.gsr_binning_mode.restype = ctypes.c_int
     lib.gsr_timing_sample.argtypes = [ctypes.c_int]
     lib.gsr_timing_sample.restype = ctypes.c_int
     lib.gsr_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -463,13 +489,15 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
         done = rc != NEED_BINNING
         if done:
             _check(rc, "rasterize_gaussians")
-        last_forward.update(capacity=cap, num_rendered=num_rendered.value, path="one call" if done else "regrown")
+        last_forward.update(capacity=cap, num_rendered=num_rendered.value, path="one call" if done else "regrown",
+                            binning=binning if done else None)
     else:
         _check(lib.gsr_forward_preprocess(ctypes.byref(s), geom.data_ptr(), _ptr(radii), ctypes.byref(num_rendered),
                                           stream), "rasterize_gaussians (preprocess)")
         last_forward.update(capacity=None, num_rendered=num_rendered.value, path="two calls")
     if not done:
         binning = _alloc((lib.gsr_binning_bytes(num_rendered.value, W, H),), torch.uint8, device)
+        last_forward.update(binning=binning)
         if gt is None:
             _check(lib.gsr_forward_render(ctypes.byref(s), geom.data_ptr(), binning.data_ptr(), img.data_ptr(),
                                           num_rendered.value, _ptr(radii), out_color.data_ptr(), stream),
@@ -717,6 +745,19 @@ def point_list_keys(P, W, H, geomBuffer, binningBuffer, num_rendered):
     return keys
 
 
+def last_spans(W: int, H: int):
+    """Row spans of the last forward (the row-span binning's pass-A output, for the
+    byte model of bench.py), or None when it took the LSD sort.  Synchronises."""
+    b = last_forward.get("binning")
+    if b is None or get_binning_mode() != "rowspan" or (W + 15) // 16 > 256 or (H + 15) // 16 > 256:
+        return None
+    cap = last_forward.get("capacity") or last_forward.get("num_rendered", 0)
+    off = layouts(1, W, H, cap)[1].get("rowspan")
+    if off is None or not last_forward.get("num_rendered"):
+        return None
+    return int(b[off + 4 * 513:off + 4 * 514].view(torch.int32).item())
+
+
 def layouts(P, W, H, num_rendered):
     """Byte offsets of the named scratch sub-arrays (parity tests read intermediates)."""
     lib = load_library()
@@ -728,5 +769,5 @@ def layouts(P, W, H, num_rendered):
     ni = lib.gsr_img_layout(W, H, im, 16)
     geom_names = ("depths", "means2D", "splats", "clamped", "tiles_touched", "ranges", "ctrl", "depth_order",
                   "dsort_ctrl")  # (binning: point_list at offset 0 for every capacity)
-    return (dict(zip(geom_names, list(g)[:n])), dict(zip(("keys", "point_list"), list(b)[:nb])),
+    return (dict(zip(geom_names, list(g)[:n])), dict(zip(("keys", "point_list", "rowspan"), list(b)[:nb])),
             dict(zip(("final_T", "n_contrib"), list(im)[:ni])))

@@ -27,10 +27,13 @@ exchange's all-reduce bucket.  ``set_grad_exchange(None)`` restores upstream
 behaviour.
 
 Tile footprint (not upstream; ``set_footprint``, env ``GSR_FOOTPRINT``): "rect"
-bins every tile of upstream's getRect rect, so ``num_rendered`` and the binning
-buffer's lists are upstream's bit for bit; "tight" (default) bins only the tiles
+(default) bins every tile of upstream's getRect rect, so ``num_rendered`` and the
+binning buffer's lists are upstream's bit for bit; "tight" bins only the tiles
 the alpha >= 1/255 ellipse reaches — the same image, radii and gradients from
 shorter lists (of upstream's outputs only the ``num_rendered`` integer differs).
+Binning form (``set_binning_mode``): "rowspan" (default; row spans sorted by tile
+row, then their tiles by column) or "lsd" (a radix sort by tile index); both give
+upstream's lists.
 
 Debug mode (``raster_settings.debug``): the native side synchronises after every
 kernel; on failure a CPU copy of the arguments is written to
@@ -46,11 +49,12 @@ import torch.nn as nn
 
 from . import _C
 
-from ._C import get_footprint, set_footprint  # noqa: E402
+from ._C import get_binning_mode, get_footprint, set_binning_mode, set_footprint  # noqa: E402
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "rasterize_model",
            "set_sh_grad_sink",
-           "set_grad_exchange", "set_footprint", "get_footprint", "set_fused_leaf_grads"]
+           "set_grad_exchange", "set_footprint", "get_footprint", "set_binning_mode", "get_binning_mode",
+           "set_fused_leaf_grads"]
 
 _exchange = None
 # None = automatic (on, except in a multi-rank process group with no exchange of

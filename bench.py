@@ -263,6 +263,9 @@ def main():
                          "with the fused loss kernel; 'reference' is the reference's render() + torch loss")
     ap.add_argument("--glue-steps", type=int, default=100,
                     help="N=1: timed steps of the same unit with the other glue, reported beside; 0 = skip")
+    ap.add_argument("--binning", default="rowspan", choices=["rowspan", "lsd"],
+                    help="the binning form (gsr_binning_mode): the row-span binning (default) or the LSD sort by "
+                         "tile index; the same lists either way")
     ap.add_argument("--config-b-steps", type=int, default=200,
                     help="N=1: timed steps of config B (100k, 800x800, SH3, fwd+bwd) reported beside; 0 = skip")
     args = ap.parse_args()
@@ -291,6 +294,7 @@ def main():
     if world > 1:
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
+    _C.set_binning_mode(args.binning)
     if not synthetic.CONFIGS[args.config]["backward"]:
         render_main(args, dev, world, rank)
         return
@@ -402,7 +406,8 @@ def main():
             "config": {
                 "workload": f"{args.config}: {WORKLOADS[args.config]}",
                 "gaussians": P, "width": W, "height": H, "sh_degree": deg,
-                "footprint": _C.get_footprint(), "num_rendered": I, "views_per_step": world,
+                "footprint": _C.get_footprint(), "binning": _C.get_binning_mode(), "num_rendered": I,
+                "views_per_step": world,
                 "loss": "L1" if not args.lambda_dssim else f"L1+{args.lambda_dssim}*(1-SSIM)",
                 "glue": GLUE_NOTE[args.glue],
                 "parallelism": f"view-parallel x{world}" + (
@@ -469,9 +474,9 @@ def main():
         if world == 1 and args.render_steps > 0:
             out = None
             line["config_E_render"] = render_rates("E", dev, args.render_steps, 3, glue=args.glue)
-            if _C.get_footprint() != "rect":  # upstream's instance set (I ~ 110M): the tile sort's stress case
-                line["config_E_render_rect"] = render_rates("E", dev, args.render_steps, 3, footprint="rect",
-                                                            glue=args.glue)
+            other_fp = "tight" if _C.get_footprint() == "rect" else "rect"  # the other footprint beside
+            line["config_E_render_" + other_fp] = render_rates("E", dev, args.render_steps, 3, footprint=other_fp,
+                                                               glue=args.glue)
             if args.glue_steps > 0:
                 other = "reference" if args.glue == "fused" else "fused"
                 line[f"config_E_render_{other}_glue"] = render_rates("E", dev, args.render_steps, 3, glue=other)

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 10
+#define GSR_ABI_VERSION 11
 
 enum gsr_status {
     GSR_OK = 0,
@@ -360,6 +360,8 @@ enum gsr_geom_field {
 enum gsr_binning_field {
     GSR_BIN_KEYS = 0,        /* uint32 [cap] tile-sort scratch */
     GSR_BIN_POINT_LIST,      /* uint32 [I]  Gaussian ids in (tile, depth, id) order: offset 0 */
+    GSR_BIN_ROWSPAN,         /* uint32 [2][257] row-span binning (gsr_binning_mode 0): per tile row the first pass-B
+                                block and first span; [256] = pass-B blocks, [513] = spans of the forward */
     GSR_BIN_NFIELDS
 };
 enum gsr_img_field {
@@ -372,6 +374,14 @@ enum gsr_img_field {
  * num_rendered entries of a forward's binning buffer (keys: device, u64). */
 int gsr_point_list_keys(int32_t P, int32_t W, int32_t H, const void *geom, const void *binning,
                         int64_t num_rendered, uint64_t *keys, void *stream);
+/* Binning form (not upstream; ABI 11).  0 (the default): the row-span binning —
+ * every footprint's per-row spans sorted stably by tile row, then their tiles by
+ * column — for tile grids of at most 256 x 256 tiles (3840 x 3840 px at 16 x 16),
+ * the LSD sort by tile index beyond; 1: the LSD sort by tile index everywhere.
+ * Both produce upstream's point_list and ranges bit for bit.  Takes effect at the
+ * next preprocess; -1 queries.  Returns the previous mode, or -1 for any other
+ * argument (gsr_last_error says why; the mode is unchanged). */
+int gsr_binning_mode(int mode);
 int gsr_geom_layout(int32_t P, int32_t W, int32_t H, size_t *offsets, int cap);
 int gsr_binning_layout(int64_t capacity, int32_t W, int32_t H, size_t *offsets, int cap);
 int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap);
@@ -386,8 +396,8 @@ enum gsr_stage {
     GSR_STAGE_PREPROCESS = 0, /* FORWARD::preprocessCUDA */
     GSR_STAGE_SCAN,           /* InclusiveSum of tiles_touched: the rects in depth order + emission offsets */
     GSR_STAGE_DEPTH_SORT,     /* stable sort of the P depths */
-    GSR_STAGE_DUPLICATE,      /* duplicateWithKeys in depth order */
-    GSR_STAGE_TILE_SORT,      /* stable sort by tile (SortPairs) + identifyTileRanges */
+    GSR_STAGE_DUPLICATE,      /* duplicateWithKeys in depth order (row-span binning: the spans sorted by tile row) */
+    GSR_STAGE_TILE_SORT,      /* stable sort by tile (SortPairs) + identifyTileRanges (row spans: tiles by column) */
     GSR_STAGE_RENDER_FWD,     /* FORWARD::renderCUDA */
     GSR_STAGE_RENDER_BWD,     /* BACKWARD::renderCUDA */
     GSR_STAGE_PREPROCESS_BWD, /* BACKWARD::computeCov2DCUDA + preprocessCUDA */

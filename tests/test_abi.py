@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 10
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 11
     assert ctypes.sizeof(_C.GsrL1Seed) == 32  # struct gsr_l1_seed: three pointers and an int64
     # 12 x 4-byte scalars, 11 pointers, then sh_rest and two int32 (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 48 + 12 * 8 + 8
@@ -166,16 +166,34 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
 def test_footprint_selector():
     from diff_gaussian_rasterization import _C, get_footprint, set_footprint
 
-    assert get_footprint() == "tight"  # package default; "rect" = upstream's lists
-    prev = set_footprint("rect")
+    assert get_footprint() == "rect"  # package default: upstream's lists
+    prev = set_footprint("tight")
     try:
-        assert prev == "tight" and get_footprint() == "rect"
+        assert prev == "rect" and get_footprint() == "tight"
         with pytest.raises(ValueError, match="footprint must be"):
             set_footprint("box")
     finally:
         set_footprint(prev)
     assert _C.FOOTPRINTS == {"rect": 0, "tight": 1}
     assert lib_point_list_keys_validates()
+
+
+def test_binning_mode_selector():
+    from diff_gaussian_rasterization import get_binning_mode, set_binning_mode
+
+    assert get_binning_mode() == "rowspan"  # the default
+    prev = set_binning_mode("lsd")
+    try:
+        assert prev == "rowspan" and get_binning_mode() == "lsd"
+        with pytest.raises(ValueError, match="binning mode must be"):
+            set_binning_mode("bitonic")
+    finally:
+        set_binning_mode(prev)
+    from diff_gaussian_rasterization import _C
+
+    lib = _C.load_library()
+    assert lib.gsr_binning_mode(7) == -1 and "binning mode 7" in lib.gsr_last_error().decode()
+    assert lib.gsr_binning_mode(-1) == 0
 
 
 def lib_point_list_keys_validates():

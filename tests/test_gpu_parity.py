@@ -313,9 +313,21 @@ def test_needle_gaussians(dev, oracle, footprint):
     assert errs["dmeans2D"][0] <= GRAD_TOL and errs["dsh"][0] <= GRAD_TOL, errs
 
 
+@pytest.fixture(params=["rowspan", "lsd"])
+def binning(request):
+    """Both binning forms (gsr_binning_mode): the row-span binning (the default) and
+    the LSD sort by tile index."""
+    from diff_gaussian_rasterization import set_binning_mode
+
+    prev = set_binning_mode(request.param)
+    yield request.param
+    set_binning_mode(prev)
+
+
 @pytest.mark.parametrize("footprint", ["rect", "tight"])
-def test_long_tiles(dev, oracle, footprint):
-    """> 8192 instances per tile (long per-tile runs in the tile sort, long blend lists)."""
+def test_long_tiles(dev, oracle, footprint, binning):
+    """> 8192 instances per tile (long per-tile runs in the tile sort, long blend lists;
+    row spans: blocks expanded over several rounds)."""
     cam, g = case(30_000, 64, 48, 0, seed=6, radius=0.4, scale_range=(0.05, 0.2))
     h = run_hip(cam, g, dev, footprint=footprint)
     r = run_oracle(oracle, cam, g)
@@ -330,11 +342,13 @@ def test_long_tiles(dev, oracle, footprint):
     (3_000, 4000, 2200), # 34,500 tiles, 16 bits: 8 + 8, ids in 24 bits
     (1_000, 4112, 4100), # 66,049 tiles, 17 bits: three passes, ranges from the sorted keys
 ])
-def test_tile_sort_widths(dev, oracle, P, W, H):
+def test_tile_sort_widths(dev, oracle, P, W, H, binning):
     """The tile sort at every pass layout: one pass (<= 8 tile bits: configs A, the small
     cases above), the packed two-pass form (segment-aligned second pass, ranges from its
-    digit counts) from 9 to 16 bits, and three plain passes above 16 bits; keys,
-    point_list and ranges equal upstream's (rect footprint)."""
+    digit counts) from 9 to 16 bits, and three plain passes above 16 bits; the row-span
+    binning up to 250 x 138 tiles (17 bits: 258 x 257 tiles, beyond its 256 x 256 the
+    LSD sort in either mode); keys, point_list and ranges equal upstream's (rect
+    footprint)."""
     cam, g = case(P, W, H, 0, seed=11, view=0)
     h = run_hip(cam, g, dev, footprint="rect")
     r = run_oracle(oracle, cam, g)
@@ -362,6 +376,29 @@ def test_tile_sort_id_width_boundary(dev, oracle, P):
     r = run_oracle(oracle, cam, g, mt=True)
     assert h["num_rendered"] > 0 and int(h["point_list"].max()) >= (1 << 24) - 2
     check_forward(h, r)
+
+
+@pytest.mark.parametrize("footprint", ["rect", "tight"])
+@pytest.mark.parametrize("cfg", [dict(P=100_000, W=800, H=800, seed=2), dict(P=60_000, W=1920, H=1080, seed=3),
+                                 dict(P=3_000, W=4096, H=4096, seed=4)])
+def test_binning_modes_bit_identical(dev, cfg, footprint):
+    """The row-span binning and the LSD tile sort give the same binning buffer lists,
+    ranges, image and n_contrib, bit for bit (4096 x 4096: 256 x 256 tiles, the
+    largest row-span grid)."""
+    from diff_gaussian_rasterization import set_binning_mode
+
+    cam, g = case(cfg["P"], cfg["W"], cfg["H"], 3, seed=cfg["seed"])
+    out = {}
+    for mode in ("lsd", "rowspan"):
+        prev = set_binning_mode(mode)
+        try:
+            out[mode] = run_hip(cam, g, dev, footprint=footprint)
+        finally:
+            set_binning_mode(prev)
+    a, b = out["lsd"], out["rowspan"]
+    assert a["num_rendered"] == b["num_rendered"] > 0
+    for k in ("point_list", "ranges", "keys64", "n_contrib", "color", "final_T"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
 def test_empty_and_culled(dev, oracle):

@@ -8,7 +8,7 @@ set -e
 SRC=$1; shift
 cd "$(dirname "$0")/../3dgs_study_amd/csrc"
 make -s
-ALL="preprocess binning render_fwd render_bwd preprocess_bwd sh_exchange train_ops knn abi"
+ALL="preprocess binning rowspan render_fwd render_bwd preprocess_bwd sh_exchange train_ops knn abi"
 mkdir -p ../build/var
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
