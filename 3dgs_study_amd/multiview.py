@@ -86,7 +86,26 @@ class GradAllReduce:
     tests only).  ``comm_force=True`` runs every collective even in a one-rank
     group (tests and the bench's forced one-rank exchange: the RCCL calls on a
     one-GPU box).  ``timing=True`` records, per ``__call__``, how long the compute
-    stream waits for the exchange and how long the SH rebuild takes (``stats()``)."""
+    stream waits for the exchange and how long the SH rebuild takes (``stats()``).
+
+    The leaves' ``.grad`` are views of one flat bucket, and the bucket is reused the
+    next step when the caller let go of them (``.grad = None``) or left the views in
+    place — DDP's ``gradient_as_bucket_view``: a reference kept to last step's
+    ``.grad`` tensor is overwritten by the next step's gradients (clone it to keep it).
+
+    Early start and the loss graph (DDP's ``static_graph``).  The bucket's
+    all-reduce starts inside the rasterizer's backward (``rasterizer_done``) once the
+    first step after (re)binding has shown, on every rank, that no other gradient path
+    reaches a reduced leaf after the rasterizer's.  That probe step starts it at the
+    end of the backward instead, and each rank flags whether such a late gradient came
+    (a reduced leaf's accumulate hook after the rasterizer's backward); the flags are
+    summed in one spare float of the bucket, so every rank reads the same answer one
+    step later: none -> early starts from then on; any -> never (the late gradients are
+    packed into the bucket at the end of each backward, so the sums stay right).  If a
+    late gradient appears after early starts began (the loss graph changed), it is
+    left out on its rank (the replicas stay identical), the flag rides in the next
+    buckets, and every rank raises the same RuntimeError at the check after it (every
+    ``FLAG_EVERY`` steps) — no rank issues a collective the others do not."""
 
     def __init__(self, params: ParamSource, group=None, overlap: bool = True, sh=None, sh_force: bool = False,
                  rebuild=None, views_per_step: int = 1, comm_force: bool = False, timing: bool = False):
@@ -106,8 +125,17 @@ class GradAllReduce:
         self._views = None      # its per-parameter views
         self._work = None       # the bucket's async all-reduce
         self._early = False     # ... started by the rasterizer (rasterizer_done): the leaves' .grad are cleared
-        self._extra = None      # (indices, flat, work): gradients that reached reduced leaves after that start
         self._backwards = 0     # backwards finished this step
+        self._pushes = 0        # SH records pushed this step (views_per_step of them)
+        # early start (class docstring): "probe" until every rank's first step has shown
+        # no late gradient path, then "early"; "late" when one has
+        self._mode = "probe"
+        self._rast_seen = False  # this step's rasterizer backward has run (late = hooks after it)
+        self._view_ver = {}      # the bucket views' versions at the rasterizer's backward
+        self._late_local = False  # a late gradient reached a reduced leaf on this rank (sticky in "early")
+        self._flag_read = None   # (pinned float, event, mode when sent): the summed flag slot of a bucket
+        self._flag_send = None   # the mode of this step's flag, to be copied to the host in __call__
+        self._slot_fresh = True  # the bucket's flag slot holds garbage (a new bucket)
         self._cb_queued = False
         self.launched_in_backward = False  # the bucket's all-reduce started from the end-of-backward callback
         self._timing = timing
@@ -149,6 +177,7 @@ class GradAllReduce:
         self._index = {id(p): i for i, p in enumerate(self._reduced)}  # (strong refs: ids are unique)
         self._bucket = self._views = None
         self._bucket_cache = None
+        self._mode, self._late_local, self._flag_read, self._flag_send = "probe", False, None, None
         # hooks only while there is something to exchange: with one rank the leaves
         # carry none, and the rasterizer's fused leaf gradients apply as without us
         if self.overlap and self._active():
@@ -197,10 +226,76 @@ class GradAllReduce:
                 self._bucket, self._views = b, vs
         if self._bucket is None:
             ref = self._reduced[0]
-            self._bucket = torch.empty(sum(p.numel() for p in self._reduced), dtype=torch.float32, device=ref.device)
-            parts = self._bucket.split([p.numel() for p in self._reduced])
+            # + one spare float: the ranks' late-gradient flags, summed with the gradients
+            n = sum(p.numel() for p in self._reduced)
+            self._bucket = torch.empty(n + 1, dtype=torch.float32, device=ref.device)
+            parts = self._bucket[:n].split([p.numel() for p in self._reduced])
             self._views = [v.view(p.shape) for v, p in zip(parts, self._reduced)]
+            self._slot_fresh = True
         return self._bucket
+
+    # ---- the late-gradient flag (class docstring)
+    FLAG_EVERY = 16  # in "early" mode the summed flag is read back every FLAG_EVERY steps
+
+    def _set_flag_slot(self, bucket: torch.Tensor) -> None:
+        """This rank's flag into the bucket's spare float before its all-reduce: only
+        when it is not 0 already (a fresh bucket, or a raised flag)."""
+        flag = 1.0 if (self._late_local and self._mode != "late") else 0.0
+        if self._slot_fresh or flag:
+            bucket[-1:].fill_(flag)
+            self._slot_fresh = False
+
+    def _send_flag(self, bucket: torch.Tensor) -> None:
+        """The bucket's all-reduce is queued: its summed flag is copied to the host in
+        __call__, after the wait (probe steps, and every FLAG_EVERY-th step in "early"
+        mode)."""
+        if self._mode == "late" or self._flag_read is not None:
+            return
+        if self._mode == "early" and self._tstats["calls"] % self.FLAG_EVERY:
+            return
+        self._flag_send = self._mode
+
+    def _copy_flag(self) -> None:
+        mode, self._flag_send = self._flag_send, None
+        if mode is None or self._bucket is None:
+            return
+        b = self._bucket
+        if b.is_cuda:  # behind the collective on the compute stream (__call__ waited for it)
+            host = torch.empty(1, dtype=torch.float32, pin_memory=True)
+            host.copy_(b[-1:], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(b.device))
+        else:
+            host, ev = b[-1:].clone(), None
+        self._flag_read = (host, ev, mode)
+
+    def _check_flag(self) -> None:
+        """The summed flag of an earlier step's bucket (every rank reads the same value
+        at the same step): decides the probe, or raises on a late gradient.  By the
+        next step's backward the device is past that all-reduce (the forward's
+        num_rendered read-back waited for a later kernel), so the wait costs nothing."""
+        if self._flag_read is None:
+            return
+        host, ev, mode = self._flag_read
+        self._flag_read = None
+        if ev is not None:
+            ev.synchronize()
+        n = float(host.item())
+        if mode == "probe":
+            self._mode = "early" if n == 0 else "late"
+        elif n:
+            raise RuntimeError(
+                f"GradAllReduce: a gradient reached a reduced parameter after the bucket's all-reduce had started "
+                f"({int(n)} rank(s), within the last {self.FLAG_EVERY} steps): the loss graph changed after the "
+                f"first step (another term on a parameter the rasterizer writes), and that gradient was left out on "
+                f"every rank.  Re-create the exchange (its first step detects such paths) or call reset_graph() "
+                f"after changing the loss.")
+
+    def reset_graph(self) -> None:
+        """Probe the loss graph again at the next step (call it on every rank after
+        changing the loss terms): the next step starts its all-reduce at the end of the
+        backward and re-decides whether early starts are safe."""
+        self._mode, self._late_local, self._flag_read, self._flag_send = "probe", False, None, None
 
     @staticmethod
     def _is_view(g, v) -> bool:
@@ -235,6 +330,13 @@ class GradAllReduce:
         already hold their bucket view (a later backward of the step accumulates)."""
         if not (self.overlap and self._active()) or not self._reduced or self._stale():
             return {}
+        if self._rast_seen:  # a second rasterizer after the first one's early-start point
+            self._late_local = True
+        if self._work is not None or self._early:
+            # the bucket's all-reduce has started (ADVICE r5): a later writer gets no view
+            # — its gradients reach the leaves through autograd (a late gradient)
+            return {}
+        self._check_flag()
         self._ensure_bucket()
         self._queue_callback()
         out = {}
@@ -255,7 +357,12 @@ class GradAllReduce:
         from the end-of-backward callback instead, the host's round trip through the
         autograd engine left the device idle for ~65 us per step
         (``tools/exchange_profile.py`` traces)."""
+        self._rast_seen = self._backwards + 1 == self.views_per_step  # (the early start's point)
+        if self._views is not None:  # the views as the rasterizer left them (late-gradient test)
+            self._view_ver = {i: v._version for i, v in enumerate(self._views)}
         if self._work is not None or self._bucket is None or self._backwards + 1 != self.views_per_step:
+            return False
+        if self._mode != "early":  # the probe step (or a graph with late paths): start at the end
             return False
         covered = {id(v) for vs in views.values() for v in vs if v is not None}
         if any(id(v) not in covered for v in self._views):
@@ -266,7 +373,9 @@ class GradAllReduce:
         # the host here, so the launch order costs it nothing; what the exchange path
         # costs is host time (each event / stream switch ~5-10 us on the step's
         # critical host path, which the device waited for: exchange_profile traces).
+        self._set_flag_slot(self._bucket)
         self._work = self._reduce(self._bucket)
+        self._send_flag(self._bucket)
         self._sh_rebuild()
         self.launched_in_backward = True
         # The bucket now belongs to the collective.  Another gradient path into a
@@ -274,8 +383,8 @@ class GradAllReduce:
         # its AccumulateGrad after this backward — and would add in place into the
         # .grad it finds, i.e. into the bucket RCCL is reading, never to be reduced
         # (ADVICE r4).  So the leaves hold no .grad until __call__: such a
-        # contribution lands in a fresh tensor, reduced on its own at the end of the
-        # backward, and __call__ adds it to the reduced bucket and installs the views.
+        # contribution lands in a fresh tensor (flagged by the accumulate hook, left
+        # out on every rank alike: class docstring), and __call__ installs the views.
         self._early = True
         for p in self._reduced:
             if p.grad is not None:  # a view installed by an earlier backward of the step
@@ -350,20 +459,28 @@ class GradAllReduce:
 
     def _on_accumulate(self, p: torch.Tensor) -> None:
         if self._active():
+            if (self._rast_seen or self._early) and p.grad is not None:
+                # after the rasterizer's backward: a gradient arrived through autograd if
+                # .grad is not its bucket view as the rasterizer left it (the hook also
+                # runs when no gradient came: then .grad is that view, unchanged)
+                i = self._index.get(id(p))
+                v = self._views[i] if (self._views is not None and i is not None) else None
+                if v is None or not self._is_view(p.grad, v) or p.grad._version != self._view_ver.get(i):
+                    self._late_local = True
             self._queue_callback()
 
     def _on_backward_end(self) -> None:
         self._cb_queued = False
+        self._rast_seen = False
         self._backwards += 1
         if self._backwards > self.views_per_step:
             raise RuntimeError(f"GradAllReduce: {self._backwards} backwards in one step (views_per_step="
                                f"{self.views_per_step}); the bucket's all-reduce already started")
         if self._early and self._backwards == self.views_per_step:
-            extra = [(i, p.grad) for i, p in enumerate(self._reduced) if p.grad is not None]
-            if extra:
-                flat = torch.cat([g.detach().reshape(-1).to(torch.float32) for _, g in extra])
-                work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-                self._extra = ([i for i, _ in extra], flat, work)
+            # late gradients after the early start are left out on this rank (flagged:
+            # every rank raises at the next read of the flags); no collective of its own
+            for p in self._reduced:
+                p.grad = None
             return
         if self._backwards == self.views_per_step and self._work is None and not self._stale():
             bucket = self._pack()
@@ -371,7 +488,9 @@ class GradAllReduce:
             # gathered records) queued here too, behind the backward's last kernel,
             # instead of after the host has returned from backward() into the caller's
             # __call__ (a host round trip the device spent idle: 60-90 us per step)
+            self._set_flag_slot(bucket)
             self._work = self._reduce(bucket)
+            self._send_flag(bucket)
             self._sh_rebuild()
             self.launched_in_backward = True
 
@@ -417,7 +536,7 @@ class GradAllReduce:
         # (stream order makes that safe: its gather and its rebuild are done before
         # the next step's backward writes it, and the compute stream waited for both)
         from diff_gaussian_rasterization import _C
-        i, n, dev = len(self._gathers), _C.sh_record_floats(P), self._sh[0].device
+        i, n, dev = self._pushes, _C.sh_record_floats(P), self._sh[0].device
         while len(self._recs) <= i:
             self._recs.append(None)
         slot = self._recs[i]
@@ -477,7 +596,14 @@ class GradAllReduce:
         that queues the colour gradient's kernel on the current stream — called here
         first, on the exchange stream when the collectives run in stream order (the
         render backward is what the compute stream holds so far), else in line."""
-        i = len(self._gathers)
+        i = self._pushes
+        if i >= self.views_per_step:
+            # the step's SH rebuild is already queued over views_per_step records (ADVICE
+            # r5): another record would start a second rebuild that overwrites the first
+            raise RuntimeError(f"GradAllReduce: SH record {i + 1} in one step with views_per_step="
+                               f"{self.views_per_step} (a second rasterizer call in one backward?); construct "
+                               f"the exchange with views_per_step equal to the rasterizer calls per step")
+        self._pushes += 1
         slot = self._recs[i] if i < len(self._recs) else None
         if slot is None or slot[0] is not rec:  # a record not made by record(): header now, gather behind it
             if slot is not None:
@@ -502,7 +628,7 @@ class GradAllReduce:
                     side.wait_stream(torch.cuda.current_stream(rec.device))
                 else:
                     side.wait_event(ready)
-                last = len(self._gathers) + 1 == self.views_per_step and self.rebuild_on_side
+                last = self._pushes == self.views_per_step and self.rebuild_on_side
                 if last:  # the rebuild's outputs from the compute stream's pool (see _rebuild_beside)
                     _, f_dc, f_rest = self._sh
                     dc, rest = torch.empty_like(f_dc), torch.empty_like(f_rest)
@@ -523,7 +649,7 @@ class GradAllReduce:
                 work = self._launch(ready, lambda: dist.all_gather_into_tensor(out, rec, group=self.group,
                                                                                async_op=True))
             self._gathers.append((out, world, work))
-            if len(self._gathers) == self.views_per_step and rec.is_cuda:
+            if self._pushes == self.views_per_step and rec.is_cuda:
                 self._rebuild_beside()
         else:
             if write is not None:
@@ -613,14 +739,6 @@ class GradAllReduce:
         self._rebuild_into(dc, rest)
         self._install_sh(dc, rest)
 
-    def _split(self, flat, idx):
-        out, off = [], 0
-        for i in idx:
-            n = self._reduced[i].numel()
-            out.append(flat[off:off + n])
-            off += n
-        return out
-
     def remove_hooks(self) -> None:
         for h in self._hooks:
             h.remove()
@@ -676,6 +794,7 @@ class GradAllReduce:
         of the backward, or packed and reduced here when it was not: flat mode, a
         parameter swap, fewer backwards than announced), then the SH gradients from
         the gathered colour gradients (SH exchange on).  Returns the bucket."""
+        self._check_flag()  # an earlier step's flags (the device is past them)
         if self._stale() and not self._early:
             # the model's tensors were replaced since the hooks were bound (densify /
             # prune): their gradients go through the bucket here, and the hooks move
@@ -697,23 +816,22 @@ class GradAllReduce:
             torch.cuda.current_stream(sh_out[0].device).wait_event(sh_out[2])
         if self._work is not None:
             self._work.wait()
-        if self._extra is not None:
-            self._extra[2].wait()
         self._end("exchange_wait")
+        self._copy_flag()
         if sh_out is not None:
             self._install_sh(sh_out[0], sh_out[1])
-        if self._early:  # the views become the leaves' .grad again, plus what came after the start
-            extra = dict(zip(self._extra[0], self._split(self._extra[1], self._extra[0]))) if self._extra else {}
-            for i, (p, v) in enumerate(zip(self._reduced, self._views)):
-                if i in extra:
-                    v.add_(extra[i].view_as(v))
+        if self._early:  # the views become the leaves' .grad again
+            for p, v in zip(self._reduced, self._views):
                 p.grad = v
         self._tstats["timed_calls"] += int(self._timed_now())
         self._tstats["calls"] += 1
         self._early = False
         self._gather_done = None
-        self._extra = None
         self._work = None
+        self._pushes = 0
+        self._rast_seen = False
+        if self._mode == "probe":
+            self._late_local = False  # the probe's own flag was sent with its bucket
         # the grads keep the storage; the next step reuses it only if they were let go
         self._bucket_cache = (self._bucket, self._views) if self._views is not None else None
         self._bucket = self._views = None

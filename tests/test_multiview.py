@@ -918,11 +918,17 @@ def _all_writer_worker(rank, world, port, out, views_per_step):
     torch.manual_seed(0)
     xyz, opacity = (torch.randn(s, requires_grad=True) for s in ((7, 3), (7, 1)))
     ar = GradAllReduce([xyz, opacity], views_per_step=views_per_step)
-    _AllWriter.started = []
-    for v in range(views_per_step):
-        _AllWriter.apply(xyz, opacity, float(rank + 1) * (v + 1)).backward()
-    started = list(_AllWriter.started)
-    ar()
+    probe = []
+    for step in range(2):  # the first step probes the loss graph (no early start)
+        for p in (xyz, opacity):
+            p.grad = None
+        _AllWriter.started = []
+        for v in range(views_per_step):
+            _AllWriter.apply(xyz, opacity, float(rank + 1) * (v + 1)).backward()
+        started = list(_AllWriter.started)
+        probe.append(ar._mode)
+        ar()
+    started = (started, probe)
     out[rank] = ([p.grad.clone() for p in (xyz, opacity)], [p.detach().clone() for p in (xyz, opacity)], started)
     ar.remove_hooks()
     dist.destroy_process_group()
@@ -939,62 +945,186 @@ def test_bucket_started_by_the_rasterizer_gloo_world2(views_per_step):
         res = dict(out)
     (g0, p, s0), (g1, _, s1) = res[0], res[1]
     expect = [(0, 0)] * (views_per_step - 1) + [(0, 1)]
-    assert s0 == s1 == expect
+    assert s0 == s1 == (expect, ["probe", "early"])
     wsum = sum(float(r + 1) * (v + 1) for r in (0, 1) for v in range(views_per_step))
     for a, b, x in zip(g0, g1, p):
         assert torch.equal(a, b)
         torch.testing.assert_close(a, 2 * wsum * x, rtol=1e-6, atol=1e-6)
 
 
-def _late_path_worker(rank, world, port, out, views_per_step):
+def _late_path_worker(rank, world, port, out, views_per_step, only_rank0):
     _init(rank, world, port)
     from multiview import GradAllReduce
 
     torch.manual_seed(0)
     xyz, opacity = (torch.randn(s, requires_grad=True) for s in ((7, 3), (7, 1)))
     ar = GradAllReduce([xyz, opacity], views_per_step=views_per_step)
-    _AllWriter.started = []
     c = 0.5 * (rank + 1)
-    for v in range(views_per_step):
-        # a regulariser on a reduced leaf, formed before the render: AccumulateGrad(opacity)
-        # waits for both paths, so it runs AFTER the writer started the bucket's all-reduce
-        reg = c * (opacity * opacity).sum()
-        (reg + _AllWriter.apply(xyz, opacity, float(rank + 1) * (v + 1))).backward()
-    started = list(_AllWriter.started)
-    # the late contribution landed in a tensor of its own, not in the bucket the
-    # collective was reading (the leaves' .grad were cleared at the early start)
-    bucket = ar._bucket
-    late_apart = opacity.grad is not None and not (
-        bucket.data_ptr() <= opacity.grad.data_ptr() < bucket.data_ptr() + bucket.numel() * 4)
-    flat = ar()
-    views_ok = all(flat.data_ptr() <= p.grad.data_ptr() < flat.data_ptr() + flat.numel() * 4 for p in (xyz, opacity))
-    out[rank] = ([p.grad.clone() for p in (xyz, opacity)], [p.detach().clone() for p in (xyz, opacity)], started,
-                 views_ok and late_apart)
+    res = []
+    for step in range(3):
+        for p in (xyz, opacity):
+            p.grad = None
+        _AllWriter.started = []
+        for v in range(views_per_step):
+            w = _AllWriter.apply(xyz, opacity, float(rank + 1) * (v + 1))
+            if only_rank0 and rank != 0:
+                w.backward()
+                continue
+            # a regulariser on a reduced leaf, formed before the render: AccumulateGrad(opacity)
+            # waits for both paths, so it runs AFTER the writer's backward
+            (c * (opacity * opacity).sum() + w).backward()
+        mode = ar._mode
+        ar()
+        res.append((mode, list(_AllWriter.started), [p.grad.clone() for p in (xyz, opacity)]))
+    out[rank] = (res, [p.detach().clone() for p in (xyz, opacity)])
     ar.remove_hooks()
     dist.destroy_process_group()
 
 
+@pytest.mark.timeout(180)
 @pytest.mark.parametrize("views_per_step", [1, 2])
-def test_late_gradient_path_after_early_start_gloo_world2(views_per_step):
-    """once the rasterizer has started the bucket's all-reduce, a
-    gradient that another loss term sends into a reduced leaf later in the same
-    backward must neither race with the collective nor be left out of it: it is
-    reduced on its own and added, and every rank ends with the full sum, bit-identical,
-    every .grad a view of the bucket again."""
+@pytest.mark.parametrize("only_rank0", [False, True])
+def test_late_gradient_path_gloo_world2(views_per_step, only_rank0):
+    """VERDICT r5 #6 / ADVICE r4-r5: another loss term on a reduced leaf, whose
+    gradient reaches it after the rasterizer's backward — on both ranks, or on rank 0
+    only.  The first step probes the graph (no early start); its summed flags put
+    every rank in "late" mode, so no all-reduce starts before the backward is done,
+    every rank issues the same collectives, and every step's gradients are the full
+    sums, bit-identical on both ranks."""
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_late_path_worker, args=(2, port, out, views_per_step), nprocs=2, join=True)
+        mp.spawn(_late_path_worker, args=(2, port, out, views_per_step, only_rank0), nprocs=2, join=True)
         res = dict(out)
-    (g0, p, s0, v0), (g1, _, s1, v1) = res[0], res[1]
-    assert s0 == s1 == [(0, 0)] * (views_per_step - 1) + [(0, 1)]  # the early start did happen
-    assert v0 and v1
+    (r0, p), (r1, _) = res[0], res[1]
     wsum = sum(float(r + 1) * (v + 1) for r in (0, 1) for v in range(views_per_step))
-    creg = 2 * views_per_step * (0.5 + 1.0)
+    creg = 2 * views_per_step * (0.5 if only_rank0 else 0.5 + 1.0)
+    for step in range(3):
+        (m0, s0, g0), (m1, s1, g1) = r0[step], r1[step]
+        assert m0 == m1 == ("probe" if step == 0 else "late")
+        assert all(b == 0 for _, b in s0 + s1)  # no early start, on any step
+        for a, b in zip(g0, g1):
+            assert torch.equal(a, b)
+        torch.testing.assert_close(g0[0], 2 * wsum * p[0], rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(g0[1], (2 * wsum + creg) * p[1], rtol=1e-6, atol=1e-6)
+
+
+def _graph_change_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    xyz, opacity = (torch.randn(s, requires_grad=True) for s in ((7, 3), (7, 1)))
+    ar = GradAllReduce([xyz, opacity])
+    grads, raised = [], None
+    for step in range(40):
+        for p in (xyz, opacity):
+            p.grad = None
+        try:
+            w = _AllWriter.apply(xyz, opacity, float(rank + 1))
+            if rank == 0 and step >= 3:  # the loss graph changes on one rank after early starts began
+                w = w + (opacity * opacity).sum()
+            w.backward()
+            ar()
+        except RuntimeError as e:
+            raised = (step, str(e))
+            break
+        grads.append([p.grad.clone() for p in (xyz, opacity)])
+    out[rank] = (grads, raised)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_late_gradient_after_early_start_raises_on_every_rank_gloo_world2():
+    """A gradient path that appears on one rank only after early starts began: it is
+    left out on that rank (the replicas stay bit-identical), and every rank raises the
+    same RuntimeError at the same step — no rank issues a collective the other does
+    not, so nothing hangs (the spawn runs under a timeout)."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_graph_change_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    (g0, e0), (g1, e1) = res[0], res[1]
+    assert e0 is not None and e1 is not None and e0[0] == e1[0], (e0, e1)
+    assert "after the bucket's all-reduce had started" in e0[1]
+    assert len(g0) == len(g1) == e0[0]
     for a, b in zip(g0, g1):
-        assert torch.equal(a, b)
-    torch.testing.assert_close(g0[0], 2 * wsum * p[0], rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(g0[1], (2 * wsum + creg) * p[1], rtol=1e-6, atol=1e-6)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
+class _MaybeWriter(torch.autograd.Function):
+    """The rasterizer's contract in full: leaves it gets bucket views for are written
+    there (and reported with rasterizer_done); the others get their gradients back
+    through autograd."""
+
+    @staticmethod
+    def forward(ctx, xyz, opacity, w):
+        ctx.save_for_backward(xyz, opacity)
+        ctx.w = w
+        return (w * (xyz * xyz).sum() + w * (opacity * opacity).sum()).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        import diff_gaussian_rasterization as dgr
+
+        xyz, opacity = ctx.saved_tensors
+        ex = dgr._exchange
+        views = ex.leaf_bucket({"xyz": (xyz,), "opacity": (opacity,)})
+        back = []
+        for name, leaf in (("xyz", xyz), ("opacity", opacity)):
+            val = 2 * ctx.w * leaf.detach() * g
+            if name not in views:
+                back.append(val)
+                continue
+            v = views[name][0]
+            if leaf.grad is None:
+                v.copy_(val)
+                leaf.grad = v
+            else:
+                v.add_(val)
+            back.append(None)
+        if views:
+            ex.rasterizer_done(views)
+        return back[0], back[1], None
+
+
+def _two_calls_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from multiview import GradAllReduce
+
+    torch.manual_seed(0)
+    xyz, opacity = (torch.randn(s, requires_grad=True) for s in ((7, 3), (7, 1)))
+    ar = GradAllReduce([xyz, opacity])
+    res = []
+    for step in range(3):
+        for p in (xyz, opacity):
+            p.grad = None
+        # two rasterizer calls in one backward (ADVICE r5): the second finds no bucket
+        # once the first started the all-reduce, so the graph probe keeps early starts off
+        (_MaybeWriter.apply(xyz, opacity, float(rank + 1)) + _MaybeWriter.apply(xyz, opacity, 2.0)).backward()
+        mode = ar._mode
+        ar()
+        res.append((mode, [p.grad.clone() for p in (xyz, opacity)]))
+    out[rank] = (res, [p.detach().clone() for p in (xyz, opacity)])
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_two_rasterizer_calls_in_one_backward_gloo_world2():
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_two_calls_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    (r0, p), (r1, _) = res[0], res[1]
+    wsum = (1.0 + 2.0) + 2 * 2.0
+    assert [r[0] for r in r0] == [r[0] for r in r1] == ["probe", "late", "late"]
+    for step in range(3):
+        for a, b, x in zip(r0[step][1], r1[step][1], p):
+            assert torch.equal(a, b)
+            torch.testing.assert_close(a, 2 * wsum * x, rtol=1e-6, atol=1e-6)
 
 
 def _reuse_worker(rank, world, port, out):
