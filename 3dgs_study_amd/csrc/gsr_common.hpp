@@ -116,9 +116,21 @@ __host__ __device__ inline int pre_blocks(int P) { return (P + PRE_THREADS - 1) 
 // footprints' row spans by tile row in blocks of RSA_GAUSS ranks, pass B their
 // tiles by column in blocks of RSB_SPANS spans of one row.  Each workgroup expands
 // and scatters its items in rounds of RS_THREADS * ITEMS.
+#ifndef GSR_RSA_GAUSS
+#define GSR_RSA_GAUSS 512
+#endif
+#ifndef GSR_RSA_ITEMS
+#define GSR_RSA_ITEMS 8
+#endif
+#ifndef GSR_RSB_SPANS
+#define GSR_RSB_SPANS 1024
+#endif
+#ifndef GSR_RSB_ITEMS
+#define GSR_RSB_ITEMS 16
+#endif
 constexpr int RS_THREADS = 256;
-constexpr int RSA_GAUSS = 512, RSA_ITEMS = 8;
-constexpr int RSB_SPANS = 1024, RSB_ITEMS = 16;
+constexpr int RSA_GAUSS = GSR_RSA_GAUSS, RSA_ITEMS = GSR_RSA_ITEMS;
+constexpr int RSB_SPANS = GSR_RSB_SPANS, RSB_ITEMS = GSR_RSB_ITEMS;
 static_assert(RS_THREADS == RADIX, "one thread per digit in the per-block digit loops");
 static_assert(RG_THREADS % RSA_GAUSS == 0, "rank_gather_kernel counts whole A blocks");
 __host__ __device__ inline bool rowspan_grid(int W, int H) {
@@ -242,6 +254,8 @@ struct BinningLayout {
     size_t hist;    // uint32 [RADIX][radix_blocks(cap, tsort_items(cap)) + RADIX] (+ RADIX: segment-aligned blocks);
                     // row-span pass B: [RADIX][rsb_blocks_max(cap, gy)] column counts per block
     size_t hist_stride;  // row-span pass B's block stride in hist (rsb_blocks_max)
+    size_t rs_btab;      // uint4 [rsb_blocks_max] row-span pass B's blocks: {first span, row | spans << 16,
+                         // the row's first block, the next row's first block} (the count kernel writes it)
     size_t totals;  // uint32 [RADIX]
     size_t totals1; // uint32 [RADIX] the first tile pass's digit totals (the second pass's segments)
     size_t seg_table; // uint32 [2][RADIX + 1] the second pass's segment table: first block, first item
@@ -275,6 +289,7 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t cap, int W, int 
     L.totals1 = take((size_t)RADIX * 4);
     L.seg_table = take((size_t)2 * (RADIX + 1) * 4);
     L.off[GSR_BIN_ROWSPAN] = L.seg_table;
+    L.rs_btab = take(L.hist_stride * 16);
     L.qmask_stride = n / 64 + (size_t)grid_dims(W, H).tiles + 2;
     L.qmask = take(4 * L.qmask_stride * 8);
     L.bytes = o;

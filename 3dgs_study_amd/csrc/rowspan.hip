@@ -49,6 +49,13 @@
 namespace gsr {
 
 constexpr int RS_WAVES = RS_THREADS / 64;
+constexpr int RS_COUNT_GRID = 2048;  // rowspan_b_count_kernel's grid at most (256 CUs x 8)
+#ifndef GSR_RSB_WAVES
+#define GSR_RSB_WAVES 4
+#endif
+#ifndef GSR_RSA_WAVES
+#define GSR_RSA_WAVES 4
+#endif
 constexpr int RSA_ROUND = RS_THREADS * RSA_ITEMS, RSB_ROUND = RS_THREADS * RSB_ITEMS;
 constexpr int RSA_PER = RSA_GAUSS / RS_THREADS;  // Gaussians per thread
 constexpr int RSB_PER = RSB_SPANS / RS_THREADS;  // spans per thread
@@ -71,6 +78,7 @@ struct RowSpanArgs {
     uint32_t *bhist;         // [RADIX][nBmax] column counts per block -> block offsets (the scan)
     const uint32_t *btot;    // [RADIX] instances per column
     int nBmax;
+    uint4 *btab;             // [nBmax] pass B's block table (rowspan_b_count_kernel)
     uint32_t *point_list;
     uint2 *ranges;           // [T] (zeroed by preprocess; empty tiles stay (0, 0))
 };
@@ -164,7 +172,7 @@ __device__ __forceinline__ void write_b_segments(const RowSpanArgs &a, uint32_t 
 
 // Pass A: the spans of RSA_GAUSS consecutive ranks, scattered by tile row.
 template <int NB>
-__global__ void __launch_bounds__(RS_THREADS) rowspan_a_kernel(RowSpanArgs a) {
+__global__ void __launch_bounds__(RS_THREADS, GSR_RSA_WAVES) rowspan_a_kernel(RowSpanArgs a) {
     __shared__ uint8_t dig[RSA_ROUND];
     __shared__ uint2 pay[RSA_ROUND];
     __shared__ uint32_t cnt[RS_WAVES][RADIX];
@@ -172,23 +180,30 @@ __global__ void __launch_bounds__(RS_THREADS) rowspan_a_kernel(RowSpanArgs a) {
     if (!spec_ok(a.g)) return;
     const uint32_t blk = radix_block(a.nA);
     const uint32_t t = threadIdx.x;
-    if (blk == 0) write_b_segments(a, wsum);
-    {  // where this block's spans of each row start: the rows before, the blocks before
-        const uint32_t tot = (int)t < a.gy ? a.atot[t] : 0u;
-        uint32_t all;
-        const uint32_t row0 = block_inclusive_scan<RS_THREADS>(tot, wsum, &all) - tot;
-        gbase[t] = row0 + ((int)t < a.gy ? a.ahist[(size_t)t * a.nA + blk] : 0u);
-        run[t] = 0u;
-    }
-    // this thread's Gaussians: ranks r0 + RSA_PER t + j, their spans' place in the block
+    // every load first (no barrier between them): this thread's Gaussians, ranks
+    // r0 + RSA_PER t + j, and row t's totals
     const int r0 = (int)blk * RSA_GAUSS + (int)t * RSA_PER;
-    Foot f[RSA_PER];
-    uint32_t id[RSA_PER], pre[RSA_PER], my = 0;
+    uint4 q[RSA_PER];
+    uint32_t id[RSA_PER];
 #pragma unroll
     for (int j = 0; j < RSA_PER; j++) {
         const int r = r0 + j;
-        f[j] = foot_of(r < a.P ? a.rects[r] : make_uint4(0u, 0u, 0u, 0u));
+        q[j] = r < a.P ? a.rects[r] : make_uint4(0u, 0u, 0u, 0u);
         id[j] = r < a.P ? a.order[r] : 0u;
+    }
+    const uint32_t tot = (int)t < a.gy ? a.atot[t] : 0u;
+    const uint32_t before = (int)t < a.gy ? a.ahist[(size_t)t * a.nA + blk] : 0u;
+    if (blk == 0) write_b_segments(a, wsum);
+    {  // where this block's spans of each row start: the rows before, the blocks before
+        uint32_t all;
+        gbase[t] = block_inclusive_scan<RS_THREADS>(tot, wsum, &all) - tot + before;
+        run[t] = 0u;
+    }
+    Foot f[RSA_PER];
+    uint32_t pre[RSA_PER], my = 0;
+#pragma unroll
+    for (int j = 0; j < RSA_PER; j++) {
+        f[j] = foot_of(q[j]);
         pre[j] = my;
         my += foot_spans(f[j]);
     }
@@ -219,75 +234,83 @@ __global__ void __launch_bounds__(RS_THREADS) rowspan_a_kernel(RowSpanArgs a) {
     }
 }
 
-// Pass-B block b: its row and span range (seg written by pass A's block 0), or
-// false beyond the device's block count.
-struct BBlock {
-    uint32_t b, row, s0, s1, first, next, nB;
-};
-__device__ __forceinline__ bool b_block(const RowSpanArgs &a, uint32_t *sfb, uint32_t *sfs, BBlock *bb) {
+// Pass B's block table entry: {first span, row | spans << 16, the row's first
+// block, the next row's first block} (the count kernel writes it, from the segment
+// table of pass A's block 0; rowspan_b_kernel reads it)
+__device__ __forceinline__ uint32_t bt_row(uint4 e) { return e.y & 0xffffu; }
+__device__ __forceinline__ uint32_t bt_end(uint4 e) { return e.x + (e.y >> 16); }
+
+// Pass B's counts: per block, the instances of each column (difference array),
+// and the block's table entry.  A grid-stride loop over the device's block count
+// (the grid is sized by the capacity, which bounds it: most of a fixed-size grid
+// sized that way would find no block).
+__global__ void __launch_bounds__(RS_THREADS) rowspan_b_count_kernel(RowSpanArgs a) {
+    __shared__ uint32_t sfb[RADIX + 1], sfs[RADIX + 1], h[RADIX + 1], wsum[RS_WAVES];
+    if (!spec_ok(a.g)) return;
     const uint32_t nB = min(a.seg[RADIX], (uint32_t)a.nBmax);
-    uint32_t b;
-    if (!radix_block_of(nB, &b)) return false;
+    // XCD-contiguous: workgroup w of XCD x takes blocks x * per + w + k * grid
+    const uint32_t per = gridDim.x >> 3, b0 = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (b0 >= nB) return;
     sfb[threadIdx.x] = a.seg[threadIdx.x];
     sfs[threadIdx.x] = a.seg[RADIX + 1 + threadIdx.x];
     if (threadIdx.x == 0) {
         sfb[RADIX] = nB;
         sfs[RADIX] = a.seg[2 * RADIX + 1];
     }
-    __syncthreads();
-    uint32_t r = 0;  // the last row whose first block is <= b (sfb is non-decreasing, sfb[0] = 0)
+    for (uint32_t b = b0; b < nB; b += gridDim.x) {
+        h[threadIdx.x] = 0u;
+        if (threadIdx.x == 0) h[RADIX] = 0u;
+        __syncthreads();
+        uint32_t r = 0;  // the last row whose first block is <= b (sfb is non-decreasing, sfb[0] = 0)
 #pragma unroll
-    for (uint32_t step = RADIX / 2; step >= 1; step >>= 1)
-        if (sfb[r + step] <= b) r += step;
-    bb->b = b;
-    bb->row = r;
-    bb->first = sfb[r];
-    bb->next = sfb[r + 1];
-    bb->s0 = sfs[r] + (b - sfb[r]) * RSB_SPANS;
-    bb->s1 = min(bb->s0 + RSB_SPANS, sfs[r + 1]);
-    bb->nB = nB;
-    return true;
-}
-
-// Pass B's counts: per block, the instances of each column (difference array).
-__global__ void __launch_bounds__(RS_THREADS) rowspan_b_count_kernel(RowSpanArgs a) {
-    __shared__ uint32_t sfb[RADIX + 1], sfs[RADIX + 1], h[RADIX + 1], wsum[RS_WAVES];
-    if (!spec_ok(a.g)) return;
-    h[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) h[RADIX] = 0u;
-    BBlock bb;
-    if (!b_block(a, sfb, sfs, &bb)) return;
-    for (uint32_t s = bb.s0 + threadIdx.x; s < bb.s1; s += RS_THREADS) {
-        const uint32_t x = a.span_x[s];
-        atomicAdd(&h[x & 0xffffu], 1u);
-        atomicAdd(&h[x >> 16], ~0u);  // - 1
+        for (uint32_t step = RADIX / 2; step >= 1; step >>= 1)
+            if (sfb[r + step] <= b) r += step;
+        const uint32_t s0 = sfs[r] + (b - sfb[r]) * RSB_SPANS, s1 = min(s0 + RSB_SPANS, sfs[r + 1]);
+        if (threadIdx.x == 0) a.btab[b] = make_uint4(s0, r | ((s1 - s0) << 16), sfb[r], sfb[r + 1]);
+        for (uint32_t s = s0 + threadIdx.x; s < s1; s += RS_THREADS) {
+            const uint32_t x = a.span_x[s];
+            atomicAdd(&h[x & 0xffffu], 1u);
+            atomicAdd(&h[x >> 16], ~0u);  // - 1
+        }
+        __syncthreads();
+        uint32_t tot;
+        const uint32_t c = block_inclusive_scan<RS_THREADS>(h[threadIdx.x], wsum, &tot);
+        if ((int)threadIdx.x < a.gx) a.bhist[(size_t)threadIdx.x * a.nBmax + b] = c;
     }
-    __syncthreads();
-    uint32_t tot;
-    const uint32_t c = block_inclusive_scan<RS_THREADS>(h[threadIdx.x], wsum, &tot);
-    if ((int)threadIdx.x < a.gx) a.bhist[(size_t)threadIdx.x * a.nBmax + bb.b] = c;
 }
 
 // Pass B: the tiles of the block's spans, their ids scattered by column into
 // point_list; the row's first block writes the row's tile ranges.
 template <int NB>
-__global__ void __launch_bounds__(RS_THREADS) rowspan_b_kernel(RowSpanArgs a) {
+__global__ void __launch_bounds__(RS_THREADS, GSR_RSB_WAVES) rowspan_b_kernel(RowSpanArgs a) {
     __shared__ uint8_t dig[RSB_ROUND];
     __shared__ uint32_t pay[RSB_ROUND];
     __shared__ uint32_t cnt[RS_WAVES][RADIX];
-    __shared__ uint32_t gbase[RADIX], run[RADIX], gsh[RADIX], sfb[RADIX + 1], sfs[RADIX + 1], wsum[RS_WAVES];
+    __shared__ uint32_t gbase[RADIX], run[RADIX], gsh[RADIX], wsum[RS_WAVES];
     if (!spec_ok(a.g)) return;
-    BBlock bb;
-    if (!b_block(a, sfb, sfs, &bb)) return;
+    const uint32_t nB = min(a.seg[RADIX], (uint32_t)a.nBmax);
+    uint32_t b;
+    if (!radix_block_of(nB, &b)) return;
+    const uint4 e = a.btab[b];
+    const uint32_t row = bt_row(e), s0 = e.x, s1 = bt_end(e), first = e.z, next = e.w;
     const uint32_t t = threadIdx.x;
+    // every load first: this thread's spans s0 + RSB_PER t + j, and column t's counts —
+    // h0 = its instances in the blocks before the row, h1 = ... before the next row,
+    // hb = ... before this block (the scanned counts)
+    const uint32_t sb = s0 + t * RSB_PER;
+    uint32_t x[RSB_PER], id[RSB_PER];
+#pragma unroll
+    for (int j = 0; j < RSB_PER; j++) {
+        const uint32_t s = sb + j;
+        x[j] = s < s1 ? a.span_x[s] : 0u;
+        id[j] = s < s1 ? a.span_id[s] : 0u;
+    }
+    const bool col = (int)t < a.gx;
+    const size_t rowc = (size_t)t * a.nBmax;
+    const uint32_t h0 = col ? a.bhist[rowc + first] : 0u;
+    const uint32_t h1 = col ? (next < nB ? a.bhist[rowc + next] : a.btot[t]) : 0u;
+    const uint32_t hb = col ? a.bhist[rowc + b] : 0u;
     {
-        // column t of this row: h0 = its instances in the blocks before the row, h1 =
-        // ... before the next row, hb = ... before this block (the scanned counts)
-        const bool col = (int)t < a.gx;
-        const size_t rowc = (size_t)t * a.nBmax;
-        const uint32_t h0 = col ? a.bhist[rowc + bb.first] : 0u;
-        const uint32_t h1 = col ? (bb.next < bb.nB ? a.bhist[rowc + bb.next] : a.btot[t]) : 0u;
-        const uint32_t hb = col ? a.bhist[rowc + bb.b] : 0u;
         uint32_t row0;
         block_inclusive_scan<RS_THREADS>(h0, wsum, &row0);  // instances of the rows before
         const uint32_t n = h1 - h0;
@@ -295,16 +318,11 @@ __global__ void __launch_bounds__(RS_THREADS) rowspan_b_kernel(RowSpanArgs a) {
         const uint32_t cs = row0 + block_inclusive_scan<RS_THREADS>(n, wsum, &rowtot) - n;
         gbase[t] = cs + (hb - h0);
         run[t] = 0u;
-        if (bb.b == bb.first && col) a.ranges[(size_t)bb.row * a.gx + t] = n ? make_uint2(cs, cs + n) : make_uint2(0u, 0u);
+        if (b == first && col) a.ranges[(size_t)row * a.gx + t] = n ? make_uint2(cs, cs + n) : make_uint2(0u, 0u);
     }
-    // this thread's spans: s0 + RSB_PER t + j
-    const uint32_t sb = bb.s0 + t * RSB_PER;
-    uint32_t x[RSB_PER], id[RSB_PER], pre[RSB_PER], my = 0;
+    uint32_t pre[RSB_PER], my = 0;
 #pragma unroll
     for (int j = 0; j < RSB_PER; j++) {
-        const uint32_t s = sb + j;
-        x[j] = s < bb.s1 ? a.span_x[s] : 0u;
-        id[j] = s < bb.s1 ? a.span_id[s] : 0u;
         pre[j] = my;
         my += (x[j] >> 16) - (x[j] & 0xffffu);
     }
@@ -315,13 +333,13 @@ __global__ void __launch_bounds__(RS_THREADS) rowspan_b_kernel(RowSpanArgs a) {
         const uint32_t n = min((uint32_t)RSB_ROUND, total - o);
 #pragma unroll
         for (int j = 0; j < RSB_PER; j++) {
-            const uint32_t first = mine + pre[j], xa = x[j] & 0xffffu, xb = x[j] >> 16;
+            const uint32_t fi = mine + pre[j], xa = x[j] & 0xffffu, xb = x[j] >> 16;
             // the span's tiles inside [o, o + n) of the block's sequence
-            const uint32_t lo = first < o ? o - first : 0u;
-            const uint32_t hi = min(xb - xa, o + n > first ? o + n - first : 0u);
+            const uint32_t lo = fi < o ? o - fi : 0u;
+            const uint32_t hi = min(xb - xa, o + n > fi ? o + n - fi : 0u);
             for (uint32_t k = lo; k < hi; k++) {
-                dig[first + k - o] = (uint8_t)(xa + k);
-                pay[first + k - o] = id[j];
+                dig[fi + k - o] = (uint8_t)(xa + k);
+                pay[fi + k - o] = id[j];
             }
         }
         __syncthreads();
@@ -355,6 +373,7 @@ static RowSpanArgs rowspan_args(int P, int W, int H, void *geom, void *binning, 
     a.bhist = at<uint32_t>(binning, B.hist);
     a.btot = at<const uint32_t>(binning, B.totals);
     a.nBmax = (int)B.hist_stride;
+    a.btab = at<uint4>(binning, B.rs_btab);
     a.point_list = at<uint32_t>(binning, B.off[GSR_BIN_POINT_LIST]);
     a.ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
     return a;
@@ -376,7 +395,9 @@ hipError_t launch_rowspan_b(int P, int W, int H, void *geom, void *binning, int6
                             hipStream_t s) {
     RowSpanArgs a = rowspan_args(P, W, H, geom, binning, cap, g);
     const dim3 grid(a.nBmax), block(RS_THREADS);
-    hipLaunchKernelGGL(rowspan_b_count_kernel, grid, block, 0, s, a);
+    // the count kernel loops: 8 workgroups per CU at most, a multiple of the 8 XCDs
+    const int cgrid = (int)(min(a.nBmax, RS_COUNT_GRID) + 7) & ~7;
+    hipLaunchKernelGGL(rowspan_b_count_kernel, dim3(cgrid), block, 0, s, a);
     if (hipError_t e = launch_count_scan(a.bhist, a.nBmax, a.seg + RADIX, const_cast<uint32_t *>(a.btot), a.gx, g, s))
         return e;
     switch (nb_class(a.gx)) {

@@ -52,20 +52,56 @@ def render_metric(cfg_name: str) -> str:
     return f"render frames/sec (fwd-only) + Mpix/sec, {c['W']}x{c['H']}, {c['P']} Gaussians, SH{c['sh_degree']}"
 
 
-def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, M: int) -> float:
-    """Bytes a launch must move at minimum (SURVEY.md §8d per-unit figures)."""
+def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, M: int, backward: bool = True,
+                      S: int = None) -> float:
+    """Bytes a launch of a stage must move at minimum, for the form the library runs
+    (SURVEY.md §8d's per-unit figures, with this library's own data flow where it
+    differs from upstream's).  backward: the unit has a backward (preprocess then
+    also stores the SH direction Jacobian, 9 floats per Gaussian, which
+    preprocess_bwd reads instead of the 192-B SH row).  S: the footprint's row spans
+    (the row-span binning; None = the LSD sort's upstream-shaped
+    figures)."""
     T = ((W + 15) // 16) * ((H + 15) // 16)
     HW = W * H
-    return {
-        "preprocess": P * (44 + 12 * M) + P * 75.0,          # means/scale/rot/opacity/SH in; geometry out
+    jac = 36 if backward and M > 1 else 0
+    out = {
+        # means/scale/rot/opacity/SH in; depth, means2D, 48-B splat record, clamp bits,
+        # tiles_touched, 16-B rect record, radii out (+ the Jacobian)
+        "preprocess": P * (44 + 12 * M) + P * (85.0 + jac),
         "scan": P * 8.0,
         "depth_sort": P * 16.0,                               # depths + tiles_touched in, order + offsets out
         "duplicate": P * 20.0 + I * 8.0,                      # duplicateWithKeys: per-G read, (tile, id) out
         "tile_sort": I * 16.0 + I * 4.0 + T * 8.0,            # one read + write of 8-B pairs; ranges
         "render_fwd": I * 40.0 + T * 16.0 + HW * 20.0,
         "render_bwd": I * 40.0 + HW * 20.0 + T * 8.0 + P * 44.0,
-        "preprocess_bwd": P * (92.0 + 147 + 24 * M),
-    }.get(stage, 0.0)
+        # reads: means3D 12, scales 12, rotations 16, opacity 4, radii 4, the accumulator's
+        # 9 sums 36, the SH direction Jacobian 36 (or the 12M-B SH row without it), clamp
+        # bits 1; writes: dmeans3D 12, dscales 12, drot 16, dopacity 4, dsh 12M
+        "preprocess_bwd": P * (85.0 + (36 if jac else 12 * M) + 44 + 12 * M),
+    }
+    if S is not None:  # the row-span binning
+        out["scan"] = P * 36.0                                 # order 4 + rects 16 (gathered) in, 16 out
+        out["duplicate"] = P * 20.0 + S * 8.0                  # rank-ordered rects + ids in, spans out
+        out["tile_sort"] = S * 12.0 + I * 4.0 + T * 8.0        # span columns (count), spans (scatter); ids, ranges
+    return out.get(stage, 0.0)
+
+
+def stage_model_fracs(per_stage: dict, P: int, I: int, W: int, H: int, M: int, backward: bool = True,
+                      S: int = None) -> dict:
+    """Each stage's model bytes / its measured mean launch time / peak (a stage whose
+    model would need more than the peak has a model that over-credits it: VERDICT r5)."""
+    out = {}
+    for k, v in per_stage.items():
+        ms = v[0] if isinstance(v, tuple) else v
+        b = algorithmic_bytes(k, P, I, W, H, M, backward, S)
+        if ms and b:
+            out[k] = round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    return out
+
+
+def model_over_peak(fracs: dict) -> list:
+    """Stages whose model bytes exceed what the measured time allows at peak."""
+    return sorted(k for k, f in fracs.items() if f > 1.0)
 
 
 def iter_bytes(P: int, I: int, W: int, H: int, M: int, backward: bool = True) -> float:
@@ -322,6 +358,7 @@ def main():
         out = one_step()
     torch.cuda.synchronize()
     I = num_rendered_seen()  # the instances of this rank's view (the byte model)
+    S = _C.last_spans(W, H)  # its row spans (the row-span binning's byte model), None with the LSD sort
     if world > 1:
         dist.barrier()
     # Stage split (HIP events on the launch stream around every rasterizer stage,
@@ -384,9 +421,10 @@ def main():
         steps = args.steps
         value = world * steps / elapsed
         dom_ms = dom_live[0] / dom_live[1] if dom_live[1] else 0.0
-        ab = algorithmic_bytes(dom, P, I, W, H, M)
+        ab = algorithmic_bytes(dom, P, I, W, H, M, True, S)
         achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         traffic = pmc_traffic(dom)
+        fracs = stage_model_fracs(per_stage, P, I, W, H, M, True, S)
         coll = "RCCL" if backend == "nccl" else backend
         line = {
             # BASELINE.json's headline metric at C; the other backward configs name their own shape
@@ -420,6 +458,9 @@ def main():
             "mpix_per_s": round(value * W * H / 1e6, 2),
             "stages_ms": {k: round(v[0], 4) for k, v in per_stage.items()},
             "stages_source": STAGES_SOURCE[args.stage_events],
+            # each stage's byte model (algorithmic_bytes) over its measured time, against 8 TB/s,
+            # and any stage whose model would need more than the peak (none expected)
+            "stage_hbm_frac": fracs, "model_over_peak": model_over_peak(fracs), "row_spans": S,
             # the rasterizer's own stages per step, and §8(d)'s bytes per unit at the
             # measured I against 8 TB/s (the north_star's iteration-level roofline)
             "raster_ms": raster_ms(per_stage),
@@ -553,6 +594,7 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
         for _ in range(max(warmup, 1)):
             one_step()
         I = num_rendered_seen()
+        S = _C.last_spans(cam.image_width, cam.image_height)
         per, _ = stage_split(one_step, steps)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -567,6 +609,7 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
             "iter_hbm_frac_measured": measured_frac("unit_" + mode, steps / dt),
             "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps, "num_rendered": I,
             "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "stages_source": STAGES_SOURCE["split"],
+            "model_over_peak": model_over_peak(stage_model_fracs(per, P, I, W, H, M, True, S)),
             "raster_ms": raster_ms(per), "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
             "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * steps / dt / 1e9 / HBM_PEAK_GBS, 4)}
 
@@ -614,6 +657,7 @@ def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, l
     §8(d)'s iteration roofline, and the host's share (ms_per_step against the
     rasterizer's own device time, raster_ms)."""
     import torch
+    from diff_gaussian_rasterization import _C
 
     import synthetic
     import train_step
@@ -636,6 +680,7 @@ def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, l
         step()
     torch.cuda.synchronize()
     I = num_rendered_seen()
+    S = _C.last_spans(W, H)
     per, _ = stage_split(step, steps)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -655,7 +700,9 @@ def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, l
             "config": {"workload": f"{cfg_name}: {WORKLOADS[cfg_name]}", "gaussians": P, "width": W, "height": H,
                        "sh_degree": deg, "num_rendered": I, "glue": GLUE_NOTE[glue]},
             "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "raster_ms": rms,
+            "model_over_peak": model_over_peak(stage_model_fracs(per, P, I, W, H, M, True, S)),
             "host_ms_per_step": round(1e3 * host / steps, 4),
+            "host_ms_per_step_vs_ms_per_step": round(1e3 * host / steps / ms, 3),
             "ms_per_step_vs_raster_ms": round(ms / rms, 3) if rms else None,
             "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
             "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * steps / dt / 1e9 / HBM_PEAK_GBS, 4)}
@@ -759,6 +806,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
         for _ in range(max(warmup, 1)):
             render(cam, g, bg)
         I = num_rendered_seen()
+        S = _C.last_spans(W, H)
         # the largest stage by measured time, from a steady-state block of its own
         per, dom = stage_split(lambda: render(cam, g, bg), steps)
         _C.timing_enable([dom])  # only the dominant stage inside the timed region
@@ -773,7 +821,8 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
         _C.timing_enable(False)
         _C.timing_sample(1)
     dom_ms = live[0] / live[1]
-    ab = algorithmic_bytes(dom, P, I, W, H, M)
+    ab = algorithmic_bytes(dom, P, I, W, H, M, False, S)
+    fracs = stage_model_fracs(per, P, I, W, H, M, False, S)
     achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     fps = steps / dt
     sfx = "" if _C.get_footprint() == "tight" else "_" + _C.get_footprint()
@@ -784,6 +833,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
                    "sh_degree": deg, "footprint": _C.get_footprint(), "num_rendered": I, "glue": GLUE_NOTE[glue]},
         "stages_ms": {k: round(v[0], 4) for k, v in per.items()},
         "stages_source": STAGES_SOURCE["split"],
+        "stage_hbm_frac": fracs, "model_over_peak": model_over_peak(fracs), "row_spans": S,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      # PMC bytes of this workload's own pass: keyed by config and footprint
@@ -791,8 +841,8 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
                      "traffic": pmc_traffic(f"{dom}_{cfg_name}{sfx}"),
                      "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(dom_ms, 4)},
     }
-    fwd_bytes = sum(algorithmic_bytes(k, P, I, W, H, M) for k in
-                    ("preprocess", "depth_sort", "duplicate", "tile_sort", "render_fwd"))
+    fwd_bytes = sum(algorithmic_bytes(k, P, I, W, H, M, False, S) for k in
+                    ("preprocess", "scan", "depth_sort", "duplicate", "tile_sort", "render_fwd"))
     res["forward_algorithmic_bytes"] = fwd_bytes
     res["forward_hbm_frac"] = round(fwd_bytes * fps / 1e9 / HBM_PEAK_GBS, 4)
     res["raster_ms"] = raster_ms(per)
