@@ -54,7 +54,7 @@ constexpr int RS_COUNT_GRID = 2048;  // rowspan_b_count_kernel's grid at most (2
 #define GSR_RSB_WAVES 4
 #endif
 #ifndef GSR_RSA_WAVES
-#define GSR_RSA_WAVES 4
+#define GSR_RSA_WAVES 6
 #endif
 constexpr int RSA_ROUND = RS_THREADS * RSA_ITEMS, RSB_ROUND = RS_THREADS * RSB_ITEMS;
 constexpr int RSA_PER = RSA_GAUSS / RS_THREADS;  // Gaussians per thread
@@ -280,7 +280,11 @@ __global__ void __launch_bounds__(RS_THREADS) rowspan_b_count_kernel(RowSpanArgs
 }
 
 // Pass B: the tiles of the block's spans, their ids scattered by column into
-// point_list; the row's first block writes the row's tile ranges.
+// point_list; the row's first block writes the row's tile ranges.  One block per
+// workgroup (a grid-stride loop over the blocks measured 52 -> 58 us at config C:
+// the dispatcher's fresh workgroups overlap each other's load chains better); the
+// grid is sized by the capacity and the workgroups beyond the device's block count
+// exit at once.
 template <int NB>
 __global__ void __launch_bounds__(RS_THREADS, GSR_RSB_WAVES) rowspan_b_kernel(RowSpanArgs a) {
     __shared__ uint8_t dig[RSB_ROUND];
@@ -394,16 +398,17 @@ hipError_t launch_rowspan_a(int P, int W, int H, void *geom, void *binning, int6
 hipError_t launch_rowspan_b(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g,
                             hipStream_t s) {
     RowSpanArgs a = rowspan_args(P, W, H, geom, binning, cap, g);
-    const dim3 grid(a.nBmax), block(RS_THREADS);
+    const dim3 block(RS_THREADS);
     // the count kernel loops: 8 workgroups per CU at most, a multiple of the 8 XCDs
     const int cgrid = (int)(min(a.nBmax, RS_COUNT_GRID) + 7) & ~7;
     hipLaunchKernelGGL(rowspan_b_count_kernel, dim3(cgrid), block, 0, s, a);
     if (hipError_t e = launch_count_scan(a.bhist, a.nBmax, a.seg + RADIX, const_cast<uint32_t *>(a.btot), a.gx, g, s))
         return e;
+    const dim3 bgrid(a.nBmax);
     switch (nb_class(a.gx)) {
-        case 6: hipLaunchKernelGGL(rowspan_b_kernel<6>, grid, block, 0, s, a); break;
-        case 7: hipLaunchKernelGGL(rowspan_b_kernel<7>, grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL(rowspan_b_kernel<8>, grid, block, 0, s, a); break;
+        case 6: hipLaunchKernelGGL(rowspan_b_kernel<6>, bgrid, block, 0, s, a); break;
+        case 7: hipLaunchKernelGGL(rowspan_b_kernel<7>, bgrid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL(rowspan_b_kernel<8>, bgrid, block, 0, s, a); break;
     }
     return hipGetLastError();
 }

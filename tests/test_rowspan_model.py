@@ -20,7 +20,7 @@ import pytest
 
 from helpers import activated, case
 
-RSA_GAUSS, RSB_SPANS = 512, 1024
+RSA_GAUSS, RSB_SPANS = 256, 1024
 
 
 def excl(v):
