@@ -79,5 +79,12 @@ def test_bench_single_gpu_line_fields():
     assert b["config"]["gaussians"] == 100_000 and b["config"]["width"] == b["config"]["height"] == 800
     assert b["value"] > 0 and b["raster_ms"] > 0 and b["iter_hbm_frac"] > 0
     assert set(b["stages_ms"]) >= {"preprocess", "render_fwd", "render_bwd", "preprocess_bwd"}
-    e = d["config_E_render_rect"]
-    assert e["config"]["footprint"] == "rect" and "iter_hbm_frac_measured" in e
+    # (3-step splits are noisy: the model check's presence here, its values in test_bench_model)
+    assert isinstance(b["model_over_peak"], list) and 0 < b["host_ms_per_step_vs_ms_per_step"]
+    # the default footprint is upstream's rect; the tight lines sit beside it
+    assert d["config"]["footprint"] == "rect" and d["config"]["binning"] == "rowspan"
+    assert d["footprint_tight"]["footprint"] == "tight" and isinstance(d["footprint_tight"]["model_over_peak"], list)
+    assert isinstance(d["model_over_peak"], list) and d["row_spans"] > 0 and set(d["stage_hbm_frac"]) >= {"render_bwd"}
+    e = d["config_E_render"]
+    assert e["config"]["footprint"] == "rect" and "iter_hbm_frac_measured" in e and "model_over_peak" in e
+    assert d["config_E_render_tight"]["config"]["footprint"] == "tight"
