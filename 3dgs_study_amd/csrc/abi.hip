@@ -94,18 +94,25 @@ bool l1sign_has(const void *img, const float *image, const float *gt) {
 // the tile grid allows it (at most 256 x 256 tiles), 1 = the LSD tile sort of
 // binning.hip everywhere.  The form of each geom buffer's last preprocess is
 // recorded, so its render uses the rank gather's matching outputs.
+// With the rect footprint the row-span binning also has the depth sort carry each
+// Gaussian's rect word beside its id (RS_CARRY; binning.hip), so nothing gathers the
+// rects in rank order.
+enum BinForm { BIN_LSD = 0, BIN_ROWSPAN = 1, BIN_ROWSPAN_CARRY = 2 };
 std::atomic<int> g_binning_mode{0};
-std::unordered_map<const void *, bool> g_rowspan;
-bool rowspan_wanted(const gsr_inputs *in) { return g_binning_mode.load() == 0 && rowspan_grid(in->W, in->H); }
-void rowspan_set(const void *geom, bool on) {
+std::unordered_map<const void *, int> g_rowspan;
+int binform_wanted(const gsr_inputs *in) {
+    if (g_binning_mode.load() != 0 || !rowspan_grid(in->W, in->H)) return BIN_LSD;
+    return in->footprint == GSR_FOOTPRINT_RECT ? BIN_ROWSPAN_CARRY : BIN_ROWSPAN;
+}
+void binform_set(const void *geom, int form) {
     std::lock_guard<std::mutex> lk(g_prep_mu);
     if (g_rowspan.size() > 4096) g_rowspan.clear();
-    g_rowspan[geom] = on;
+    g_rowspan[geom] = form;
 }
-bool rowspan_get(const void *geom, const gsr_inputs *in) {
+int binform_get(const void *geom, const gsr_inputs *in) {
     std::lock_guard<std::mutex> lk(g_prep_mu);
     const auto it = g_rowspan.find(geom);
-    return it == g_rowspan.end() ? rowspan_wanted(in) : it->second;
+    return it == g_rowspan.end() ? binform_wanted(in) : it->second;
 }
 // the num_rendered read-back's event (per host thread, like g_pinned): timing off
 // and no system-scope fence — the pinned words are written with system-scope stores
@@ -301,8 +308,9 @@ static int ensure_pinned() {
 // queued, not waited for.  passes: the depth passes queued (3, or 4 up front).
 static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int passes, hipStream_t s, bool dbg) {
     prepared_set(geom, false);  // preprocess resets the device's flag words too
-    const bool rowspan = rowspan_wanted(in);
-    rowspan_set(geom, rowspan);
+    const int form = binform_wanted(in);
+    binform_set(geom, form);
+    const bool rowspan = form != BIN_LSD, carry = form == BIN_ROWSPAN_CARRY;
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
     g_pinned[CTRL_DSORT_PASSES] = 0;
@@ -314,7 +322,7 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
     if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s,
                             [&] {
                                 return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom,
-                                                         passes, g_pinned, s);
+                                                         passes, g_pinned, carry, s);
                             }),
                       "depth sort", dbg, s))
         return rc;
@@ -323,7 +331,7 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
     // tiles_touched, in depth order), queued before the host waits: the device stays
     // busy (with three passes queued it returns at once if the keys need four)
     return step(timed(GSR_STAGE_SCAN, s,
-                      [&] { return launch_rank_gather(in->P, in->W, in->H, geom, passes == 3, rowspan, s); }),
+                      [&] { return launch_rank_gather(in->P, in->W, in->H, geom, passes == 3, rowspan, carry, s); }),
                 "rank gather", dbg, s);
 }
 
@@ -342,13 +350,17 @@ static int finish_preprocess(const gsr_inputs *in, void *geom, int passes, hipSt
         // the keys span more than 2^24: the fourth pass, then the rank gather the
         // queued one skipped (rank_gather_kernel returns at once on a four-pass sort)
         if (int rc = step(timed(GSR_STAGE_DEPTH_SORT | TIMED_MORE, s,
-                                [&] { return launch_depth_sort_fourth(in->P, in->W, in->H, geom, s); }),
+                                [&] {
+                                    return launch_depth_sort_fourth(in->P, in->W, in->H, geom,
+                                                                    binform_get(geom, in) == BIN_ROWSPAN_CARRY, s);
+                                }),
                           "depth sort (fourth pass)", dbg, s))
             return rc;
         if (int rc = step(timed(GSR_STAGE_SCAN | TIMED_MORE, s,
                                 [&] {
-                                    return launch_rank_gather(in->P, in->W, in->H, geom, false,
-                                                              rowspan_get(geom, in), s);
+                                    const int f = binform_get(geom, in);
+                                    return launch_rank_gather(in->P, in->W, in->H, geom, false, f != BIN_LSD,
+                                                              f == BIN_ROWSPAN_CARRY, s);
                                 }),
                           "rank gather", dbg, s))
             return rc;
@@ -390,10 +402,14 @@ static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t
                         uint8_t *visible_out, hipStream_t s, bool dbg) {
     const size_t npix = (size_t)3 * in->W * in->H;
     float *l1_part = gt ? at<float>(img, img_layout(in->W, in->H).l1_part) : nullptr;
-    if (n > 0 && rowspan_get(geom, in)) {
+    const int form = binform_get(geom, in);
+    if (n > 0 && form != BIN_LSD) {
         // row-span binning: pass A (spans by tile row), pass B (tiles by column)
         if (int rc = step(timed(GSR_STAGE_DUPLICATE, s,
-                                [&] { return launch_rowspan_a(in->P, in->W, in->H, geom, binning, cap, g, s); }),
+                                [&] {
+                                    return launch_rowspan_a(in->P, in->W, in->H, geom, binning, cap, g,
+                                                            form == BIN_ROWSPAN_CARRY, s);
+                                }),
                           "row spans", dbg, s))
             return rc;
         if (int rc = step(timed(GSR_STAGE_TILE_SORT, s,

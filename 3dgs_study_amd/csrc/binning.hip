@@ -106,6 +106,13 @@ struct RadixPass {
     // then the hist stride and *nb_dev (<= NB) the blocks to scan; the scan does
     // nothing unless the speculative guard holds
     const uint32_t *nb_dev;
+    // depth sort with the rect footprint's words carried beside the ids (the
+    // row-span binning, gsr_spans.hpp rect_word): the first pass packs them from
+    // the rects (rin), the later ones move them (win -> wout; the last pass into
+    // wout_final, in rank order).  NULL otherwise (a downsweep without carry).
+    const uint4 *rin;
+    const uint32_t *win;
+    uint32_t *wout, *wout_final;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
@@ -333,7 +340,7 @@ hipError_t launch_count_scan(uint32_t *hist, int NB, const uint32_t *nb_dev, uin
     return hipGetLastError();
 }
 
-template <int ITEMS, int MODE>
+template <int ITEMS, int MODE, bool CARRY = false>
 __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a) {
     constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
     constexpr int SEG = MODE == RXM_UNPACK ? RADIX + 1 : 1;
@@ -345,12 +352,13 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     __shared__ uint32_t wsum[RX_WAVES];
     __shared__ uint32_t sfb[SEG], sst[SEG];
     // RXM_UNPACK stages the packed words alone (the value is in the word)
-    __shared__ uint32_t stage_k[TILE_N], stage_v[MODE == RXM_UNPACK ? 1 : TILE_N];
+    __shared__ uint32_t stage_k[TILE_N], stage_v[MODE == RXM_UNPACK ? 1 : TILE_N], stage_w[CARRY ? TILE_N : 1];
     if (pass_skipped(a)) return;
     // three-pass depth sort: the third pass is the last one
     const bool final3 = a.role == RX_DEPTH_THIRD && a.ctrl[DCTRL_PASSES] == 3;
     uint32_t *const kout = final3 ? nullptr : a.kout;
     uint32_t *const vout = final3 ? a.vout_final : a.vout;
+    uint32_t *const wout = final3 ? a.wout_final : a.wout;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t blk = radix_block(a.NB);
     const uint2 span = block_span<TILE_N, MODE>(a, blk, sfb, sst, wsum);
@@ -414,7 +422,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         }
         __syncthreads();
     }
-    uint32_t kk[ITEMS], vv[MODE == RXM_UNPACK ? 1 : ITEMS], rk[ITEMS];
+    uint32_t kk[ITEMS], vv[MODE == RXM_UNPACK ? 1 : ITEMS], rk[ITEMS], ww[CARRY ? ITEMS : 1];
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
         const uint32_t idx = base + 64u * r;
@@ -424,6 +432,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         else
             kk[r] = ok ? load_key(a, idx) : 0u;
         if constexpr (MODE != RXM_UNPACK) vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
+        if constexpr (CARRY) ww[r] = ok ? (a.win ? a.win[idx] : rect_word(a.rin[idx])) : 0u;
     }
     {
         if (!grouped) {
@@ -491,6 +500,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
             const uint32_t p = cnt[w][d] + rk[r];
             stage_k[p] = kk[r];
             if constexpr (MODE != RXM_UNPACK) stage_v[p] = vv[r];
+            if constexpr (CARRY) stage_w[p] = ww[r];
         }
     }
     __syncthreads();
@@ -508,6 +518,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
             const uint32_t v = stage_v[i];
             if (kout) kout[pos] = k;
             vout[pos] = v;
+            if constexpr (CARRY) wout[pos] = stage_w[i];
         }
     }
     if constexpr (MODE == RXM_UNPACK) {
@@ -538,7 +549,10 @@ static hipError_t radix_pass(const RadixPass &a, hipStream_t s, bool counted = f
     if (!a.sup)  // grouped depth passes: each downsweep block sums its own prefix
         hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(a.pub_sums ? RADIX + 2 : a.minmax ? RADIX + 1 : RADIX),
                            dim3(DSCAN_THREADS), 0, s, a);
-    hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
+    if (MODE == RXM_KV && (a.wout || a.wout_final))
+        hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, RXM_KV, true>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
+    else
+        hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
     return hipGetLastError();
 }
 
@@ -583,9 +597,13 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t lo, uint32_t hi, uint32
 // so no scan launch sits between this kernel and the emission.
 // Row-span binning (rs_gy > 0, rowspan.hip) instead: the spans of each pass-A
 // block (RSA_GAUSS ranks) per tile row, rs_ahist[row][block] (one LDS add per span).
+// With the words carried through the depth sort (rwords: the rect footprint in rank
+// order, gsr_spans.hpp rect_word) the row counts read those, coalesced, and nothing
+// is gathered or written beside them.
 __global__ void __launch_bounds__(RG_THREADS)
     rank_gather_kernel(const uint32_t *order, const uint4 *rects, int P, uint4 *rects_ranked, uint32_t *local,
-                       uint32_t *super, const uint32_t *dsort_ctrl, uint32_t *rs_ahist, int rs_nA, int rs_gy) {
+                       uint32_t *super, const uint32_t *dsort_ctrl, uint32_t *rs_ahist, int rs_nA, int rs_gy,
+                       const uint32_t *rwords) {
     constexpr int AB = RG_THREADS * RG_RANKS / RSA_GAUSS;  // pass-A blocks per workgroup
     __shared__ uint32_t wsum[RG_RANKS][RG_THREADS / 64];
     __shared__ uint32_t rows[AB][RADIX];
@@ -596,21 +614,29 @@ __global__ void __launch_bounds__(RG_THREADS)
     if (rs_gy)
         for (int i = threadIdx.x; i < AB * RADIX; i += RG_THREADS) (&rows[0][0])[i] = 0u;
     uint32_t id[RG_RANKS];
-#pragma unroll
-    for (int k = 0; k < RG_RANKS; k++) {
-        const int r = r0 + k * RG_THREADS;
-        id[k] = r < P ? order[r] : 0u;
-    }
     uint4 q[RG_RANKS];
+    if (rwords) {
 #pragma unroll
-    for (int k = 0; k < RG_RANKS; k++) q[k] = r0 + k * RG_THREADS < P ? rects[id[k]] : make_uint4(0u, 0u, 0u, 0u);
+        for (int k = 0; k < RG_RANKS; k++) {
+            const int r = r0 + k * RG_THREADS;
+            id[k] = r < P ? rwords[r] : 0xffu;  // (the word, not the id)
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < RG_RANKS; k++) {
+            const int r = r0 + k * RG_THREADS;
+            id[k] = r < P ? order[r] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < RG_RANKS; k++) q[k] = r0 + k * RG_THREADS < P ? rects[id[k]] : make_uint4(0u, 0u, 0u, 0u);
+    }
     if (rs_gy) {
         __syncthreads();  // the row counts are zeroed
 #pragma unroll
         for (int k = 0; k < RG_RANKS; k++) {
             const int r = r0 + k * RG_THREADS;
-            if (r < P) rects_ranked[r] = q[k];
-            const Foot f = foot_of(q[k]);
+            if (!rwords && r < P) rects_ranked[r] = q[k];
+            const Foot f = rwords ? foot_of_word(id[k]) : foot_of(q[k]);
             uint32_t *h = rows[(k * RG_THREADS + threadIdx.x) / RSA_GAUSS];
             for (uint32_t y = f.y0; y < f.y1; y++)
                 if (foot_row_kept(f, y - f.y0)) atomicAdd(&h[y], 1u);
@@ -918,7 +944,9 @@ __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) 
 // by the host after its sync when the published pass count needs it, or queued up
 // front (the last forward needed four) as a kernel that returns at once unless the
 // key range needs it.  The order lands in GSR_GEOM_DEPTH_ORDER either way.
-static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
+// carry: the rect footprint's words travel with the ids (rank_gather_kernel and the
+// row-span pass A then read them in rank order: no random gather of the rects)
+static RadixPass depth_pass(int P, int W, int H, void *geom, int p, bool carry) {
     const GeomLayout L = geom_layout(P, W, H);
     RadixPass a = {};
     a.n = (uint32_t)P;
@@ -945,6 +973,15 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
     a.kout = kout[p];
     a.vout = vout[p];
     a.role = role[p];
+    if (carry) {  // words: rects (packed) -> b -> c -> b -> final, like the values
+        uint32_t *wb = at<uint32_t>(geom, L.rs_words), *wc = wb + P, *wf = wb + 2 * (size_t)P;
+        const uint32_t *win[4] = {nullptr, wb, wc, wb};
+        uint32_t *wout[4] = {wb, wc, wb, wf};
+        a.rin = at<const uint4>(geom, L.rects);
+        a.win = win[p];
+        a.wout = wout[p];
+        a.wout_final = wf;
+    }
     a.shift = 8 * p;
     a.nbits = RADIX_BITS;
     a.dmask = RADIX - 1;
@@ -957,7 +994,7 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p) {
 
 template <int ITEMS>
 static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                                   int passes, uint32_t *host_ctrl, hipStream_t s) {
+                                   int passes, uint32_t *host_ctrl, bool carry, hipStream_t s) {
     const GeomLayout L = geom_layout(P, W, H);
     DepthKeyArgs k;
     k.means3D = means3D;
@@ -976,7 +1013,7 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     // passes 4: queued up front (the last forward needed it), returning at once
     // when three suffice
     for (int p = 0; p < passes; p++) {
-        RadixPass a = depth_pass(P, W, H, geom, p);
+        RadixPass a = depth_pass(P, W, H, geom, p, carry);
         if (p == 0) {  // the first digit scan publishes the pass count and num_rendered
             a.host_ctrl = host_ctrl;
             a.pub_sums = at<const uint4>(geom, L.block_sums);
@@ -991,24 +1028,25 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
 }
 
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             int passes, uint32_t *host_ctrl, hipStream_t s) {
+                             int passes, uint32_t *host_ctrl, bool carry, hipStream_t s) {
     if (P <= 0) return hipSuccess;
     return dsort_items(P) == DSORT_ITEMS_BIG
-               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, s)
-               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, s);
+               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, carry, s)
+               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, carry, s);
 }
 
-hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s) {
+hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, bool carry, hipStream_t s) {
     if (P <= 0) return hipSuccess;
-    return dsort_items(P) == DSORT_ITEMS_BIG ? radix_pass<DSORT_ITEMS_BIG>(depth_pass(P, W, H, geom, 3), s)
-                                             : radix_pass<DSORT_ITEMS>(depth_pass(P, W, H, geom, 3), s);
+    return dsort_items(P) == DSORT_ITEMS_BIG ? radix_pass<DSORT_ITEMS_BIG>(depth_pass(P, W, H, geom, 3, carry), s)
+                                             : radix_pass<DSORT_ITEMS>(depth_pass(P, W, H, geom, 3, carry), s);
 }
 
 // After the depth sort: the rects in rank order and the rank-order instance offsets
 // of the emit blocks.
 // rowspan: the row-span binning follows (rowspan.hip): the pass-A row counts
 // instead of the emission offsets, and their per-row scan
-hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, bool rowspan, hipStream_t s) {
+hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, bool rowspan, bool carry,
+                              hipStream_t s) {
     if (P <= 0) return hipSuccess;
     const GeomLayout L = geom_layout(P, W, H);
     const int gy = rowspan ? grid_dims(W, H).gy : 0, nA = rsa_blocks(P);
@@ -1017,7 +1055,7 @@ hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, bo
                        at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]), at<const uint4>(geom, L.rects), P,
                        at<uint4>(geom, L.rects_ranked), at<uint32_t>(geom, L.emit_sums),
                        at<uint32_t>(geom, L.emit_super), require3 ? at<const uint32_t>(geom, L.dsort_ctrl) : nullptr,
-                       ahist, nA, gy);
+                       ahist, nA, gy, rowspan && carry ? at<const uint32_t>(geom, L.rs_words) + 2 * (size_t)P : nullptr);
     if (!rowspan) return hipGetLastError();
     return launch_count_scan(ahist, nA, nullptr, at<uint32_t>(geom, L.rs_atot), gy, SpecGuard{}, s);
 }

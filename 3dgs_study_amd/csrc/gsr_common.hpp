@@ -202,6 +202,8 @@ struct GeomLayout {
     size_t emit_super;    // uint32 [rg_blocks(P)] instances per rank-gather block (RG_SUPER emit blocks)
     size_t rs_ahist;      // uint32 [gy][rsa_blocks(P)] row-span pass A: spans per (tile row, block) -> block offsets
     size_t rs_atot;       // uint32 [RADIX] spans per tile row
+    size_t rs_words;      // uint32 [3][P] the depth sort's carried rect words (two ping-pong arrays, then the
+                          // rank-ordered result); aliases rects_ranked, which that form does not use
     size_t order_cnt;    // uint32 [8][32] backward wave-order bucket counts + the ORDER_FLAGS words (zeroed by preprocess)
     size_t accum;         // float [P][ACCUM_STRIDE] the backward's gradient accumulator (gsr.h GSR_FLAG_PREPARE_BACKWARD)
     size_t shjac;         // float [9][P] d colour / d view direction (GSR_FLAG_PREPARE_BACKWARD with SH colours)
@@ -237,6 +239,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.emit_super = take((size_t)rg_blocks(P) * 4 + 4);
     L.rs_ahist = take(rowspan_grid(W, H) ? (size_t)g.gy * rsa_blocks(P) * 4 : 4);
     L.rs_atot = take((size_t)RADIX * 4);
+    L.rs_words = L.rects_ranked;
     L.order_cnt = take((8 * 32 + 2) * 4);
     L.accum = take((size_t)(P > 0 ? P : 1) * 16 * 4);
     L.shjac = take((size_t)9 * (P > 0 ? P : 1) * 4);

@@ -17,11 +17,14 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 // count says so) or 4 (queued up front; returns at once when three suffice).
 // host_ctrl: the caller's pinned words, which the first digit scan fills with the
 // pass count and num_rendered (after preprocess, in stream order).
+// carry: the rect footprint's words travel with the ids (the row-span binning of the
+// rect footprint; gsr_spans.hpp rect_word)
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             int passes, uint32_t *host_ctrl, hipStream_t s);
-hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, hipStream_t s);
+                             int passes, uint32_t *host_ctrl, bool carry, hipStream_t s);
+hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, bool carry, hipStream_t s);
 // rowspan: the row-span binning follows (pass A's row counts and their scan)
-hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, bool rowspan, hipStream_t s);
+hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, bool rowspan, bool carry,
+                              hipStream_t s);
 hipError_t launch_count_scan(uint32_t *hist, int NB, const uint32_t *nb_dev, uint32_t *totals, int digits,
                              const SpecGuard &g, hipStream_t s);
 // cap: the binning buffer's instance capacity (its layout); g: speculative guard
@@ -35,7 +38,7 @@ hipError_t launch_tile_sort(int P, int W, int H, void *geom, void *binning, int6
 // launch_rank_gather(..., rowspan = true): pass A (spans by tile row), pass B
 // (tiles by column into point_list, and the tile ranges)
 hipError_t launch_rowspan_a(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g,
-                            hipStream_t s);
+                            bool carry, hipStream_t s);
 hipError_t launch_rowspan_b(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g,
                             hipStream_t s);
 hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const void *binning, int64_t I,

@@ -52,4 +52,25 @@ __device__ __forceinline__ uint32_t foot_row_span(const Foot &f, uint32_t k) {
     return xa | (xb << 16);
 }
 
+// The rect footprint's record as one word, for grids of at most 256 x 256 tiles:
+// x0 | (x1 - 1) << 8 | y0 << 16 | (y1 - 1) << 24 (every tile of the rect), 0xff for
+// an empty rect (x0 = 255 > x1 - 1 = 0).  The depth sort carries it beside each
+// Gaussian's id (binning.hip), so the rank-ordered footprints need no random gather.
+__device__ __forceinline__ uint32_t rect_word(uint4 q) {
+    const uint32_t x0 = q.x & 0xffffu, x1 = q.x >> 16, y0 = q.y & 0xffffu, y1 = q.y >> 16;
+    if (x1 <= x0 || y1 <= y0) return 0xffu;
+    return x0 | ((x1 - 1u) << 8) | (y0 << 16) | ((y1 - 1u) << 24);
+}
+__device__ __forceinline__ Foot foot_of_word(uint32_t w) {
+    Foot f;
+    f.x0 = w & 0xffu;
+    f.x1 = ((w >> 8) & 0xffu) + 1u;
+    f.y0 = (w >> 16) & 0xffu;
+    f.y1 = (w >> 24) + 1u;
+    f.m = ~0ull;
+    f.full = true;
+    if (f.x1 <= f.x0) f.y1 = f.y0;  // empty
+    return f;
+}
+
 }  // namespace gsr

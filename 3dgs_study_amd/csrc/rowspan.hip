@@ -66,7 +66,8 @@ struct RowSpanArgs {
     SpecGuard g;
     // pass A
     const uint32_t *order;   // GSR_GEOM_DEPTH_ORDER: id of each rank
-    const uint4 *rects;      // the footprints in rank order (rank_gather_kernel)
+    const uint4 *rects;      // the footprints in rank order (rank_gather_kernel), or NULL: rwords
+    const uint32_t *rwords;  // the rect footprint's words in rank order (carried by the depth sort)
     const uint32_t *ahist;   // [gy][nA] after the scan: spans of row y in the blocks before
     const uint32_t *atot;    // [RADIX] spans per row
     int nA;
@@ -188,7 +189,10 @@ __global__ void __launch_bounds__(RS_THREADS, GSR_RSA_WAVES) rowspan_a_kernel(Ro
 #pragma unroll
     for (int j = 0; j < RSA_PER; j++) {
         const int r = r0 + j;
-        q[j] = r < a.P ? a.rects[r] : make_uint4(0u, 0u, 0u, 0u);
+        if (a.rwords)
+            q[j].x = r < a.P ? a.rwords[r] : 0xffu;
+        else
+            q[j] = r < a.P ? a.rects[r] : make_uint4(0u, 0u, 0u, 0u);
         id[j] = r < a.P ? a.order[r] : 0u;
     }
     const uint32_t tot = (int)t < a.gy ? a.atot[t] : 0u;
@@ -203,7 +207,7 @@ __global__ void __launch_bounds__(RS_THREADS, GSR_RSA_WAVES) rowspan_a_kernel(Ro
     uint32_t pre[RSA_PER], my = 0;
 #pragma unroll
     for (int j = 0; j < RSA_PER; j++) {
-        f[j] = foot_of(q[j]);
+        f[j] = a.rwords ? foot_of_word(q[j].x) : foot_of(q[j]);
         pre[j] = my;
         my += foot_spans(f[j]);
     }
@@ -357,7 +361,8 @@ static int nb_class(int digits) {
     return bits <= 6 ? 6 : bits == 7 ? 7 : 8;
 }
 
-static RowSpanArgs rowspan_args(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g) {
+static RowSpanArgs rowspan_args(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g,
+                                bool carry = false) {
     const GeomLayout L = geom_layout(P, W, H);
     const BinningLayout B = binning_layout(cap, W, H);
     const GridDims gd = grid_dims(W, H);
@@ -367,7 +372,8 @@ static RowSpanArgs rowspan_args(int P, int W, int H, void *geom, void *binning, 
     a.gy = gd.gy;
     a.g = g;
     a.order = at<const uint32_t>(geom, L.off[GSR_GEOM_DEPTH_ORDER]);
-    a.rects = at<const uint4>(geom, L.rects_ranked);
+    a.rects = carry ? nullptr : at<const uint4>(geom, L.rects_ranked);
+    a.rwords = carry ? at<const uint32_t>(geom, L.rs_words) + 2 * (size_t)P : nullptr;
     a.ahist = at<const uint32_t>(geom, L.rs_ahist);
     a.atot = at<const uint32_t>(geom, L.rs_atot);
     a.nA = rsa_blocks(P);
@@ -384,8 +390,8 @@ static RowSpanArgs rowspan_args(int P, int W, int H, void *geom, void *binning, 
 }
 
 hipError_t launch_rowspan_a(int P, int W, int H, void *geom, void *binning, int64_t cap, const SpecGuard &g,
-                            hipStream_t s) {
-    const RowSpanArgs a = rowspan_args(P, W, H, geom, binning, cap, g);
+                            bool carry, hipStream_t s) {
+    const RowSpanArgs a = rowspan_args(P, W, H, geom, binning, cap, g, carry);
     const dim3 grid(a.nA), block(RS_THREADS);
     switch (nb_class(a.gy)) {
         case 6: hipLaunchKernelGGL(rowspan_a_kernel<6>, grid, block, 0, s, a); break;

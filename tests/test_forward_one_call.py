@@ -26,7 +26,7 @@ def _run(cam, g, dev, footprint, cap):
     try:
         H, W = cam.image_height, cam.image_width
         out = run_hip(cam, g, dev, dL=random_dL(H, W), footprint=footprint)
-        out["path"] = dict(_C.last_forward)
+        out["path"] = {k: _C.last_forward.get(k) for k in ("capacity", "num_rendered", "path")}
         return out
     finally:
         _C.capacity_override = prev
