@@ -100,9 +100,12 @@ bool l1sign_has(const void *img, const float *image, const float *gt) {
 enum BinForm { BIN_LSD = 0, BIN_ROWSPAN = 1, BIN_ROWSPAN_CARRY = 2 };
 std::atomic<int> g_binning_mode{0};
 std::unordered_map<const void *, int> g_rowspan;
+#ifndef GSR_RS_CARRY
+#define GSR_RS_CARRY 1  // (0: a timing build whose rect footprint gathers the rects like the tight one)
+#endif
 int binform_wanted(const gsr_inputs *in) {
     if (g_binning_mode.load() != 0 || !rowspan_grid(in->W, in->H)) return BIN_LSD;
-    return in->footprint == GSR_FOOTPRINT_RECT ? BIN_ROWSPAN_CARRY : BIN_ROWSPAN;
+    return in->footprint == GSR_FOOTPRINT_RECT && GSR_RS_CARRY ? BIN_ROWSPAN_CARRY : BIN_ROWSPAN;
 }
 void binform_set(const void *geom, int form) {
     std::lock_guard<std::mutex> lk(g_prep_mu);
@@ -314,7 +317,7 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
     g_pinned[CTRL_DSORT_PASSES] = 0;
-    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, s); }),
+    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, carry, s); }),
                       "preprocess", dbg, s))
         return rc;
     // the sort needs only the view depths; after preprocess, so that its first digit

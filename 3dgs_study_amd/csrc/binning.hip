@@ -973,11 +973,10 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p, bool carry) 
     a.kout = kout[p];
     a.vout = vout[p];
     a.role = role[p];
-    if (carry) {  // words: rects (packed) -> b -> c -> b -> final, like the values
-        uint32_t *wb = at<uint32_t>(geom, L.rs_words), *wc = wb + P, *wf = wb + 2 * (size_t)P;
-        const uint32_t *win[4] = {nullptr, wb, wc, wb};
+    if (carry) {  // words: preprocess's (the fourth array) -> b -> c -> b -> final, like the values
+        uint32_t *wb = at<uint32_t>(geom, L.rs_words), *wc = wb + P, *wf = wb + 2 * (size_t)P, *wp = wb + 3 * (size_t)P;
+        const uint32_t *win[4] = {wp, wb, wc, wb};
         uint32_t *wout[4] = {wb, wc, wb, wf};
-        a.rin = at<const uint4>(geom, L.rects);
         a.win = win[p];
         a.wout = wout[p];
         a.wout_final = wf;

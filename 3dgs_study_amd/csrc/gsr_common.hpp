@@ -202,8 +202,9 @@ struct GeomLayout {
     size_t emit_super;    // uint32 [rg_blocks(P)] instances per rank-gather block (RG_SUPER emit blocks)
     size_t rs_ahist;      // uint32 [gy][rsa_blocks(P)] row-span pass A: spans per (tile row, block) -> block offsets
     size_t rs_atot;       // uint32 [RADIX] spans per tile row
-    size_t rs_words;      // uint32 [3][P] the depth sort's carried rect words (two ping-pong arrays, then the
-                          // rank-ordered result); aliases rects_ranked, which that form does not use
+    size_t rs_words;      // uint32 [4][P] the depth sort's carried rect words (two ping-pong arrays, the
+                          // rank-ordered result, preprocess's output); aliases rects_ranked (16 P bytes),
+                          // which that form does not use
     size_t order_cnt;    // uint32 [8][32] backward wave-order bucket counts + the ORDER_FLAGS words (zeroed by preprocess)
     size_t accum;         // float [P][ACCUM_STRIDE] the backward's gradient accumulator (gsr.h GSR_FLAG_PREPARE_BACKWARD)
     size_t shjac;         // float [9][P] d colour / d view direction (GSR_FLAG_PREPARE_BACKWARD with SH colours)

@@ -8,7 +8,9 @@
 namespace gsr {
 
 // preprocess.hip (num_rendered is published by the depth sort's first digit scan)
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, hipStream_t s);
+// rwords: write each rect as one word into the depth sort's carried-word input
+// (the row-span binning of the rect footprint) instead of the 16-B rect records
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 

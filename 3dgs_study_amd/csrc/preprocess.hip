@@ -15,6 +15,7 @@
 #include "gsr_math.hpp"
 #include "gsr_publish.hpp"
 #include "gsr_rows.hpp"
+#include "gsr_spans.hpp"
 #include "gsr_wave.hpp"
 
 namespace gsr {
@@ -29,6 +30,7 @@ struct PreArgs {
     uint8_t *clamped;
     uint32_t *tiles_touched;
     uint4 *rects;  // tile rect {x0 | x1 << 16, y0 | y1 << 16} + 64-bit tile mask per Gaussian (binning.hip)
+    uint32_t *rwords;  // instead (the row-span binning of the rect footprint): the rect as one word (gsr_spans.hpp)
     uint2 *ranges;           // [T] zeroed here (empty tiles keep (0, 0); binning.hip fills the rest)
     int tiles;
     uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, 0, 0, 0}
@@ -234,7 +236,10 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         if (!radius_out) a.depths[idx] = __uint_as_float(0x7f800000u);
         a.radii[idx] = radius_out;
         a.tiles_touched[idx] = touched;
-        a.rects[idx] = rect_out;
+        if (a.rwords)
+            a.rwords[idx] = rect_word(rect_out);
+        else
+            a.rects[idx] = rect_out;
     }
     // (stores are counted by vmcnt too: issued here, after the geometry, they do not
     // hold up its waits for the per-Gaussian loads)
@@ -304,7 +309,7 @@ __global__ void mark_visible_kernel(int P, const float *means3D, const float *vi
     present[idx] = !(pv.z <= 0.2f);
 }
 
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, hipStream_t s) {
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s) {
     const GeomLayout L = geom_layout(in.P, in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
     PreArgs a;
@@ -319,6 +324,7 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, h
     a.clamped = at<uint8_t>(geom, L.off[GSR_GEOM_CLAMPED]);
     a.tiles_touched = at<uint32_t>(geom, L.off[GSR_GEOM_TILES_TOUCHED]);
     a.rects = at<uint4>(geom, L.rects);
+    a.rwords = rwords ? at<uint32_t>(geom, L.rs_words) + 3 * (size_t)in.P : nullptr;
     a.ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
     a.tiles = g.tiles;
     a.block_sums = at<uint4>(geom, L.block_sums);
