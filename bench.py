@@ -141,6 +141,12 @@ def pmc_traffic(stage: str):
     return float(v) if v is not None else None
 
 
+def pmc_key(cfg_name: str, footprint: str) -> str:
+    """The suffix of a workload's PMC records (tools/round_profile.sh runs one pass per
+    config and footprint): "<stage>_C_rect", "unit_C_rect", ..."""
+    return f"_{cfg_name}_{footprint}"
+
+
 def pmc_unit_bytes(key: str):
     """profiles/pmc_summary.json's measured HBM bytes of one benchmark unit (every gsr
     kernel's per-dispatch bytes x dispatches per unit; tools/pmc_summary.py), or None."""
@@ -423,7 +429,8 @@ def main():
         dom_ms = dom_live[0] / dom_live[1] if dom_live[1] else 0.0
         ab = algorithmic_bytes(dom, P, I, W, H, M, True, S)
         achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-        traffic = pmc_traffic(dom)
+        pkey = pmc_key(args.config, _C.get_footprint())
+        traffic = pmc_traffic(dom + pkey) if args.glue == "fused" else None
         fracs = stage_model_fracs(per_stage, P, I, W, H, M, True, S)
         coll = "RCCL" if backend == "nccl" else backend
         line = {
@@ -468,8 +475,8 @@ def main():
             "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * value / world / 1e9 / HBM_PEAK_GBS, 4),
             # the same with the PMC-measured HBM bytes per unit (profiles/pmc_summary.json,
             # tools/pmc.sh on the default footprint and glue; null for other workloads)
-            "iter_hbm_frac_measured": (measured_frac("unit", value / world)
-                                       if args.config == "C" and args.glue == "fused" else None),
+            "iter_hbm_frac_measured": (measured_frac("unit" + pkey, value / world)
+                                       if args.glue == "fused" else None),
             # host time inside one_step per step (launches, autograd, the one read-back wait)
             "host_ms_per_step": round(1e3 * host / steps, 4),
             "roofline": {
@@ -483,7 +490,7 @@ def main():
                 "algorithmic_bytes_per_launch": ab,
                 "avg_launch_ms": round(dom_ms, 4),
                 # the blend loops are issue-bound, not byte-bound: PMC VALU issue share
-                "valu_issue_frac": pmc_stage(dom).get("valu_issue_frac"),
+                "valu_issue_frac": pmc_stage(dom + pkey).get("valu_issue_frac"),
             },
             **({"exchange": exchange} if exchange is not None else {}),
             "cpu_baseline": None,
@@ -606,7 +613,7 @@ def footprint_rates(one_step, cam, g, bg, steps: int, warmup: int) -> dict:
         set_footprint(prev)
     P, W, H, M = g.xyz.shape[0], cam.image_width, cam.image_height, g.features_rest.shape[1] + 1
     return {"footprint": mode, "value": round(steps / dt, 3), "unit": "train-iters/s",
-            "iter_hbm_frac_measured": measured_frac("unit_" + mode, steps / dt),
+            "iter_hbm_frac_measured": measured_frac("unit" + pmc_key("C", mode), steps / dt),
             "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps, "num_rendered": I,
             "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "stages_source": STAGES_SOURCE["split"],
             "model_over_peak": model_over_peak(stage_model_fracs(per, P, I, W, H, M, True, S)),
@@ -825,7 +832,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
     fracs = stage_model_fracs(per, P, I, W, H, M, False, S)
     achieved = ab / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     fps = steps / dt
-    sfx = "" if _C.get_footprint() == "tight" else "_" + _C.get_footprint()
+    sfx = pmc_key(cfg_name, _C.get_footprint())
     res = {
         "metric": render_metric(cfg_name), "value": round(fps, 3), "unit": "frames/s", "ms_per_frame": round(1e3 * dt / steps, 4),
         "mpix_per_s": round(fps * W * H / 1e6, 2), "steps": steps, "warmup": warmup,
@@ -837,8 +844,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      # PMC bytes of this workload's own pass: keyed by config and footprint
-                     # (the default tight pass is "<stage>_E", upstream's rect "<stage>_E_rect")
-                     "traffic": pmc_traffic(f"{dom}_{cfg_name}{sfx}"),
+                     "traffic": pmc_traffic(f"{dom}{sfx}") if glue == "fused" else None,
                      "algorithmic_bytes_per_launch": ab, "avg_launch_ms": round(dom_ms, 4)},
     }
     fwd_bytes = sum(algorithmic_bytes(k, P, I, W, H, M, False, S) for k in
@@ -848,7 +854,7 @@ def _render_rates(cfg_name: str, dev, steps: int, warmup: int, view: int, glue: 
     res["raster_ms"] = raster_ms(per)
     res["iter_algorithmic_bytes"] = iter_bytes(P, I, W, H, M, backward=False)  # §8(d)'s forward formula
     res["iter_hbm_frac"] = round(res["iter_algorithmic_bytes"] * fps / 1e9 / HBM_PEAK_GBS, 4)
-    res["iter_hbm_frac_measured"] = measured_frac(f"unit_{cfg_name}{sfx}", fps) if glue == "fused" else None
+    res["iter_hbm_frac_measured"] = measured_frac(f"unit{sfx}", fps) if glue == "fused" else None
     del g
     torch.cuda.empty_cache()
     return res

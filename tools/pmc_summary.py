@@ -20,7 +20,7 @@ for f in sorted(glob.glob(str(d / "**" / "*counter_collection.csv"), recursive=T
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 STAGE = {"gsr::preprocess_fwd_kernel": "preprocess", "gsr::render_fwd_kernel": "render_fwd",
          "gsr::render_bwd_kernel": "render_bwd", "gsr::preprocess_bwd_kernel": "preprocess_bwd",
-         "gsr::emit_kernel": "duplicate"}
+         "gsr::emit_kernel": "duplicate", "gsr::bwd_prepare_kernel": "bwd_prepare"}
 summary = {"note": "per-dispatch means; hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE "
                    "counts half of wide streaming reads, MI355X_MICROARCH.md §HBM)", "kernels": {}, "stages": {}}
 for k, cs in sorted(vals.items()):
@@ -78,6 +78,33 @@ def tile_sort_stage(kernels, titems, suffix=""):
 rec = tile_sort_stage(summary["kernels"], "16" if SUFFIX.startswith("_E") else "8")
 if rec:
     summary["stages"]["tile_sort" + SUFFIX] = rec
+
+
+def rowspan_stages(kernels):
+    """The row-span binning (rowspan.hip): duplicate = pass A; tile_sort = pass B's
+    counts + one digit scan + its scatter; scan = the rank gather + one digit scan."""
+    def find(prefix):
+        for k, line in kernels.items():
+            if k.startswith(prefix) and "hbm_bytes_per_launch" in line:
+                return k, line["hbm_bytes_per_launch"]
+        return None, None
+    out = {}
+    ka, a = find("gsr::rowspan_a_kernel")
+    kc, c = find("gsr::rowspan_b_count_kernel")
+    kb, b = find("gsr::rowspan_b_kernel")
+    ks, sc = find("gsr::radix_digit_scan_kernel")
+    kg, g = find("gsr::rank_gather_kernel")
+    if a is not None:
+        out["duplicate"] = {"hbm_bytes_per_launch": a, "kernel": ka}
+    if None not in (c, b, sc):
+        out["tile_sort"] = {"hbm_bytes_per_launch": c + sc + b, "kernel": f"{kc} + {ks} + {kb}"}
+    if None not in (g, sc):
+        out["scan"] = {"hbm_bytes_per_launch": g + sc, "kernel": f"{kg} + {ks}"}
+    return out
+
+
+for st, rec in rowspan_stages(summary["kernels"]).items():
+    summary["stages"][st + SUFFIX] = rec
 # One benchmark unit's measured HBM bytes (bench.py iter_hbm_frac_measured): every
 # gsr kernel's per-dispatch bytes times its dispatches, over the units the run made.
 # The run repeats one unit (tools/pmc.sh: warm-up, stage split and timed steps of
