@@ -8,6 +8,7 @@
 // Python side).  The only host synchronisation is the num_rendered read-back
 // in gsr_forward_preprocess, as upstream.
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -56,21 +57,32 @@ bool prepared_take(const void *geom) {
 // masks' place in it): every forward into a buffer records or forgets it, and a
 // backward finds the masks only for the buffer its forward wrote.  Without a
 // record the backward culls itself (same entries, same pairs).
-std::unordered_map<const void *, int64_t> g_qmask;
-void qmask_set(const void *binning, int64_t cap) {
+// The record also holds the split replay's SEG of that forward (0: no checkpoints).
+std::unordered_map<const void *, std::pair<int64_t, int>> g_qmask;
+void qmask_set(const void *binning, int64_t cap, int seg) {
     std::lock_guard<std::mutex> lk(g_prep_mu);
     if (cap <= 0) {
         g_qmask.erase(binning);
         return;
     }
     if (g_qmask.size() > 4096) g_qmask.clear();
-    g_qmask[binning] = cap;
+    g_qmask[binning] = {cap, seg};
 }
 int64_t qmask_get(const void *binning) {
     std::lock_guard<std::mutex> lk(g_prep_mu);
     const auto it = g_qmask.find(binning);
-    return it == g_qmask.end() ? 0 : it->second;
+    return it == g_qmask.end() ? 0 : it->second.first;
 }
+int split_get(const void *binning) {
+    std::lock_guard<std::mutex> lk(g_prep_mu);
+    const auto it = g_qmask.find(binning);
+    return it == g_qmask.end() ? 0 : it->second.second;
+}
+// Split replay (gsr_split_mode; gsr_common.hpp): -1 automatic SEG, 0 off, > 0 that SEG
+std::atomic<int> g_split_mode{-1};
+// the host's time inside the forward's num_rendered wait (gsr_host_wait_us: the
+// benchmark separates the host's own work per step from its waiting on the device)
+std::atomic<int64_t> g_wait_ns{0};
 // img buffers whose last forward wrote sign(image - gt) beside the L1 loss's partial
 // sums (gsr_forward_render_l1 with GSR_FLAG_PREPARE_BACKWARD), with the image and
 // target it compared: an L1-seeded backward of that pair reads the signs (3 B per
@@ -289,6 +301,21 @@ int gsr_binning_mode(int mode) {
     return mode < 0 ? g_binning_mode.load() : g_binning_mode.exchange(mode);
 }
 
+double gsr_host_wait_us(int reset) {
+    const int64_t ns = reset ? g_wait_ns.exchange(0) : g_wait_ns.load();
+    return (double)ns * 1e-3;
+}
+
+int gsr_split_mode(int mode) {
+    if (mode == -2) return g_split_mode.load();
+    if (mode < -1 || mode > 65536) {
+        fail(GSR_ERR_ARGS, "split mode %d: -1 (automatic), 0 (off), a segment length in list entries, or -2 (query)",
+             mode);
+        return -3;
+    }
+    return g_split_mode.exchange(mode);
+}
+
 const char *gsr_last_error(void) { return g_err.c_str(); }
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 
@@ -343,7 +370,10 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
 // are queued now (*late).
 static int finish_preprocess(const gsr_inputs *in, void *geom, int passes, hipStream_t s, bool dbg, int64_t *I,
                              bool *late) {
-    if (int rc = check_hip(hipEventSynchronize(g_ctrl_ready), "num_rendered read-back")) return rc;
+    const auto w0 = std::chrono::steady_clock::now();
+    const hipError_t we = hipEventSynchronize(g_ctrl_ready);
+    g_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
+    if (int rc = check_hip(we, "num_rendered read-back")) return rc;
     if (g_pinned[CTRL_PREFILTER_ERR])
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     const bool four = g_pinned[CTRL_DSORT_PASSES] != 3u;
@@ -436,15 +466,17 @@ static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t
     const GeomLayout G = geom_layout(in->P, in->W, in->H);
     void *acc = at<void>(geom, G.accum);
     const size_t acc_bytes = (size_t)in->P * ACCUM_STRIDE * sizeof(float);
+    // the split replay's SEG (0: none), for the lists this forward bins into cap
+    const int seg = prep && n > 0 ? split_seg(cap, g_split_mode.load()) : 0;
     if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s,
                             [&] {
                                 return launch_render_fwd(*in, geom, n > 0 ? binning : nullptr, img, out_color,
                                                          prep ? (float *)acc : nullptr, acc_bytes, s,
-                                                         prep && n > 0 ? cap : 0);
+                                                         prep && n > 0 ? cap : 0, seg);
                             }),
                       "render", dbg, s))
         return rc;
-    if (binning) qmask_set(binning, prep && n > 0 ? cap : 0);
+    if (binning) qmask_set(binning, prep && n > 0 ? cap : 0, seg);
     l1sign_set(img, prep && gt ? out_color : nullptr, gt);
     if (!prep) {  // the L1 loss, if asked for, on its own
         prepared_set(geom, false);
@@ -590,7 +622,8 @@ static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void 
             if (int rc = step(timed(GSR_STAGE_RENDER_BWD, s, [&] {
                                   return launch_render_bwd(*in, geom, binning, img, seed ? nullptr : dL_dout_color,
                                                            seed, acc, s, qmask_get(binning),
-                                                           seed && l1sign_has(img, seed->image, seed->gt));
+                                                           seed && l1sign_has(img, seed->image, seed->gt),
+                                                           split_get(binning));
                               }),
                               "render backward", dbg, s))
                 return rc;

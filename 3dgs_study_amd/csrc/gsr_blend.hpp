@@ -225,10 +225,10 @@ __host__ __device__ inline int quad_xcd(int q) { return (q / ORDER_STRIP) & 7; }
 __device__ __forceinline__ int order_bucket(uint32_t work) {  // 16 blended Gaussians per bucket
     return ORDER_NBUCKET - 1 - (int)min(work >> 4, (uint32_t)ORDER_NBUCKET - 1);
 }
-// Workgroup 8 r + x -> XCD x's r-th quadrant in bucket order, or -1 past the end
-// of that XCD's list (all lanes of the wave must be active).
-__device__ __forceinline__ int ordered_quad(const uint32_t *cnt, const uint32_t *qlist, int maxc) {
-    const int lane = threadIdx.x & 63, x = blockIdx.x & 7, rr = blockIdx.x >> 3;
+// Ordered workgroup 8 r + x (blk) -> XCD x's r-th quadrant in bucket order, or -1
+// past the end of that XCD's list (all lanes of the wave must be active).
+__device__ __forceinline__ int ordered_quad(const uint32_t *cnt, const uint32_t *qlist, int maxc, int blk) {
+    const int lane = threadIdx.x & 63, x = blk & 7, rr = blk >> 3;
     const uint32_t c = lane < ORDER_NBUCKET ? cnt[x * ORDER_NBUCKET + lane] : 0u;
     const uint32_t incl = wave_inclusive_scan(c);
     const int b = __builtin_popcountll(__ballot(incl <= (uint32_t)rr));  // buckets wholly before entry rr

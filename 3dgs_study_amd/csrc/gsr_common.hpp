@@ -269,8 +269,59 @@ struct BinningLayout {
     size_t qmask;   // uint64 [4][qmask_stride] per quadrant, per 64-entry chunk of its tile's list: the
                     // entries that reach the quadrant (render_fwd's cull), for render_bwd (qmask_index)
     size_t qmask_stride;
+    // split replay (render_bwd.hip): per checkpoint slot (split_slot), per quadrant and
+    // pixel, the forward's {T, C} before the slot's list position; per split tile (the
+    // slot of its first checkpoint) the final {C, T}; the tile of each slot
+    size_t ckpt;    // float4 [split_slots][4][64]
+    size_t cfin;    // float4 [split_slots][4][64]
+    size_t ctab;    // uint32 [split_slots]
     size_t bytes;
 };
+
+// ---- split replay: the backward of a long tile list in segments (render_bwd.hip)
+// A wave replays its quadrant's list serially, so a tile far longer than the
+// average load per wave slot sets the kernel's time on its own (config B: 743
+// entries against a mean of 125).  The forward stores each pixel's T and colour
+// at every SEG-th list position of a list longer than SEG; the backward then
+// replays segment k ([k SEG, (k + 1) SEG)) of such a list in a wave of its own,
+// starting from that state.  SEG balances the longest segment against the average
+// wave-slot load 4 I / SPLIT_SLOTS (256 CUs x 4 SIMDs x 6 waves); lists are never
+// split when that exceeds SPLIT_MAX (the longest lists then hold a small share of a
+// wave slot's load: config C, E).
+#ifndef GSR_SPLIT_SLOTS
+#define GSR_SPLIT_SLOTS 6144
+#endif
+constexpr int SPLIT_MIN = 128, SPLIT_MAX = 1024;
+constexpr int SPLIT_SLOT_CAP = 4096;  // checkpoint slots at most (8 KB each)
+// checkpoint slots of a binning buffer of capacity cap (every SEG the buffer allows)
+__host__ __device__ inline int64_t split_slots(int64_t cap) {
+    const int64_t s = cap / SPLIT_MIN;
+    return (s < SPLIT_SLOT_CAP ? s : SPLIT_SLOT_CAP) + 2;
+}
+__host__ __device__ inline int64_t pow2_at_least(int64_t v) {
+    int64_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+// the smallest SEG the buffer's slots allow (a power of two: render_fwd tests chunk
+// positions against it with a mask)
+__host__ __device__ inline int split_seg_min(int64_t cap) {
+    const int64_t q = (cap + SPLIT_SLOT_CAP - 1) / SPLIT_SLOT_CAP;
+    return (int)pow2_at_least(q > SPLIT_MIN ? q : SPLIT_MIN);
+}
+// SEG for a forward into capacity cap: mode < 0 automatic, 0 off, > 0 that length
+// (raised to a power of two >= 64 the buffer allows); 0 = no split
+__host__ inline int split_seg(int64_t cap, int mode) {
+    if (mode == 0 || cap <= 0) return 0;
+    int64_t s = pow2_at_least(mode > 0 ? (int64_t)mode : 4 * cap / GSR_SPLIT_SLOTS);
+    if (s < split_seg_min(cap)) s = split_seg_min(cap);
+    if (mode < 0 && s > SPLIT_MAX) return 0;
+    return (int)s;
+}
+// the slot of list position p (= r.x + k SEG, k >= 1, p < r.y) of a sorted list:
+// distinct for every (tile, k) — a later tile's first checkpoint lies more than
+// SEG past an earlier tile's last — and at most cap / SEG
+__host__ __device__ inline uint32_t split_slot(uint32_t p, uint32_t seg) { return p / seg; }
 // The chunk-mask slot of quadrant w's chunk j of tile t (list range r): (r.x >> 6) + t + j
 // is distinct for every (tile, chunk) of a sorted list whose tile ranges follow each
 // other (tile t + 1 starts at r.y: (r.y >> 6) + 1 >= (r.x >> 6) + ceil((r.y - r.x) / 64)),
@@ -298,6 +349,10 @@ __host__ __device__ inline BinningLayout binning_layout(int64_t cap, int W, int 
     L.rs_btab = take(L.hist_stride * 16);
     L.qmask_stride = n / 64 + (size_t)grid_dims(W, H).tiles + 2;
     L.qmask = take(4 * L.qmask_stride * 8);
+    const size_t ns = (size_t)split_slots((int64_t)n);
+    L.ckpt = take(ns * 4 * 64 * 16);
+    L.cfin = take(ns * 4 * 64 * 16);
+    L.ctab = take((ns + 2) * 4);  // (+ 2: render_bwd reads the word of every slot workgroup, an even count)
     L.bytes = o;
     return L;
 }

@@ -49,9 +49,10 @@ hipError_t launch_point_list_keys(int P, int W, int H, const void *geom, const v
 // render_fwd.hip
 // (binning: point_list at offset 0, whatever the buffer's capacity)
 // qmask_cap > 0: record each chunk's cull mask for render_bwd in the binning
-// buffer's qmask region (binning_layout(qmask_cap): the buffer's capacity)
+// buffer's qmask region (binning_layout(qmask_cap): the buffer's capacity), and with
+// seg > 0 the split replay's checkpoints of the lists longer than seg (gsr_common.hpp)
 hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binning, void *img, float *out_color,
-                             float *acc_zero, size_t acc_bytes, hipStream_t s, int64_t qmask_cap = 0);
+                             float *acc_zero, size_t acc_bytes, hipStream_t s, int64_t qmask_cap = 0, int seg = 0);
 
 // render_bwd.hip
 // l1 (forward only, or NULL): the L1 loss mean|l1_x - l1_y| (n = 3 W H) into
@@ -66,7 +67,7 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
 // capacity (launch_render_fwd); the replay then skips the cull
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, const void *img,
                              const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s,
-                             int64_t qmask_cap = 0, bool l1_signs = false);
+                             int64_t qmask_cap = 0, bool l1_signs = false, int seg = 0);
 
 // preprocess_bwd.hip
 struct BwdOutputs {

@@ -59,6 +59,11 @@ struct RenderBwdArgs {
     // the forward's chunk cull masks (render_fwd.hip; binning's qmask region), or NULL
     const uint64_t *qmask;
     size_t qmask_stride;
+    // split replay (gsr_common.hpp; MASKS only): SEG or 0, the checkpoint slots (the
+    // grid's first 4 nslots workgroups: slot b / 4, quadrant b % 4) and regions
+    int seg, nslots;
+    const float *ckpt, *cfin;
+    const uint32_t *ctab;
 };
 __device__ __forceinline__ float l1_sign(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }  // torch.sign
 
@@ -105,8 +110,32 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         a.flags[0] = 1u;                 // ORDER_FILED
         a.flags[1] = 0u;                 // ORDER_FRESH
     }
-    const int quad = ordered_quad(a.order_cnt, a.qlist, a.maxc);
-    if (quad < 0) return;
+    // Split replay (gsr_common.hpp): the grid's first 4 nslots workgroups replay
+    // segment k >= 1 ([k SEG, (k + 1) SEG)) of the split lists, slot by slot (a slot's
+    // tile is validated against this forward's ranges: a stale or unwritten word names
+    // no segment, or the slot's own); the ordered waves replay segment 0 of every
+    // quadrant, i.e. all of an unsplit list.
+    const uint32_t seg = MASKS ? (uint32_t)a.seg : 0u;
+    const int xb = MASKS ? 4 * a.nslots : 0;  // a multiple of 8: the ordered waves keep their XCD
+    int quad = -1;
+    uint32_t s0 = 0;  // the segment's first list position
+    bool segment = false;
+    if constexpr (MASKS) {
+        if ((int)blockIdx.x < xb) {
+            const uint32_t slot = blockIdx.x >> 2, t = a.ctab[slot];
+            if (t >= (uint32_t)a.tiles) return;
+            const uint2 rr = a.ranges[t];
+            const uint32_t k = slot - rr.x / seg;
+            if (slot < rr.x / seg || k == 0u || rr.x + k * seg >= rr.y) return;
+            s0 = k * seg;
+            quad = (int)(4 * t + (blockIdx.x & 3));
+            segment = true;
+        }
+    }
+    if (!segment) {
+        quad = ordered_quad(a.order_cnt, a.qlist, a.maxc, (int)blockIdx.x - xb);
+        if (quad < 0) return;
+    }
     const int tile = (int)(quad >> 2), w = (int)(quad & 3);
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int qx0 = tx * TILE_X + (w & 1) * 8, qy0 = ty * TILE_Y + (w >> 1) * 8;
@@ -143,7 +172,11 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     int end = last_contrib;  // wave max: the first (from the back) entry any pixel replays
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) end = max(end, __shfl_xor(end, o));
-    if (end <= 0) return;
+    // the segment [s0, e): the whole list unless it is split
+    const uint32_t n = r.y - r.x;
+    const uint32_t e = seg && n > seg ? min(s0 + seg, n) : n;
+    end = min(end, (int)e);
+    if (end <= (int)s0) return;
 
     __shared__ QuadChunk stage[BLEND_WAVES];
     QuadChunk &st = stage[0];
@@ -155,6 +188,17 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // so the replay carries its projection D = sum_c accum_rec_c dL/dpix_c (advanced
     // eagerly: after a blended Gaussian it already holds the next Gaussian's value)
     float D = 0.f;
+    // A pixel that blends past the segment's end starts from the forward's state
+    // there: T = T(e), and accum_rec = the colour the entries from e on composite,
+    // relative to T(e): (C_final - C(e)) / T(e) (the forward's checkpoint and final
+    // colour).  Others start as upstream's replay does, from final_T.
+    if (e < n && last_contrib > (int)e) {
+        // planes of 64 floats per (slot, quadrant): {T, C0, C1, C2}, and the final {C0, C1, C2}
+        const float *ck = a.ckpt + ((size_t)split_slot(r.x + e, seg) * 4 + w) * 256 + lane;
+        const float *cf = a.cfin + ((size_t)split_slot(r.x + seg, seg) * 4 + w) * 256 + lane;
+        T = ck[0];
+        D = ((cf[0] - ck[64]) * dpx0 + (cf[64] - ck[128]) * dpx1 + (cf[128] - ck[192]) * dpx2) / T;
+    }
     const uint32_t *list = a.point_list + r.x;
 
     // The role-swapped reduce-scatter below leaves Gaussian a's nine sums in lanes
@@ -363,7 +407,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     // survivor's record instead (one line for all of them).  The one wait per chunk
     // also drains the previous chunk's accumulator atomics, none are waited for
     // inside the Gaussian loop.
-    const int jend = (end - 1) >> 6, e1 = end - 1;
+    const int jend = (end - 1) >> 6, e1 = end - 1, js = (int)(s0 >> 6);
     auto cmask = [&](int j) -> uint64_t { return !MASKS || j < 0 ? ~0ull : qm[j]; };
     auto pick = [&](uint32_t idx, uint64_t m) -> uint32_t {
         if constexpr (!MASKS) return idx;
@@ -384,7 +428,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         C1 = sp[2];
         wait_vmcnt_4();
         replay_chunk(64 * j, A0, B0, C0, mj);
-        if (--j < 0) break;
+        if (--j < js) break;
         idx_b = at_list(j - 2);
         mc = cmask(j - 2);
         sp = a.splats + 3 * (size_t)pick(idx_a, ma);
@@ -393,7 +437,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         C0 = sp[2];
         wait_vmcnt_4();
         replay_chunk(64 * j, A1, B1, C1, mb);
-        if (--j < 0) break;
+        if (--j < js) break;
         mj = ma;
         mb = mc;
     }
@@ -527,7 +571,7 @@ hipError_t launch_bwd_prepare(const gsr_inputs &in, void *geom, const void *img,
 
 hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void *binning, const void *img,
                              const float *dL_dpix, const gsr_l1_seed *l1, float *accum, hipStream_t s,
-                             int64_t qmask_cap, bool l1_signs) {
+                             int64_t qmask_cap, bool l1_signs, int seg) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -555,13 +599,23 @@ hipError_t launch_render_bwd(const gsr_inputs &in, const void *geom, const void 
     a.maxc = order_max_per_xcd(4 * g.tiles);
     a.qmask = nullptr;
     a.qmask_stride = 0;
+    a.seg = a.nslots = 0;
+    a.ckpt = a.cfin = nullptr;
+    a.ctab = nullptr;
     if (qmask_cap > 0) {
         const BinningLayout B = binning_layout(qmask_cap, in.W, in.H);
         a.qmask = at<uint64_t>(binning, B.qmask);
         a.qmask_stride = B.qmask_stride;
+        if (seg > 0) {  // the forward's checkpoints: slots 0 .. cap / seg
+            a.seg = seg;
+            a.nslots = (int)((qmask_cap / seg + 2 + 1) & ~1ll);  // even: 4 nslots workgroups, a multiple of 8
+            a.ckpt = at<float>(binning, B.ckpt);
+            a.cfin = at<float>(binning, B.cfin);
+            a.ctab = at<uint32_t>(binning, B.ctab);
+        }
     }
     if (a.qmask)
-        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);
+        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(4 * a.nslots + 8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);
     else
         hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(8 * a.maxc), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();

@@ -44,6 +44,10 @@ struct RenderFwdArgs {
     // qmask: quadrant w at w * qmask_stride, chunk slot qmask_index), or NULL
     uint64_t *qmask;
     size_t qmask_stride;
+    // split replay (gsr_common.hpp; qmask set): SEG, or 0; the checkpoint regions
+    int seg, seg_log2;
+    float *ckpt, *cfin;  // [slot][quadrant][4 | 3][64]: {T, C} planes; the final C planes
+    uint32_t *ctab;
 };
 
 #ifndef GSR_FWD_GROUP
@@ -57,6 +61,10 @@ static_assert(FWD_GROUP >= 1 && FWD_GROUP <= 3, "QuadChunk holds 64 survivors + 
 // instructions render_bwd uses.  The zero record after the survivors lets the
 // odd count's second Gaussian blend nothing without a mask (render_fwd 145 ->
 // 142 us at C, 374-379 -> 370 us at E).
+// SPLIT: the split replay's checkpoints (gsr_common.hpp) — a separate instantiation,
+// so that the unsplit kernel keeps its 64 VGPRs (8 waves per SIMD; the checkpoint
+// path costs 2-4 more)
+template <bool SPLIT>
 __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(7))) render_fwd_kernel(RenderFwdArgs a) {
     auto zero_slice = [&]() {  // every workgroup its slice of the backward's accumulator
         if (a.zero4) {
@@ -188,10 +196,33 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
         // of being copied (a register copy of an in-flight load would force a full
         // vmcnt drain).  Indices are clamped: every load is unconditional, so the
         // single wait per chunk keeps exactly the 4 prefetch loads in flight.
+        // Split replay (gsr_common.hpp): a list longer than SEG stores each pixel's
+        // state {T, C} before every SEG-th entry (at the chunk's start, ahead of its
+        // prefetch: the one wait per chunk then also covers the stores), and the final
+        // colour once at the end; the backward replays the segments in waves of their
+        // own.  SEG is a power of two, so the test and the slot come from the chunk
+        // position alone (a loop-carried "next checkpoint" lived in a VGPR: render_fwd
+        // 64 -> 68 VGPRs, 8 -> 7 waves per SIMD).
+        const bool split = SPLIT && n > a.seg;
+        const int smask = split ? a.seg - 1 : 0x7fffffff;
+        auto checkpoint = [&](int pos) {
+            const uint32_t slot = (r.x + (uint32_t)pos) >> a.seg_log2;  // split_slot
+            // four planes of 64 floats, a dword store straight from each state register
+            // (the lane offset made here: hoisted, a per-lane address costs the loop registers)
+            uint32_t lo = (uint32_t)lane * 4u;  // bytes: the stores take a scalar base + 32-bit offset
+            asm volatile("" : "+v"(lo));
+            char *ck = reinterpret_cast<char *>(a.ckpt + ((size_t)slot * 4 + w) * 256);
+            *reinterpret_cast<float *>(ck + lo) = T;
+            *reinterpret_cast<float *>(ck + 256 + lo) = C0;
+            *reinterpret_cast<float *>(ck + 512 + lo) = C1;
+            *reinterpret_cast<float *>(ck + 768 + lo) = C2;
+            if (lane == 0) a.ctab[slot] = (uint32_t)tile;  // every quadrant that gets here: the same word
+        };
         const float4 *sp = a.splats + 3 * (size_t)list[min(lane, nm1)];
         float4 A0 = sp[0], B0 = sp[1], C0_ = sp[2], A1, B1, C1_;
         uint32_t idx_a, idx_b = list[min(64 + lane, nm1)];
         for (int pos = 0;;) {
+            if (SPLIT && (pos & smask) == 0 && pos > 0) checkpoint(pos);
             idx_a = list[min(pos + 128 + lane, nm1)];
             sp = a.splats + 3 * (size_t)idx_b;
             A1 = sp[0];
@@ -200,6 +231,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             wait_vmcnt_4();
             if (blend_chunk(pos, A0, B0, C0_)) break;
             if ((pos += 64) >= n) break;
+            if (SPLIT && (pos & smask) == 0 && pos > 0) checkpoint(pos);
             idx_b = list[min(pos + 128 + lane, nm1)];
             sp = a.splats + 3 * (size_t)idx_a;
             A0 = sp[0];
@@ -208,6 +240,12 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
             wait_vmcnt_4();
             if (blend_chunk(pos, A1, B1, C1_)) break;
             if ((pos += 64) >= n) break;
+        }
+        if (split) {
+            float *cf = a.cfin + ((size_t)((r.x + (uint32_t)a.seg) >> a.seg_log2) * 4 + w) * 256;
+            cf[lane] = C0;
+            cf[64 + lane] = C1;
+            cf[128 + lane] = C2;
         }
     }
     // the quadrant's work bucket for the backward's wave order (filed by bwd_prepare_kernel,
@@ -231,7 +269,7 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
 }
 
 hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binning, void *img, float *out_color,
-                             float *acc_zero, size_t acc_bytes, hipStream_t s, int64_t qmask_cap) {
+                             float *acc_zero, size_t acc_bytes, hipStream_t s, int64_t qmask_cap, int seg) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
     const ImgLayout Im = img_layout(in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
@@ -254,12 +292,25 @@ hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binni
     a.l1_ticket = at<uint32_t>(img, Im.l1_ticket);
     a.qmask = nullptr;
     a.qmask_stride = 0;
+    a.seg = a.seg_log2 = 0;
+    a.ckpt = a.cfin = nullptr;
+    a.ctab = nullptr;
     if (binning && qmask_cap > 0) {
         const BinningLayout B = binning_layout(qmask_cap, in.W, in.H);
         a.qmask = at<uint64_t>(const_cast<void *>(binning), B.qmask);
         a.qmask_stride = B.qmask_stride;
+        if (seg > 0) {
+            a.seg = seg;
+            a.seg_log2 = __builtin_ctz((unsigned)seg);
+            a.ckpt = at<float>(const_cast<void *>(binning), B.ckpt);
+            a.cfin = at<float>(const_cast<void *>(binning), B.cfin);
+            a.ctab = at<uint32_t>(const_cast<void *>(binning), B.ctab);
+        }
     }
-    hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
+    if (a.seg)
+        hipLaunchKernelGGL(render_fwd_kernel<true>, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
+    else
+        hipLaunchKernelGGL(render_fwd_kernel<false>, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

@@ -64,7 +64,8 @@ EXPORTED = (
     "gsr_backward_colors", "gsr_sh_record_floats", "gsr_sh_grad_from_colors", "gsr_backward_planar",
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
     "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
-    "gsr_forward_render_l1", "gsr_forward", "gsr_timing_sample", "gsr_binning_mode",
+    "gsr_forward_render_l1", "gsr_forward", "gsr_timing_sample", "gsr_binning_mode", "gsr_split_mode",
+    "gsr_host_wait_us",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -118,6 +119,25 @@ def set_binning_mode(mode: str) -> str:
 
 def get_binning_mode() -> str:
     return {v: k for k, v in BINNING_MODES.items()}[load_library().gsr_binning_mode(-1)]
+
+
+def set_split(seg) -> int:
+    """Split replay of long tile lists in the backward (include/gsr.h gsr_split_mode):
+    -1 automatic (the default), 0 off, or a segment length in list entries.  Returns
+    the previous setting; takes effect at the next forward."""
+    prev = load_library().gsr_split_mode(int(seg))
+    if prev < -1:
+        raise ValueError(load_library().gsr_last_error().decode())
+    return prev
+
+
+def get_split() -> int:
+    return load_library().gsr_split_mode(-2)
+
+
+def host_wait_ms(reset: bool = False) -> float:
+    """Milliseconds the host spent in the forward's num_rendered wait (gsr_host_wait_us)."""
+    return load_library().gsr_host_wait_us(int(bool(reset))) * 1e-3
 
 
 class GsrLeafGrads(ctypes.Structure):
@@ -181,7 +201,7 @@ class GsrAdamSegment(ctypes.Structure):
 
 
 ADAM_MAX_SEGS = 8
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lib = None
 
@@ -248,6 +268,10 @@ def load_library():
     lib.gsr_timing_enable.restype = ctypes.c_int
     lib.gsr_binning_mode.argtypes = [ctypes.c_int]
     lib.gsr_binning_mode.restype = ctypes.c_int
+    lib.gsr_split_mode.argtypes = [ctypes.c_int]
+    lib.gsr_split_mode.restype = ctypes.c_int
+    lib.gsr_host_wait_us.argtypes = [ctypes.c_int]
+    lib.gsr_host_wait_us.restype = ctypes.c_double
     lib.gsr_timing_sample.argtypes = [ctypes.c_int]
     lib.gsr_timing_sample.restype = ctypes.c_int
     lib.gsr_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -277,6 +301,9 @@ def load_library():
     lib.gsr_build_id.restype = ctypes.c_char_p
     if lib.gsr_abi_version() != ABI_VERSION:
         raise ImportError(f"{path}: ABI version {lib.gsr_abi_version()} != {ABI_VERSION}; rebuild")
+    if os.environ.get("GSR_SPLIT"):  # the split replay's setting (set_split), e.g. 0 for A/B timing
+        if lib.gsr_split_mode(int(os.environ["GSR_SPLIT"])) < -1:
+            raise ImportError(f"GSR_SPLIT={os.environ['GSR_SPLIT']!r}: {lib.gsr_last_error().decode()}")
     _lib = lib
     return lib
 

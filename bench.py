@@ -690,6 +690,7 @@ def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, l
     S = _C.last_spans(W, H)
     per, _ = stage_split(step, steps)
     torch.cuda.synchronize()
+    _C.host_wait_ms(reset=True)
     t0 = time.perf_counter()
     host = 0.0
     for _ in range(steps):
@@ -698,6 +699,7 @@ def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, l
         host += time.perf_counter() - h0
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    wait = _C.host_wait_ms() * 1e-3
     del g, params
     ms = 1e3 * dt / steps
     rms = raster_ms(per)
@@ -710,6 +712,10 @@ def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, l
             "model_over_peak": model_over_peak(stage_model_fracs(per, P, I, W, H, M, True, S)),
             "host_ms_per_step": round(1e3 * host / steps, 4),
             "host_ms_per_step_vs_ms_per_step": round(1e3 * host / steps / ms, 3),
+            # of which waiting for the device (the forward's num_rendered read-back), and the
+            # host's own work: launches, autograd, Python
+            "host_wait_ms_per_step": round(1e3 * wait / steps, 4),
+            "host_busy_ms_per_step": round(1e3 * (host - wait) / steps, 4),
             "ms_per_step_vs_raster_ms": round(ms / rms, 3) if rms else None,
             "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
             "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * steps / dt / 1e9 / HBM_PEAK_GBS, 4)}

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 11
+#define GSR_ABI_VERSION 12
 
 enum gsr_status {
     GSR_OK = 0,
@@ -382,6 +382,23 @@ int gsr_point_list_keys(int32_t P, int32_t W, int32_t H, const void *geom, const
  * next preprocess; -1 queries.  Returns the previous mode, or -1 for any other
  * argument (gsr_last_error says why; the mode is unchanged). */
 int gsr_binning_mode(int mode);
+/* Split replay (not upstream; ABI 12).  The backward replays a tile's list serially
+ * per 8x8 pixel quadrant; a list far longer than the average load of a wave slot
+ * (config B's centre tiles) then sets the kernel's time.  With split replay the
+ * forward (GSR_FLAG_PREPARE_BACKWARD) stores each pixel's transmittance and colour
+ * at every SEG-th entry of a list longer than SEG, and the backward replays each
+ * SEG-entry segment in a wave of its own from that state.  Gradients agree with the
+ * unsplit replay to float rounding (the segment's start state is the forward's T and
+ * (C_final - C) / T instead of upstream's divided-down T and running accum_rec).
+ * mode -1 (default): SEG from the binning capacity (4 cap / 6144 wave slots, raised
+ * to a power of two >= 128; no split when above 1024); 0: off; > 0: that SEG (raised
+ * to a power of two the buffer allows).  Takes effect at the next forward; -2
+ * queries.  Returns the previous mode, or -3 for an invalid argument. */
+int gsr_split_mode(int mode);
+/* Microseconds the host has spent in the forward's one wait (the num_rendered
+ * read-back) since the last reset, summed over threads; reset != 0 also zeroes it.
+ * For benchmarks: a step's host time minus this is the host's own work. */
+double gsr_host_wait_us(int reset);
 int gsr_geom_layout(int32_t P, int32_t W, int32_t H, size_t *offsets, int cap);
 int gsr_binning_layout(int64_t capacity, int32_t W, int32_t H, size_t *offsets, int cap);
 int gsr_img_layout(int32_t W, int32_t H, size_t *offsets, int cap);

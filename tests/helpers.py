@@ -35,7 +35,10 @@ def activated(g, python_branch=False, scale_modifier=1.0):
 
 
 def run_hip(cam, g, dev, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=None, python_branch=False,
-            dL=None, debug=False, dsh_planar=False, footprint="rect", misalign_sh=False):
+            dL=None, debug=False, dsh_planar=False, footprint="rect", misalign_sh=False, prepare=None):
+    """prepare: the forward's GSR_FLAG_PREPARE_BACKWARD (None: the binding's default,
+    off here — the inputs need no grad); with it the backward replays the forward's
+    chunk masks and, for long lists, its split-replay checkpoints."""
     from diff_gaussian_rasterization import _C
 
     a = activated(g, python_branch, scale_modifier)
@@ -50,7 +53,7 @@ def run_hip(cam, g, dev, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=
             float(scale_modifier), t(a.get("cov3D_precomp")), t(cam.world_view_transform),
             t(cam.full_proj_transform), math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5), cam.image_height,
             cam.image_width, shs, g.active_sh_degree, t(cam.camera_center), False, debug)
-    I, color, radii, geom, binning, img = _C.rasterize_gaussians(*args, footprint=footprint)
+    I, color, radii, geom, binning, img = _C.rasterize_gaussians(*args, footprint=footprint, prepare_backward=prepare)
     torch.cuda.synchronize()
     P, W, H = a["means3D"].shape[0], cam.image_width, cam.image_height
     out = dict(num_rendered=I, color=color.cpu().numpy(), radii=radii.cpu().numpy(), footprint=footprint)

@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_struct_layout(lib):
     from diff_gaussian_rasterization import _C
 
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 11
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 12
     assert ctypes.sizeof(_C.GsrL1Seed) == 32  # struct gsr_l1_seed: three pointers and an int64
     # 12 x 4-byte scalars, 11 pointers, then sh_rest and two int32 (include/gsr.h struct gsr_inputs)
     assert ctypes.sizeof(_C.GsrInputs) == 48 + 12 * 8 + 8
@@ -346,3 +346,18 @@ def test_backward_phase_validates(lib):
         assert rc != 0 and "phases must be 1 .. 7" in lib.gsr_last_error().decode(), bad
     for ok in (1, 2, 3, 4, 5, 6, 7):  # P = 0: accepted, nothing to do
         assert lib.gsr_backward_phase(ctypes.byref(s), None, None, None, None, 0, *([None] * 12), ok, None) == 0, ok
+
+
+def test_split_mode_values():
+    """gsr_split_mode: set / query / reject (no GPU call)."""
+    from diff_gaussian_rasterization import _C
+
+    prev = _C.get_split()
+    try:
+        assert _C.set_split(0) == prev
+        assert _C.get_split() == 0
+        with pytest.raises(ValueError):
+            _C.set_split(-5)
+        assert _C.get_split() == 0
+    finally:
+        _C.set_split(prev)
