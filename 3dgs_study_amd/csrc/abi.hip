@@ -229,7 +229,7 @@ int validate(const gsr_inputs *in, bool forward) {
         return fail(GSR_ERR_CAPACITY, "image too large");
     if (in->footprint != GSR_FOOTPRINT_RECT && in->footprint != GSR_FOOTPRINT_TIGHT)
         return fail(GSR_ERR_ARGS, "footprint must be GSR_FOOTPRINT_RECT or GSR_FOOTPRINT_TIGHT (got %d)", in->footprint);
-    if (in->flags & ~(GSR_FLAG_PREPARE_BACKWARD | GSR_FLAG_L1_SEED)) return fail(GSR_ERR_ARGS, "unknown flags 0x%x", in->flags);
+    if (in->flags & ~(GSR_FLAG_PREPARE_BACKWARD | GSR_FLAG_L1_SEED | GSR_FLAG_NO_WAIT)) return fail(GSR_ERR_ARGS, "unknown flags 0x%x", in->flags);
     if (forward && (in->flags & GSR_FLAG_L1_SEED)) return fail(GSR_ERR_ARGS, "GSR_FLAG_L1_SEED is a backward flag");
     if (in->activations & ~(GSR_ACT_OPACITY | GSR_ACT_SCALE | GSR_ACT_ROTATION))
         return fail(GSR_ERR_ARGS, "unknown activations 0x%x", in->activations);
@@ -336,7 +336,8 @@ static int ensure_pinned() {
 // Preprocess, the depth sort (its first digit scan publishes num_rendered and the
 // pass count into the pinned words), the read-back event and the rank-order gather:
 // queued, not waited for.  passes: the depth passes queued (3, or 4 up front).
-static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int passes, hipStream_t s, bool dbg) {
+static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int passes, hipStream_t s, bool dbg,
+                            bool wait_event = true) {
     prepared_set(geom, false);  // preprocess resets the device's flag words too
     const int form = binform_wanted(in);
     binform_set(geom, form);
@@ -356,7 +357,8 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
                             }),
                       "depth sort", dbg, s))
         return rc;
-    if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
+    if (wait_event)
+        if (int rc = check_hip(hipEventRecord(g_ctrl_ready, s), "num_rendered read-back")) return rc;
     // the rects in rank order and the emission offsets (upstream's InclusiveSum of
     // tiles_touched, in depth order), queued before the host waits: the device stays
     // busy (with three passes queued it returns at once if the keys need four)
@@ -542,8 +544,14 @@ int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning,
     if (in->P == 0) return render_empty(in, img, out_color, gt, loss_out, s);
     if (!geom || !radii || !img || (capacity > 0 && !binning)) return fail(GSR_ERR_ARGS, "scratch buffers are NULL");
     const bool dbg = in->debug != 0;
-    const int passes = g_four_hint ? 4 : 3;
-    if (int rc = queue_preprocess(in, geom, radii, passes, s, dbg)) return rc;
+    // GSR_FLAG_NO_WAIT (stream capture): all four depth passes queued (the fourth
+    // returns at once when three suffice), nothing read back; gsr_forward_status
+    // checks the device's count once the work has run
+    const bool nowait = (in->flags & GSR_FLAG_NO_WAIT) != 0;
+    if (nowait && (dbg || capacity <= 0))
+        return fail(GSR_ERR_ARGS, "GSR_FLAG_NO_WAIT needs a binning capacity and debug off");
+    const int passes = nowait || g_four_hint ? 4 : 3;
+    if (int rc = queue_preprocess(in, geom, radii, passes, s, dbg, !nowait)) return rc;
     // Speculative: everything after the depth sort is queued before the host reads
     // num_rendered, into the caller's buffer of `capacity` instances; each binning
     // kernel checks the published count on the device and does nothing unless it
@@ -556,6 +564,10 @@ int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning,
         if (int rc = queue_render(in, geom, binning, capacity, capacity, g, img, radii, out_color, gt, loss_out,
                                   visible_out, s, dbg))
             return rc;
+    }
+    if (nowait) {
+        *num_rendered = capacity;
+        return GSR_OK;
     }
     int64_t I = 0;
     bool late = false;
@@ -570,6 +582,19 @@ int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning,
     // debug mode, or the fourth depth pass queued only now: the rest, exactly
     return queue_render(in, geom, binning, I, capacity, SpecGuard{}, img, radii, out_color, gt, loss_out, visible_out,
                         s, dbg);
+}
+
+int gsr_forward_status(int64_t capacity, int64_t *num_rendered) {
+    if (!num_rendered) return fail(GSR_ERR_ARGS, "num_rendered is NULL");
+    if (int rc = ensure_pinned()) return rc;
+    const int64_t I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
+    *num_rendered = I;
+    if (g_pinned[CTRL_PREFILTER_ERR])
+        return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (I > capacity)
+        return fail(GSR_NEED_BINNING, "binning capacity %lld < num_rendered %lld: the forward's lists are incomplete",
+                    (long long)capacity, (long long)I);
+    return GSR_OK;
 }
 
 static int backward_impl(const gsr_inputs *in, const int32_t *radii, const void *geom, const void *binning,

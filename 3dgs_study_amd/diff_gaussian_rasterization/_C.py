@@ -65,7 +65,7 @@ EXPORTED = (
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
     "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
     "gsr_forward_render_l1", "gsr_forward", "gsr_timing_sample", "gsr_binning_mode", "gsr_split_mode",
-    "gsr_host_wait_us",
+    "gsr_host_wait_us", "gsr_forward_status",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -272,6 +272,8 @@ def load_library():
     lib.gsr_split_mode.restype = ctypes.c_int
     lib.gsr_host_wait_us.argtypes = [ctypes.c_int]
     lib.gsr_host_wait_us.restype = ctypes.c_double
+    lib.gsr_forward_status.argtypes = [i64, ctypes.POINTER(i64)]
+    lib.gsr_forward_status.restype = ctypes.c_int
     lib.gsr_timing_sample.argtypes = [ctypes.c_int]
     lib.gsr_timing_sample.restype = ctypes.c_int
     lib.gsr_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -353,6 +355,7 @@ def _stream(device):
 
 FLAG_PREPARE_BACKWARD = 1  # gsr.h gsr_flags
 FLAG_L1_SEED = 2
+FLAG_NO_WAIT = 4
 NEED_BINNING = 5  # gsr.h gsr_status: gsr_forward's binning capacity was too small
 PHASE_COLOURS_APART = 4  # gsr.h gsr_backward_phase: the colour gradient in a call of its own
 
@@ -368,6 +371,17 @@ _CAP_PAD = 4096
 _capacity_level = {}  # (W, H, footprint) -> (P, num_rendered) of the last forward
 capacity_override = None  # test hook: an int capacity for every forward (0: always the two-call form)
 last_forward = {}  # how the last forward ran: {"capacity", "num_rendered", "path"} (tests, bench)
+captured_forwards = []  # capacities of the forwards queued under stream capture (forward_status)
+
+
+def forward_status(capacity: int) -> int:
+    """After a captured forward (GSR_FLAG_NO_WAIT) has run — a graph replay, then a
+    synchronize — the num_rendered its preprocess published on this thread; raises
+    if it exceeded ``capacity`` (that replay's lists, image and gradients are then
+    incomplete: capture again after an eager forward, which re-sizes the buffer)."""
+    n = ctypes.c_int64(0)
+    _check(load_library().gsr_forward_status(int(capacity), ctypes.byref(n)), "captured forward")
+    return n.value
 
 
 def _capacity_for(key, P):
@@ -509,6 +523,26 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
     key = (W, H, s.footprint)
     cap = None if s.debug or P == 0 else _capacity_for(key, P)
     done = False
+    if P > 0 and torch.cuda.is_current_stream_capturing():
+        # stream capture (torch.cuda.graph): nothing may wait for the device, so the
+        # forward is queued whole into the capacity a forward of this scene size set
+        # (gsr.h GSR_FLAG_NO_WAIT); forward_status() checks the count after a replay
+        if cap is None or s.debug:
+            raise RuntimeError("rasterize_gaussians under stream capture needs an eager forward of the same image "
+                               "size and footprint first (it sizes the binning buffer) and debug off")
+        s.flags |= FLAG_NO_WAIT
+        binning = _alloc((lib.gsr_binning_bytes(cap, W, H),), torch.uint8, device)
+        _check(lib.gsr_forward(ctypes.byref(s), geom.data_ptr(), _ptr(radii), binning.data_ptr(), cap, img.data_ptr(),
+                               out_color.data_ptr(), _ptr(gt), _ptr(loss), _ptr(vis), ctypes.byref(num_rendered),
+                               stream), "rasterize_gaussians (captured)")
+        s.flags &= ~FLAG_NO_WAIT
+        captured_forwards.append(cap)
+        last_forward.update(capacity=cap, num_rendered=None, path="captured", binning=binning)
+        if vis is None and gt is not None:
+            vis = radii > 0
+        if gt is None:
+            return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M)
+        return num_rendered.value, out_color, radii, geom, binning, img, (s, keep, device, M), loss[0], vis
     if cap is not None:  # one call, queued before the count is read (gsr_forward)
         binning = _alloc((lib.gsr_binning_bytes(cap, W, H),), torch.uint8, device)
         rc = lib.gsr_forward(ctypes.byref(s), geom.data_ptr(), _ptr(radii), binning.data_ptr(), cap, img.data_ptr(),

@@ -232,6 +232,55 @@ def train_step(camera, gaussians, target: torch.Tensor, bg: torch.Tensor, lambda
     return out
 
 
+class CapturedUnit:
+    """One fused training unit (render -> L1 -> loss.backward(), ``train_step`` with
+    glue="fused") captured once as a CUDA (HIP) graph and replayed: every kernel of
+    the unit runs on every replay, over the same parameter, camera and target
+    tensors (update them in place between replays: an optimizer step, a new view's
+    matrices copied into the captured ones), with one graph launch instead of the
+    per-step Python, autograd and ~20 kernel launches.  The gradients land in the
+    leaves' ``.grad`` tensors the capture created (``self.out`` holds the image,
+    loss, radii and visibility of the latest replay).
+
+    The capture needs an eager step of the same scene size first (warm-up, which
+    also sizes the binning buffer); inside it the forward queues everything without
+    reading num_rendered back (gsr.h GSR_FLAG_NO_WAIT), so ``check()`` — after a
+    synchronize — confirms the last replay's count fit the captured capacity and
+    raises otherwise (capture again then)."""
+
+    def __init__(self, camera, gaussians, target: torch.Tensor, bg: torch.Tensor, warmup: int = 3):
+        from diff_gaussian_rasterization import _C
+
+        self._C = _C
+        params = gaussians.params()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up on a side stream (torch.cuda.graph's recipe)
+            for _ in range(max(warmup, 1)):
+                for p in params:
+                    p.grad = None
+                train_step(camera, gaussians, target, bg, glue="fused")
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        for p in params:
+            p.grad = None
+        n0 = len(_C.captured_forwards)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = train_step(camera, gaussians, target, bg, glue="fused")
+        self.capacities = _C.captured_forwards[n0:]
+        del _C.captured_forwards[n0:]
+
+    def replay(self) -> dict:
+        self.graph.replay()
+        return self.out
+
+    def check(self) -> int:
+        """num_rendered of the last replay (after torch.cuda.synchronize()); raises if
+        it exceeded the captured binning capacity."""
+        return self._C.forward_status(self.capacities[-1])
+
+
 # ---------------------------------------------------------------- the full training step (train.py:86-141)
 def expon_lr(lr_init: float, lr_final: float, lr_delay_steps: int = 0, lr_delay_mult: float = 1.0,
              max_steps: int = 1_000_000):

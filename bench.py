@@ -308,6 +308,8 @@ def main():
     ap.add_argument("--binning", default="rowspan", choices=["rowspan", "lsd"],
                     help="the binning form (gsr_binning_mode): the row-span binning (default) or the LSD sort by "
                          "tile index; the same lists either way")
+    ap.add_argument("--graph-steps", type=int, default=200,
+                    help="N = 1: also time the unit captured as a HIP graph (train_step.CapturedUnit); 0 = off")
     ap.add_argument("--config-b-steps", type=int, default=200,
                     help="N=1: timed steps of config B (100k, 800x800, SH3, fwd+bwd) reported beside; 0 = skip")
     args = ap.parse_args()
@@ -422,6 +424,33 @@ def main():
         per_stage = {k: (ms / n if n else 0.0, n) for k, (ms, n) in stages.items() if n}
         dom = _dominant(per_stage)
     dom_live = stages.get(dom, (0.0, 0))
+    # N = 1: the same unit captured once as a HIP graph and replayed (train_step.
+    # CapturedUnit): every kernel of the unit runs every step, one graph launch
+    # replaces the per-step Python, autograd and ~20 kernel launches; the line
+    # reports the faster form, both beside (a slow host makes the eager form
+    # host-bound: C 1,250 vs 1,478 it/s on one box, tools/graph_probe.py)
+    eager_elapsed, graph_form = elapsed, None
+    if world == 1 and args.glue == "fused" and not args.lambda_dssim and args.graph_steps > 0:
+        del out
+        unit = train_step.CapturedUnit(cam, g, target, bg, warmup=2)
+        for _ in range(max(args.warmup, 1)):
+            unit.replay()
+        torch.cuda.synchronize()
+        gt0 = time.perf_counter()
+        ghost = 0.0
+        for _ in range(args.graph_steps):
+            h0 = time.perf_counter()
+            out = unit.replay()
+            ghost += time.perf_counter() - h0
+        torch.cuda.synchronize()
+        gdt = time.perf_counter() - gt0
+        graph_form = {"value": round(args.graph_steps / gdt, 3), "ms_per_step": round(1e3 * gdt / args.graph_steps, 4),
+                      "steps": args.graph_steps, "host_ms_per_step": round(1e3 * ghost / args.graph_steps, 4),
+                      "num_rendered": unit.check(), "capacity": unit.capacities[-1]}
+        out = None
+        del unit
+        if graph_form["value"] > args.steps / elapsed:
+            elapsed, host = gdt * args.steps / args.graph_steps, ghost * args.steps / args.graph_steps
 
     if rank == 0:
         steps = args.steps
@@ -479,6 +508,10 @@ def main():
                                        if args.glue == "fused" else None),
             # host time inside one_step per step (launches, autograd, the one read-back wait)
             "host_ms_per_step": round(1e3 * host / steps, 4),
+            # which form the value is (eager steps, or replays of the captured unit), both beside
+            "form": "graph" if elapsed != eager_elapsed else "eager",
+            "eager": {"value": round(world * steps / eager_elapsed, 3), "ms_per_step": round(1e3 * eager_elapsed / steps, 4)},
+            "graph": graph_form,
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -700,12 +733,43 @@ def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, l
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     wait = _C.host_wait_ms() * 1e-3
-    del g, params
     ms = 1e3 * dt / steps
+    eager = {"value": round(steps / dt, 3), "ms_per_step": round(ms, 4),
+             "host_ms_per_step": round(1e3 * host / steps, 4), "host_wait_ms_per_step": round(1e3 * wait / steps, 4),
+             "host_busy_ms_per_step": round(1e3 * (host - wait) / steps, 4)}
+    # the same unit captured once as a HIP graph and replayed (train_step.CapturedUnit):
+    # every kernel runs every step; one graph launch replaces the per-step Python,
+    # autograd and ~20 kernel launches, which bound this small config
+    graph = None
+    if glue == "fused" and not lambda_dssim:
+        unit = train_step.CapturedUnit(cam, g, target, bg, warmup=max(warmup // 4, 1))
+        for _ in range(max(warmup, 1)):
+            unit.replay()
+        torch.cuda.synchronize()
+        gt0 = time.perf_counter()
+        ghost = 0.0
+        for _ in range(steps):
+            h0 = time.perf_counter()
+            unit.replay()
+            ghost += time.perf_counter() - h0
+        torch.cuda.synchronize()
+        gdt = time.perf_counter() - gt0
+        n_graph = unit.check()  # raises if a replay's lists outgrew the captured capacity
+        graph = {"value": round(steps / gdt, 3), "ms_per_step": round(1e3 * gdt / steps, 4),
+                 "host_ms_per_step": round(1e3 * ghost / steps, 4),
+                 "host_ms_per_step_vs_ms_per_step": round(ghost / gdt, 3), "num_rendered": n_graph,
+                 "capacity": unit.capacities[-1]}
+        del unit
+    del g, params
     rms = raster_ms(per)
+    if graph is not None and graph["value"] > eager["value"]:  # the line reports the faster form, both beside
+        value, ms, host, wait, form = graph["value"], graph["ms_per_step"], ghost, 0.0, "graph"
+    else:
+        value, form = eager["value"], "eager"
     return {"metric": f"train iters/sec (fwd+bwd) + Mpix/sec, {W}x{H}, {P} Gaussians, SH{deg}",
-            "value": round(steps / dt, 3), "unit": "train-iters/s", "ms_per_step": round(ms, 4), "steps": steps,
-            "mpix_per_s": round(steps / dt * W * H / 1e6, 2),
+            "value": value, "unit": "train-iters/s", "ms_per_step": round(ms, 4), "steps": steps,
+            "form": form, "eager": eager, "graph": graph,
+            "mpix_per_s": round(value * W * H / 1e6, 2),
             "config": {"workload": f"{cfg_name}: {WORKLOADS[cfg_name]}", "gaussians": P, "width": W, "height": H,
                        "sh_degree": deg, "num_rendered": I, "glue": GLUE_NOTE[glue]},
             "stages_ms": {k: round(v[0], 4) for k, v in per.items()}, "raster_ms": rms,
@@ -718,7 +782,7 @@ def train_config_rates(cfg_name: str, dev, steps: int, warmup: int, glue: str, l
             "host_busy_ms_per_step": round(1e3 * (host - wait) / steps, 4),
             "ms_per_step_vs_raster_ms": round(ms / rms, 3) if rms else None,
             "iter_algorithmic_bytes": iter_bytes(P, I, W, H, M),
-            "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * steps / dt / 1e9 / HBM_PEAK_GBS, 4)}
+            "iter_hbm_frac": round(iter_bytes(P, I, W, H, M) * value / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmup: int, plain_ms: float,

@@ -73,7 +73,8 @@ enum gsr_status {
  * the same, with ~40 % fewer instances to sort and stream (config C: 8.0M ->
  * 4.9M); num_rendered, the lists and n_contrib then index the shorter lists.
  * Forward and backward of one render must use the same footprint.  The Python
- * package defaults to TIGHT (of upstream's outputs only num_rendered differs). */
+ * package defaults to RECT (upstream's); TIGHT changes only num_rendered and the
+ * lists among upstream's outputs. */
 enum gsr_footprint { GSR_FOOTPRINT_RECT = 0, GSR_FOOTPRINT_TIGHT = 1 };
 
 /* gsr_inputs.flags.  GSR_FLAG_PREPARE_BACKWARD (forward calls; not upstream):
@@ -84,7 +85,16 @@ enum gsr_footprint { GSR_FOOTPRINT_RECT = 0, GSR_FOOTPRINT_TIGHT = 1 };
  * the same forward zeroes it again itself).  Only a speed hint: every backward
  * is correct with or without it, and any number of forward renders may follow
  * one preprocess (each files its own quadrants afresh). */
-enum gsr_flags { GSR_FLAG_PREPARE_BACKWARD = 1, GSR_FLAG_L1_SEED = 2 };
+enum gsr_flags { GSR_FLAG_PREPARE_BACKWARD = 1, GSR_FLAG_L1_SEED = 2, GSR_FLAG_NO_WAIT = 4 };
+
+/* GSR_FLAG_NO_WAIT (gsr_forward only; not upstream): for stream capture (HIP
+ * graphs, torch.cuda.graph).  gsr_forward queues the whole forward into the
+ * capacity-sized binning buffer and returns without reading anything back (all four
+ * depth passes are queued; the fourth returns at once when three suffice), with
+ * *num_rendered = capacity.  Each binning kernel still checks the count the device
+ * publishes and does nothing unless it fits, so after the queued (or replayed) work
+ * has run the caller checks it with gsr_forward_status.  Needs capacity > 0 and
+ * debug off. */
 
 /* GSR_FLAG_L1_SEED (backward calls; not upstream): the image's gradient is that of
  * the L1 loss mean|image - gt| (utils/loss_utils.py l1_loss, train.py:102 with
@@ -395,6 +405,12 @@ int gsr_binning_mode(int mode);
  * to a power of two the buffer allows).  Takes effect at the next forward; -2
  * queries.  Returns the previous mode, or -3 for an invalid argument. */
 int gsr_split_mode(int mode);
+/* After a GSR_FLAG_NO_WAIT forward (or a replay of its capture) has run on the
+ * device: *num_rendered = the count its preprocess published to this host
+ * thread's pinned words; GSR_OK when it fits `capacity`, GSR_NEED_BINNING when it
+ * does not (that forward's lists, image and the backward that followed are
+ * incomplete), GSR_ERR_PREFILTERED for upstream's prefiltered error. */
+int gsr_forward_status(int64_t capacity, int64_t *num_rendered);
 /* Microseconds the host has spent in the forward's one wait (the num_rendered
  * read-back) since the last reset, summed over threads; reset != 0 also zeroes it.
  * For benchmarks: a step's host time minus this is the host's own work. */
