@@ -544,13 +544,13 @@ int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning,
     if (in->P == 0) return render_empty(in, img, out_color, gt, loss_out, s);
     if (!geom || !radii || !img || (capacity > 0 && !binning)) return fail(GSR_ERR_ARGS, "scratch buffers are NULL");
     const bool dbg = in->debug != 0;
-    // GSR_FLAG_NO_WAIT (stream capture): all four depth passes queued (the fourth
-    // returns at once when three suffice), nothing read back; gsr_forward_status
-    // checks the device's count once the work has run
+    // GSR_FLAG_NO_WAIT (stream capture): the depth passes the last forward needed
+    // (gsr_depth_passes_hint), nothing read back; gsr_forward_status checks the
+    // device's count and pass count once the work has run
     const bool nowait = (in->flags & GSR_FLAG_NO_WAIT) != 0;
     if (nowait && (dbg || capacity <= 0))
         return fail(GSR_ERR_ARGS, "GSR_FLAG_NO_WAIT needs a binning capacity and debug off");
-    const int passes = nowait || g_four_hint ? 4 : 3;
+    const int passes = g_four_hint ? 4 : 3;
     if (int rc = queue_preprocess(in, geom, radii, passes, s, dbg, !nowait)) return rc;
     // Speculative: everything after the depth sort is queued before the host reads
     // num_rendered, into the caller's buffer of `capacity` instances; each binning
@@ -584,13 +584,18 @@ int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning,
                         s, dbg);
 }
 
-int gsr_forward_status(int64_t capacity, int64_t *num_rendered) {
+int gsr_depth_passes_hint(void) { return g_four_hint ? 4 : 3; }
+
+int gsr_forward_status(int64_t capacity, int passes, int64_t *num_rendered) {
     if (!num_rendered) return fail(GSR_ERR_ARGS, "num_rendered is NULL");
     if (int rc = ensure_pinned()) return rc;
     const int64_t I = (int64_t)g_pinned[CTRL_NUM_RENDERED_LO] | ((int64_t)g_pinned[CTRL_NUM_RENDERED_HI] << 32);
     *num_rendered = I;
     if (g_pinned[CTRL_PREFILTER_ERR])
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (passes == 3 && g_pinned[CTRL_DSORT_PASSES] == 4u)
+        return fail(GSR_NEED_BINNING, "the depth keys need four sort passes, three were queued: the forward's lists "
+                    "are incomplete (an eager forward sets the hint; capture again)");
     if (I > capacity)
         return fail(GSR_NEED_BINNING, "binning capacity %lld < num_rendered %lld: the forward's lists are incomplete",
                     (long long)capacity, (long long)I);

@@ -53,8 +53,15 @@ struct RenderFwdArgs {
 #ifndef GSR_FWD_GROUP
 #define GSR_FWD_GROUP 2
 #endif
-constexpr int FWD_GROUP = GSR_FWD_GROUP;  // Gaussians per blend iteration (zero records after the survivors pad the last group)
-static_assert(FWD_GROUP >= 1 && FWD_GROUP <= 3, "QuadChunk holds 64 survivors + 2 zero records");
+constexpr int FWD_GROUP_MAIN = GSR_FWD_GROUP;  // Gaussians per blend iteration (zero records after the survivors pad the last group)
+// the split-replay instantiation runs where a few long lists set the kernel's time
+// (config B): there a wave's serial chain, not the issue rate, is the bound, so
+// more Gaussians per iteration (more independent work per step of the chain)
+#ifndef GSR_FWD_GROUP_SPLIT
+#define GSR_FWD_GROUP_SPLIT 3
+#endif
+static_assert(FWD_GROUP_MAIN >= 1 && FWD_GROUP_MAIN <= 3 && GSR_FWD_GROUP_SPLIT >= 1 && GSR_FWD_GROUP_SPLIT <= 3,
+              "QuadChunk holds 64 survivors + 2 zero records");
 
 // The survivors of a chunk are staged as QuadChunk records (gsr_blend.hpp): the
 // power is upstream's expression in upstream's order (exact_power), the same
@@ -65,7 +72,8 @@ static_assert(FWD_GROUP >= 1 && FWD_GROUP <= 3, "QuadChunk holds 64 survivors + 
 // so that the unsplit kernel keeps its 64 VGPRs (8 waves per SIMD; the checkpoint
 // path costs 2-4 more)
 template <bool SPLIT>
-__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(7))) render_fwd_kernel(RenderFwdArgs a) {
+__device__ __forceinline__ void render_fwd_body(const RenderFwdArgs &a) {
+    constexpr int FWD_GROUP = SPLIT ? GSR_FWD_GROUP_SPLIT : FWD_GROUP_MAIN;
     auto zero_slice = [&]() {  // every workgroup its slice of the backward's accumulator
         if (a.zero4) {
             const size_t per = (a.zero_n4 + gridDim.x - 1) / gridDim.x, z0 = (size_t)blockIdx.x * per;
@@ -268,6 +276,17 @@ __global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per
     zero_slice();
 }
 
+__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(7))) render_fwd_kernel(RenderFwdArgs a) {
+    render_fwd_body<false>(a);
+}
+// the split-replay form (checkpoints, groups of GSR_FWD_GROUP_SPLIT).  (Records two
+// chunks ahead in a third buffer, 85 VGPRs at 5 waves per SIMD: render_fwd 42.8 ->
+// 51.7 us at config B — the long lists' waves do not run alone enough for the
+// lost occupancy to pay.)
+__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(7))) render_fwd_split_kernel(RenderFwdArgs a) {
+    render_fwd_body<true>(a);
+}
+
 hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binning, void *img, float *out_color,
                              float *acc_zero, size_t acc_bytes, hipStream_t s, int64_t qmask_cap, int seg) {
     const GeomLayout G = geom_layout(in.P, in.W, in.H);
@@ -308,9 +327,9 @@ hipError_t launch_render_fwd(const gsr_inputs &in, void *geom, const void *binni
         }
     }
     if (a.seg)
-        hipLaunchKernelGGL(render_fwd_kernel<true>, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
+        hipLaunchKernelGGL(render_fwd_split_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     else
-        hipLaunchKernelGGL(render_fwd_kernel<false>, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
+        hipLaunchKernelGGL(render_fwd_kernel, dim3(blend_grid(g.tiles)), dim3(BLEND_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

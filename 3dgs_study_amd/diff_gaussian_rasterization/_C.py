@@ -65,7 +65,7 @@ EXPORTED = (
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
     "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
     "gsr_forward_render_l1", "gsr_forward", "gsr_timing_sample", "gsr_binning_mode", "gsr_split_mode",
-    "gsr_host_wait_us", "gsr_forward_status",
+    "gsr_host_wait_us", "gsr_forward_status", "gsr_depth_passes_hint",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -272,8 +272,9 @@ def load_library():
     lib.gsr_split_mode.restype = ctypes.c_int
     lib.gsr_host_wait_us.argtypes = [ctypes.c_int]
     lib.gsr_host_wait_us.restype = ctypes.c_double
-    lib.gsr_forward_status.argtypes = [i64, ctypes.POINTER(i64)]
+    lib.gsr_forward_status.argtypes = [i64, ctypes.c_int, ctypes.POINTER(i64)]
     lib.gsr_forward_status.restype = ctypes.c_int
+    lib.gsr_depth_passes_hint.restype = ctypes.c_int
     lib.gsr_timing_sample.argtypes = [ctypes.c_int]
     lib.gsr_timing_sample.restype = ctypes.c_int
     lib.gsr_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -374,13 +375,16 @@ last_forward = {}  # how the last forward ran: {"capacity", "num_rendered", "pat
 captured_forwards = []  # capacities of the forwards queued under stream capture (forward_status)
 
 
-def forward_status(capacity: int) -> int:
-    """After a captured forward (GSR_FLAG_NO_WAIT) has run — a graph replay, then a
+def forward_status(captured) -> int:
+    """After a captured forward (GSR_FLAG_NO_WAIT; ``captured`` = its (capacity,
+    depth passes) record in ``captured_forwards``) has run — a graph replay, then a
     synchronize — the num_rendered its preprocess published on this thread; raises
-    if it exceeded ``capacity`` (that replay's lists, image and gradients are then
-    incomplete: capture again after an eager forward, which re-sizes the buffer)."""
+    if it exceeded the capacity or the keys needed a fourth depth pass (that
+    replay's lists, image and gradients are then incomplete: capture again after an
+    eager forward, which re-sizes the buffer and the pass hint)."""
+    capacity, passes = captured
     n = ctypes.c_int64(0)
-    _check(load_library().gsr_forward_status(int(capacity), ctypes.byref(n)), "captured forward")
+    _check(load_library().gsr_forward_status(int(capacity), int(passes), ctypes.byref(n)), "captured forward")
     return n.value
 
 
@@ -531,12 +535,13 @@ def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_mo
             raise RuntimeError("rasterize_gaussians under stream capture needs an eager forward of the same image "
                                "size and footprint first (it sizes the binning buffer) and debug off")
         s.flags |= FLAG_NO_WAIT
+        passes = lib.gsr_depth_passes_hint()
         binning = _alloc((lib.gsr_binning_bytes(cap, W, H),), torch.uint8, device)
         _check(lib.gsr_forward(ctypes.byref(s), geom.data_ptr(), _ptr(radii), binning.data_ptr(), cap, img.data_ptr(),
                                out_color.data_ptr(), _ptr(gt), _ptr(loss), _ptr(vis), ctypes.byref(num_rendered),
                                stream), "rasterize_gaussians (captured)")
         s.flags &= ~FLAG_NO_WAIT
-        captured_forwards.append(cap)
+        captured_forwards.append((cap, passes))
         last_forward.update(capacity=cap, num_rendered=None, path="captured", binning=binning)
         if vis is None and gt is not None:
             vis = radii > 0

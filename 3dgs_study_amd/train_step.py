@@ -20,7 +20,8 @@ image, radii and gradients.
 train.py:102-104 (L1, or L1 + 0.2·(1 - SSIM)), and ``loss.backward()``; with
 ``glue="fused"`` through ``render_fused`` and the fused loss kernel
 (``train_ops.l1_ssim_loss``), with ``glue="reference"`` through ``render`` and the
-reference's torch loss.
+reference's torch loss.  ``CapturedUnit`` is the fused unit captured once as a HIP
+graph and replayed (the same kernels, one graph launch per step).
 """
 from __future__ import annotations
 
@@ -268,7 +269,8 @@ class CapturedUnit:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = train_step(camera, gaussians, target, bg, glue="fused")
-        self.capacities = _C.captured_forwards[n0:]
+        self.captured = _C.captured_forwards[n0:]  # (capacity, depth passes) per captured forward
+        self.capacities = [c for c, _ in self.captured]
         del _C.captured_forwards[n0:]
 
     def replay(self) -> dict:
@@ -278,7 +280,7 @@ class CapturedUnit:
     def check(self) -> int:
         """num_rendered of the last replay (after torch.cuda.synchronize()); raises if
         it exceeded the captured binning capacity."""
-        return self._C.forward_status(self.capacities[-1])
+        return self._C.forward_status(self.captured[-1])
 
 
 # ---------------------------------------------------------------- the full training step (train.py:86-141)

@@ -89,12 +89,12 @@ enum gsr_flags { GSR_FLAG_PREPARE_BACKWARD = 1, GSR_FLAG_L1_SEED = 2, GSR_FLAG_N
 
 /* GSR_FLAG_NO_WAIT (gsr_forward only; not upstream): for stream capture (HIP
  * graphs, torch.cuda.graph).  gsr_forward queues the whole forward into the
- * capacity-sized binning buffer and returns without reading anything back (all four
- * depth passes are queued; the fourth returns at once when three suffice), with
- * *num_rendered = capacity.  Each binning kernel still checks the count the device
- * publishes and does nothing unless it fits, so after the queued (or replayed) work
- * has run the caller checks it with gsr_forward_status.  Needs capacity > 0 and
- * debug off. */
+ * capacity-sized binning buffer and returns without reading anything back (the
+ * depth sort with gsr_depth_passes_hint() passes), with *num_rendered = capacity.
+ * Each binning kernel still checks the count and pass count the device publishes
+ * and does nothing unless both fit, so after the queued (or replayed) work has run
+ * the caller checks them with gsr_forward_status.  Needs capacity > 0 and debug
+ * off. */
 
 /* GSR_FLAG_L1_SEED (backward calls; not upstream): the image's gradient is that of
  * the L1 loss mean|image - gt| (utils/loss_utils.py l1_loss, train.py:102 with
@@ -405,12 +405,16 @@ int gsr_binning_mode(int mode);
  * to a power of two the buffer allows).  Takes effect at the next forward; -2
  * queries.  Returns the previous mode, or -3 for an invalid argument. */
 int gsr_split_mode(int mode);
+/* The depth-sort passes (3 or 4) the next forward on this host thread queues up
+ * front: 4 once a forward's keys spanned more than 2^24 steps. */
+int gsr_depth_passes_hint(void);
 /* After a GSR_FLAG_NO_WAIT forward (or a replay of its capture) has run on the
  * device: *num_rendered = the count its preprocess published to this host
- * thread's pinned words; GSR_OK when it fits `capacity`, GSR_NEED_BINNING when it
- * does not (that forward's lists, image and the backward that followed are
- * incomplete), GSR_ERR_PREFILTERED for upstream's prefiltered error. */
-int gsr_forward_status(int64_t capacity, int64_t *num_rendered);
+ * thread's pinned words; GSR_OK when it fits `capacity` and the keys needed no
+ * more than the `passes` that forward queued (gsr_depth_passes_hint at its call),
+ * GSR_NEED_BINNING when not (that forward's lists, image and the backward that
+ * followed are incomplete), GSR_ERR_PREFILTERED for upstream's prefiltered error. */
+int gsr_forward_status(int64_t capacity, int passes, int64_t *num_rendered);
 /* Microseconds the host has spent in the forward's one wait (the num_rendered
  * read-back) since the last reset, summed over threads; reset != 0 also zeroes it.
  * For benchmarks: a step's host time minus this is the host's own work. */

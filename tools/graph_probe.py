@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--configs", nargs="+", default=["B", "C"])
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--graph-only", action="store_true", help="replays only (for a kernel trace)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     for name in args.configs:
@@ -49,6 +50,10 @@ def main():
         for _ in range(20):
             eager()
         unit = train_step.CapturedUnit(cam, g, target, bg)
+        if args.graph_only:
+            for r in range(args.rounds):
+                print(f"{name} graph {rate(unit.replay, args.steps):.1f} it/s", flush=True)
+            continue
         for r in range(args.rounds):
             e = rate(eager, args.steps)
             gr = rate(unit.replay, args.steps)
