@@ -80,6 +80,33 @@ int split_get(const void *binning) {
 }
 // Split replay (gsr_split_mode; gsr_common.hpp): -1 automatic SEG, 0 off, > 0 that SEG
 std::atomic<int> g_split_mode{-1};
+// Colour apart (gsr_colour_mode, opt-in): preprocess's colour half on a side stream of
+// this host thread and device, forked after the geometry half and joined before the
+// blend.  Measured slower, so off by default: the side queue's kernels and the
+// cross-queue waits opened ~35-40 us gaps in the binning chain (config B graph
+// replays 4,786 -> 2,000-2,380 it/s, C 1,472 -> 1,016-1,026).
+std::atomic<int> g_colour_mode{0};
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+thread_local SideStream g_side[64];
+static SideStream *side_stream() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStream &ss = g_side[dev];
+    if (!ss.s) {
+        int least = 0, greatest = 0;  // the side stream at the lowest priority: the binning chain's
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);  // kernels take the CUs first
+        if (hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, least) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+            ss.s = nullptr;
+            return nullptr;
+        }
+    }
+    return &ss;
+}
 // the host's time inside the forward's num_rendered wait (gsr_host_wait_us: the
 // benchmark separates the host's own work per step from its waiting on the device)
 std::atomic<int64_t> g_wait_ns{0};
@@ -174,7 +201,7 @@ size_t g_open[GSR_STAGE_COUNT];  // gsr_timing_begin: the pool slot whose end ev
 
 const char *kStageNames[GSR_STAGE_COUNT] = {"preprocess", "scan",           "depth_sort",  "duplicate",
                                             "tile_sort",  "render_fwd",     "render_bwd",  "preprocess_bwd",
-                                            "bwd_prepare", "exchange_wait", "sh_rebuild"};
+                                            "bwd_prepare", "exchange_wait", "sh_rebuild",  "colour"};
 
 // st | TIMED_MORE: more work of a stage already counted once in this step (its
 // time is added, its launch count is not)
@@ -306,6 +333,15 @@ double gsr_host_wait_us(int reset) {
     return (double)ns * 1e-3;
 }
 
+int gsr_colour_mode(int mode) {
+    if (mode == -2) return g_colour_mode.load();
+    if (mode != 0 && mode != 1) {
+        fail(GSR_ERR_ARGS, "colour mode %d: 1 (colour half on a side stream), 0 (fused) or -2 (query)", mode);
+        return -3;
+    }
+    return g_colour_mode.exchange(mode);
+}
+
 int gsr_split_mode(int mode) {
     if (mode == -2) return g_split_mode.load();
     if (mode < -1 || mode > 65536) {
@@ -337,7 +373,7 @@ static int ensure_pinned() {
 // pass count into the pinned words), the read-back event and the rank-order gather:
 // queued, not waited for.  passes: the depth passes queued (3, or 4 up front).
 static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, int passes, hipStream_t s, bool dbg,
-                            bool wait_event = true) {
+                            bool wait_event = true, hipEvent_t *colour_join = nullptr) {
     prepared_set(geom, false);  // preprocess resets the device's flag words too
     const int form = binform_wanted(in);
     binform_set(geom, form);
@@ -345,9 +381,25 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
     if (int rc = ensure_pinned()) return rc;
     g_pinned[CTRL_NUM_RENDERED_LO] = g_pinned[CTRL_NUM_RENDERED_HI] = g_pinned[CTRL_PREFILTER_ERR] = 0;
     g_pinned[CTRL_DSORT_PASSES] = 0;
-    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s, [&] { return launch_preprocess(*in, geom, radii, carry, s); }),
+    // colour apart: the geometry half here, the colour half on the side stream (its
+    // join event goes back to the caller, who waits on it before the blend)
+    SideStream *side = nullptr;
+    if (colour_join && !dbg && g_colour_mode.load() == 1 && in->sh && !in->colors_precomp) side = side_stream();
+    if (colour_join) *colour_join = nullptr;
+    if (int rc = step(timed(GSR_STAGE_PREPROCESS, s,
+                            [&] { return launch_preprocess(*in, geom, radii, carry, s, side ? PRE_PHASE_GEOM : PRE_PHASE_FUSED); }),
                       "preprocess", dbg, s))
         return rc;
+    if (side) {
+        if (int rc = check_hip(hipEventRecord(side->fork, s), "colour fork")) return rc;
+        if (int rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "colour fork")) return rc;
+        if (int rc = check_hip(timed(GSR_STAGE_COLOUR, side->s,
+                                     [&] { return launch_preprocess(*in, geom, radii, carry, side->s, PRE_PHASE_COLOUR); }),
+                               "preprocess colour"))
+            return rc;
+        if (int rc = check_hip(hipEventRecord(side->join, side->s), "colour join")) return rc;
+        *colour_join = side->join;
+    }
     // the sort needs only the view depths; after preprocess, so that its first digit
     // scan can also publish num_rendered (one launch fewer than a publish kernel)
     if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s,
@@ -434,7 +486,7 @@ static int render_empty(const gsr_inputs *in, void *img, float *out_color, const
 // blend, the backward's preparation and the L1 loss.
 static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t n, int64_t cap, const SpecGuard &g,
                         void *img, const int32_t *radii, float *out_color, const float *gt, float *loss_out,
-                        uint8_t *visible_out, hipStream_t s, bool dbg) {
+                        uint8_t *visible_out, hipStream_t s, bool dbg, hipEvent_t colour_join = nullptr) {
     const size_t npix = (size_t)3 * in->W * in->H;
     float *l1_part = gt ? at<float>(img, img_layout(in->W, in->H).l1_part) : nullptr;
     const int form = binform_get(geom, in);
@@ -470,6 +522,9 @@ static int queue_render(const gsr_inputs *in, void *geom, void *binning, int64_t
     const size_t acc_bytes = (size_t)in->P * ACCUM_STRIDE * sizeof(float);
     // the split replay's SEG (0: none), for the lists this forward bins into cap
     const int seg = prep && n > 0 ? split_seg(cap, g_split_mode.load()) : 0;
+    // the colour half (side stream) lands before the blend reads the records
+    if (colour_join)
+        if (int rc = check_hip(hipStreamWaitEvent(s, colour_join, 0), "colour join")) return rc;
     if (int rc = step(timed(GSR_STAGE_RENDER_FWD, s,
                             [&] {
                                 return launch_render_fwd(*in, geom, n > 0 ? binning : nullptr, img, out_color,
@@ -551,7 +606,16 @@ int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning,
     if (nowait && (dbg || capacity <= 0))
         return fail(GSR_ERR_ARGS, "GSR_FLAG_NO_WAIT needs a binning capacity and debug off");
     const int passes = g_four_hint ? 4 : 3;
-    if (int rc = queue_preprocess(in, geom, radii, passes, s, dbg, !nowait)) return rc;
+    hipEvent_t join = nullptr;  // the colour half's (gsr_colour_mode), until a blend waits on it
+    if (int rc = queue_preprocess(in, geom, radii, passes, s, dbg, !nowait, &join)) return rc;
+    // every path out of here leaves the caller's stream after the colour half
+    auto joined = [&](int rc) {
+        if (join) {
+            if (int e = check_hip(hipStreamWaitEvent(s, join, 0), "colour join")) return rc ? rc : e;
+            join = nullptr;
+        }
+        return rc;
+    };
     // Speculative: everything after the depth sort is queued before the host reads
     // num_rendered, into the caller's buffer of `capacity` instances; each binning
     // kernel checks the published count on the device and does nothing unless it
@@ -562,26 +626,29 @@ int gsr_forward(const gsr_inputs *in, void *geom, int32_t *radii, void *binning,
         const SpecGuard g{at<const uint32_t>(geom, G.off[GSR_GEOM_CTRL]), at<const uint32_t>(geom, G.dsort_ctrl),
                           (uint32_t)capacity, passes == 3 ? 1 : 0};
         if (int rc = queue_render(in, geom, binning, capacity, capacity, g, img, radii, out_color, gt, loss_out,
-                                  visible_out, s, dbg))
+                                  visible_out, s, dbg, join))
             return rc;
+        join = nullptr;  // the blend waited on it
     }
     if (nowait) {
         *num_rendered = capacity;
-        return GSR_OK;
+        return joined(GSR_OK);
     }
     int64_t I = 0;
     bool late = false;
-    if (int rc = finish_preprocess(in, geom, passes, s, dbg, &I, &late)) return rc;
+    if (int rc = finish_preprocess(in, geom, passes, s, dbg, &I, &late)) return joined(rc);
     *num_rendered = I;
     if (I > capacity) {
         fail(GSR_NEED_BINNING, "binning capacity %lld < num_rendered %lld: call gsr_forward_render with a buffer of "
              "gsr_binning_bytes(num_rendered)", (long long)capacity, (long long)I);
-        return GSR_NEED_BINNING;
+        return joined(GSR_NEED_BINNING);
     }
     if (spec && !late) return GSR_OK;
     // debug mode, or the fourth depth pass queued only now: the rest, exactly
+    const hipEvent_t j = join;
+    join = nullptr;
     return queue_render(in, geom, binning, I, capacity, SpecGuard{}, img, radii, out_color, gt, loss_out, visible_out,
-                        s, dbg);
+                        s, dbg, j);
 }
 
 int gsr_depth_passes_hint(void) { return g_four_hint ? 4 : 3; }

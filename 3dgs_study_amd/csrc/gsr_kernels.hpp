@@ -10,7 +10,13 @@ namespace gsr {
 // preprocess.hip (num_rendered is published by the depth sort's first digit scan)
 // rwords: write each rect as one word into the depth sort's carried-word input
 // (the row-span binning of the rect footprint) instead of the 16-B rect records
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s);
+// phase: PRE_PHASE_FUSED (one kernel), or the geometry half (PRE_PHASE_GEOM: no SH
+// rows read, colour words 0) and the colour half (PRE_PHASE_COLOUR, SH inputs only:
+// the records' colour words, clamp bits and Jacobian of the Gaussians the geometry
+// half kept) — abi.hip runs the colour half on a side stream beside the binning
+enum PrePhase { PRE_PHASE_FUSED = 0, PRE_PHASE_GEOM = 1, PRE_PHASE_COLOUR = 2 };
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s,
+                             int phase = PRE_PHASE_FUSED);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 

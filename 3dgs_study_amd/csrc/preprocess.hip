@@ -68,8 +68,10 @@ __device__ inline float sh_channel(const float *sh, int c, int deg, float x, flo
 }
 
 // SPLIT: the SH rows come from GaussianModel's two leaves (gsr_inputs.sh_rest)
-// instead of their cat.
-template <int RWC, bool SPLIT>
+// instead of their cat.  GEOM: everything but the colour (no SH rows read; the
+// splat records' colour words left 0, clamped and the Jacobian unwritten) —
+// preprocess_colour_kernel fills those on a side stream while the binning runs.
+template <int RWC, bool SPLIT, bool GEOM = false>
 __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) {
     __shared__ uint32_t wsum[PRE_THREADS / 64];
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
@@ -77,7 +79,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     const int g0 = blockIdx.x * PRE_THREADS;
     const int idx = g0 + threadIdx.x;
     const int RW = RWC > 0 ? RWC : 3 * in.M;  // SH row width (floats)
-    const bool use_sh = in.sh != nullptr && in.colors_precomp == nullptr;
+    const bool use_sh = !GEOM && in.sh != nullptr && in.colors_precomp == nullptr;
     const int n = min(PRE_THREADS, in.P - g0);
     // This Gaussian's own inputs are loaded first and its SH row after them: at
     // degree 3 each thread loads its own 192-B row as 12 x 16 B straight into
@@ -87,7 +89,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     // re-touches; without an LDS stage the kernel is no longer LDS-limited to 3
     // waves per SIMD (preprocess 68 -> 66 us at C, 334 -> 317 us at E).  Other
     // degrees stage the workgroup's rows through LDS (coalesced, odd row stride).
-    constexpr bool DIRECT = RWC == 48;  // each thread's own row in registers, no LDS
+    constexpr bool DIRECT = RWC == 48 && !GEOM;  // each thread's own row in registers, no LDS
     const bool live = idx < in.P;
     const int li = live ? idx : in.P - 1;
     const f3 p = {in.means3D[3 * li], in.means3D[3 * li + 1], in.means3D[3 * li + 2]};
@@ -248,14 +250,16 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     if (idx == 0) {  // and the flag words (one block may be all there is)
         a.order_cnt[ORDER_FILED] = 0u;
         a.order_cnt[ORDER_FRESH] = 0u;
-        a.ctrl[CTRL_SHJAC] = a.shjac != nullptr && use_sh ? 1u : 0u;  // this call's Jacobian, or none
+        a.ctrl[CTRL_SHJAC] = a.shjac != nullptr && (use_sh || GEOM) ? 1u : 0u;  // this call's Jacobian, or none
     }
     // colour stage: the SH rows land in LDS now, after the geometry
     if (use_sh && !DIRECT) __syncthreads();
     if (emit) {
-        float rgb[3];
+        float rgb[3] = {0.f, 0.f, 0.f};
         uint8_t clampbits = 0;
-        if (in.colors_precomp) {
+        if (GEOM) {
+            // the colour words and clamp bits: preprocess_colour_kernel
+        } else if (in.colors_precomp) {
             rgb[0] = in.colors_precomp[3 * (size_t)idx];
             rgb[1] = in.colors_precomp[3 * (size_t)idx + 1];
             rgb[2] = in.colors_precomp[3 * (size_t)idx + 2];
@@ -290,13 +294,76 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         sp[0] = make_float4(px, py, ca, cb);
         sp[1] = make_float4(cc, opac, rgb[0], rgb[1]);
         sp[2] = make_float4(rgb[2], __uint_as_float((uint32_t)idx), qm, 0.0f);
-        a.clamped[idx] = clampbits;
+        if (!GEOM) a.clamped[idx] = clampbits;
     }
     // num_rendered is only a total (emit works in depth order, binning.hip): each
     // workgroup stores its sum (bit 31 flags a prefiltered violation)
     const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
     const int berr = __syncthreads_or(perr);
     if (threadIdx.x == 0) a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), 0u, 0u, 0u);
+}
+
+// The colour half of preprocess for the Gaussians the geometry half kept (radii >
+// 0; launched after it on a side stream, beside the depth sort and the binning,
+// which are bound by their launches' latency and leave the CUs mostly idle):
+// forward.cu computeColorFromSH -> the splat record's colour words, the clamp bits
+// and, when a backward follows, the SH direction Jacobian — the same operations
+// as the fused kernel's colour stage, so the same bits.
+template <int RWC, bool SPLIT>
+__global__ void __launch_bounds__(PRE_THREADS) preprocess_colour_kernel(PreArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
+    const gsr_inputs &in = a.in;
+    const int g0 = blockIdx.x * PRE_THREADS;
+    const int idx = g0 + threadIdx.x;
+    const int RW = RWC > 0 ? RWC : 3 * in.M;
+    const int n = min(PRE_THREADS, in.P - g0);
+    constexpr bool DIRECT = RWC == 48;
+    const bool emit = idx < in.P && a.radii[idx] > 0;
+    if constexpr (!DIRECT) {  // the workgroup's rows through LDS (coalesced), every thread takes part
+        if constexpr (SPLIT) {
+            rows_to_lds_cols<PRE_THREADS>(in.sh, g0, n, 3, 0, RW + 1, sh_lds);
+            if (RW > 3) rows_to_lds_cols<PRE_THREADS>(in.sh_rest, g0, n, RW - 3, 3, RW + 1, sh_lds);
+        } else {
+            rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
+        }
+        __syncthreads();
+    }
+    if (!emit) return;
+    float4 rowv[DIRECT ? 12 : 1];
+    if constexpr (DIRECT && SPLIT) {
+        float r[48];
+        load_sh_row_split(in.sh, in.sh_rest, (size_t)idx, r);
+#pragma unroll
+        for (int b = 0; b < 12; b++) rowv[b] = make_float4(r[4 * b], r[4 * b + 1], r[4 * b + 2], r[4 * b + 3]);
+    } else if constexpr (DIRECT) {
+        const float4 *r4 = reinterpret_cast<const float4 *>(in.sh + (size_t)idx * 48);
+#pragma unroll
+        for (int b = 0; b < 12; b++) rowv[b] = r4[b];
+    }
+    const f3 p = {in.means3D[3 * idx], in.means3D[3 * idx + 1], in.means3D[3 * idx + 2]};
+    const float dx = p.x - in.campos[0], dy = p.y - in.campos[1], dz = p.z - in.campos[2];
+    const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+    const float x = dx / len, y = dy / len, z = dz / len;
+    const float *sh = DIRECT ? reinterpret_cast<const float *>(rowv) : sh_lds + threadIdx.x * (RW + 1);
+    float rgb[3];
+    uint8_t clampbits = 0;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const float v = sh_channel(sh, c, in.D, x, y, z);
+        clampbits |= (v < 0) ? (uint8_t)(1u << c) : (uint8_t)0;
+        rgb[c] = fmaxf(v, 0.0f);
+    }
+    if (a.shjac) {
+        float J[9];
+        sh_dir_jacobian(sh, in.D, x, y, z, J);
+#pragma unroll
+        for (int k = 0; k < 9; k++) a.shjac[(size_t)k * in.P + idx] = J[k];
+    }
+    // the record's colour words: floats 6, 7 ({cc, opacity, r, g}) and 8 ({b, ...})
+    float *rec = reinterpret_cast<float *>(a.splats + 3 * (size_t)idx);
+    *reinterpret_cast<float2 *>(rec + 6) = make_float2(rgb[0], rgb[1]);
+    rec[8] = rgb[2];
+    a.clamped[idx] = clampbits;
 }
 
 // auxiliary.h in_frustum via checkFrustum (markVisible).
@@ -309,7 +376,8 @@ __global__ void mark_visible_kernel(int P, const float *means3D, const float *vi
     present[idx] = !(pv.z <= 0.2f);
 }
 
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s) {
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s,
+                             int phase) {
     const GeomLayout L = geom_layout(in.P, in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
     PreArgs a;
@@ -340,13 +408,23 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, b
     // SH row width as a compile-time constant for the common degrees (cheap LDS
     // row indexing); any other width takes the run-time path
     const int width = in.sh && !in.colors_precomp ? 3 * in.M : 0;
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(nb), dim3(PRE_THREADS), lds, s, a); };
-    if (width == 3)  // (M = 1 has no rest coefficients: never split)
-        go(preprocess_fwd_kernel<3, false>);
-    else if (width == 48 && direct)
-        split ? go(preprocess_fwd_kernel<48, true>) : go(preprocess_fwd_kernel<48, false>);
-    else
-        split ? go(preprocess_fwd_kernel<0, true>) : go(preprocess_fwd_kernel<0, false>);
+    auto go = [&](auto kern, size_t shm) { hipLaunchKernelGGL(kern, dim3(nb), dim3(PRE_THREADS), shm, s, a); };
+    if (phase == PRE_PHASE_GEOM) {  // (SH inputs only: launch_preprocess_apart)
+        go(preprocess_fwd_kernel<0, false, true>, 0);
+    } else if (phase == PRE_PHASE_COLOUR) {
+        if (width == 3)
+            go(preprocess_colour_kernel<3, false>, lds);
+        else if (width == 48 && direct)
+            split ? go(preprocess_colour_kernel<48, true>, 0) : go(preprocess_colour_kernel<48, false>, 0);
+        else
+            split ? go(preprocess_colour_kernel<0, true>, lds) : go(preprocess_colour_kernel<0, false>, lds);
+    } else if (width == 3) {  // (M = 1 has no rest coefficients: never split)
+        go(preprocess_fwd_kernel<3, false>, lds);
+    } else if (width == 48 && direct) {
+        split ? go(preprocess_fwd_kernel<48, true>, lds) : go(preprocess_fwd_kernel<48, false>, lds);
+    } else {
+        split ? go(preprocess_fwd_kernel<0, true>, lds) : go(preprocess_fwd_kernel<0, false>, lds);
+    }
     // num_rendered: the depth sort's first digit scan publishes it (binning.hip)
     return hipGetLastError();
 }

@@ -65,7 +65,7 @@ EXPORTED = (
     "gsr_backward_colors_render", "gsr_backward_colors_finish", "gsr_point_list_keys", "gsr_backward_leaves",
     "gsr_build_id", "gsr_backward_phase", "gsr_timing_begin", "gsr_timing_end", "gsr_l1_grad",
     "gsr_forward_render_l1", "gsr_forward", "gsr_timing_sample", "gsr_binning_mode", "gsr_split_mode",
-    "gsr_host_wait_us", "gsr_forward_status", "gsr_depth_passes_hint",
+    "gsr_host_wait_us", "gsr_forward_status", "gsr_depth_passes_hint", "gsr_colour_mode",
 )
 
 # gsr_footprint (include/gsr.h): which bounding-rect tiles of a Gaussian are binned
@@ -129,6 +129,17 @@ def set_split(seg) -> int:
     if prev < -1:
         raise ValueError(load_library().gsr_last_error().decode())
     return prev
+
+
+def set_colour_apart(on: bool) -> bool:
+    """Preprocess's colour half on a side stream beside the binning (include/gsr.h
+    gsr_colour_mode; opt-in, measured slower) or one fused kernel (the default).
+    Returns the previous setting."""
+    return bool(load_library().gsr_colour_mode(1 if on else 0))
+
+
+def get_colour_apart() -> bool:
+    return bool(load_library().gsr_colour_mode(-2))
 
 
 def get_split() -> int:
@@ -275,6 +286,8 @@ def load_library():
     lib.gsr_forward_status.argtypes = [i64, ctypes.c_int, ctypes.POINTER(i64)]
     lib.gsr_forward_status.restype = ctypes.c_int
     lib.gsr_depth_passes_hint.restype = ctypes.c_int
+    lib.gsr_colour_mode.argtypes = [ctypes.c_int]
+    lib.gsr_colour_mode.restype = ctypes.c_int
     lib.gsr_timing_sample.argtypes = [ctypes.c_int]
     lib.gsr_timing_sample.restype = ctypes.c_int
     lib.gsr_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -304,6 +317,9 @@ def load_library():
     lib.gsr_build_id.restype = ctypes.c_char_p
     if lib.gsr_abi_version() != ABI_VERSION:
         raise ImportError(f"{path}: ABI version {lib.gsr_abi_version()} != {ABI_VERSION}; rebuild")
+    if os.environ.get("GSR_COLOUR_APART"):  # preprocess's colour half on a side stream (set_colour_apart)
+        if lib.gsr_colour_mode(int(os.environ["GSR_COLOUR_APART"])) < -1:
+            raise ImportError(f"GSR_COLOUR_APART={os.environ['GSR_COLOUR_APART']!r}: {lib.gsr_last_error().decode()}")
     if os.environ.get("GSR_SPLIT"):  # the split replay's setting (set_split), e.g. 0 for A/B timing
         if lib.gsr_split_mode(int(os.environ["GSR_SPLIT"])) < -1:
             raise ImportError(f"GSR_SPLIT={os.environ['GSR_SPLIT']!r}: {lib.gsr_last_error().decode()}")

@@ -68,6 +68,10 @@ def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, M: int, backwa
         # means/scale/rot/opacity/SH in; depth, means2D, 48-B splat record, clamp bits,
         # tiles_touched, 16-B rect record, radii out (+ the Jacobian)
         "preprocess": P * (44 + 12 * M) + P * (85.0 + jac),
+        # preprocess's colour half when it runs apart (gsr_colour_mode 1; the
+        # geometry half is then "preprocess" without the SH row, colour words and
+        # Jacobian): means 12 + radii 4 + the SH row in, colour 12 + clamp 1 + Jacobian out
+        "colour": P * (16 + 12 * M) + P * (13.0 + jac),
         "scan": P * 8.0,
         "depth_sort": P * 16.0,                               # depths + tiles_touched in, order + offsets out
         "duplicate": P * 20.0 + I * 8.0,                      # duplicateWithKeys: per-G read, (tile, id) out
@@ -94,6 +98,8 @@ def stage_model_fracs(per_stage: dict, P: int, I: int, W: int, H: int, M: int, b
     for k, v in per_stage.items():
         ms = v[0] if isinstance(v, tuple) else v
         b = algorithmic_bytes(k, P, I, W, H, M, backward, S)
+        if k == "preprocess" and "colour" in per_stage:
+            b = P * (44 + 72.0)  # the geometry half alone: the colour half is its own stage
         if ms and b:
             out[k] = round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     return out

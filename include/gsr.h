@@ -415,6 +415,14 @@ int gsr_depth_passes_hint(void);
  * GSR_NEED_BINNING when not (that forward's lists, image and the backward that
  * followed are incomplete), GSR_ERR_PREFILTERED for upstream's prefiltered error. */
 int gsr_forward_status(int64_t capacity, int passes, int64_t *num_rendered);
+/* Colour apart (not upstream; ABI 12; opt-in): 1 — gsr_forward runs preprocess as
+ * its geometry half on the caller's stream and its colour half (SH -> RGB, the clamp
+ * bits, the SH direction Jacobian) on a low-priority side stream forked after it,
+ * beside the depth sort and the binning, joined before the blend; 0 (default) — one
+ * fused preprocess kernel (the side queue measured slower: DESIGN.md §9).  SH inputs
+ * only, never in debug mode or the two-call form.  The same bits either way.  -2
+ * queries; returns the previous mode, or -3 for an invalid argument. */
+int gsr_colour_mode(int mode);
 /* Microseconds the host has spent in the forward's one wait (the num_rendered
  * read-back) since the last reset, summed over threads; reset != 0 also zeroes it.
  * For benchmarks: a step's host time minus this is the host's own work. */
@@ -441,6 +449,7 @@ enum gsr_stage {
     GSR_STAGE_BWD_PREPARE,    /* accumulator zeroing + the render backward's wave order (no upstream kernel) */
     GSR_STAGE_EXCHANGE_WAIT,  /* caller-marked (gsr_timing_begin/end): the view-parallel exchange's wait for its collectives */
     GSR_STAGE_SH_REBUILD,     /* caller-marked: the SH gradients rebuilt from the gathered colour records */
+    GSR_STAGE_COLOUR,         /* preprocess's colour half on the side stream (gsr_colour_mode 1), beside the binning */
     GSR_STAGE_COUNT
 };
 int gsr_timing_enable(int mask);

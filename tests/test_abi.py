@@ -129,9 +129,9 @@ def test_sh_exchange_entry_points_validate(lib):
 def test_stage_names(lib):
     from diff_gaussian_rasterization import _C
 
-    names = [lib.gsr_stage_name(i).decode() for i in range(11)]
+    names = [lib.gsr_stage_name(i).decode() for i in range(12)]
     assert names == ["preprocess", "scan", "depth_sort", "duplicate", "tile_sort", "render_fwd", "render_bwd",
-                     "preprocess_bwd", "bwd_prepare", "exchange_wait", "sh_rebuild"]
+                     "preprocess_bwd", "bwd_prepare", "exchange_wait", "sh_rebuild", "colour"]
     assert lib.gsr_stage_name(99).decode() == ""
     assert lib.gsr_timing_sample(0) != 0 and "sample period" in lib.gsr_last_error().decode()
     assert lib.gsr_timing_sample(4) == 0 and lib.gsr_timing_sample(1) == 0
@@ -361,3 +361,17 @@ def test_split_mode_values():
         assert _C.get_split() == 0
     finally:
         _C.set_split(prev)
+
+
+def test_colour_mode_values():
+    """gsr_colour_mode: set / query / reject (no GPU call)."""
+    from diff_gaussian_rasterization import _C
+
+    prev = _C.get_colour_apart()
+    try:
+        assert _C.set_colour_apart(False) == prev
+        assert _C.get_colour_apart() is False
+        assert _C.load_library().gsr_colour_mode(7) == -3
+        assert _C.get_colour_apart() is False
+    finally:
+        _C.set_colour_apart(prev)
