@@ -140,8 +140,13 @@ __host__ __device__ inline bool rowspan_grid(int W, int H) {
     return g.gx <= RADIX && g.gy <= RADIX;
 }
 __host__ __device__ inline int rsa_blocks(int P) { return P > 0 ? (P + RSA_GAUSS - 1) / RSA_GAUSS : 1; }
-// pass B's blocks: ceil(spans of row r / RSB_SPANS) per row, spans <= instances <= cap
-__host__ __device__ inline int rsb_blocks_max(int64_t cap, int gy) { return (int)(cap / RSB_SPANS) + gy + 1; }
+// Pass B's block size: RSB_SPANS spans, or RSB_SPANS_SMALL for capacities up to
+// RSB_SMALL_CAP (config B: ~100 blocks of 1,024 spans left most CUs idle)
+constexpr int RSB_SPANS_SMALL = 256;
+constexpr int64_t RSB_SMALL_CAP = 1 << 20;
+__host__ __device__ inline int rsb_spans(int64_t cap) { return cap <= RSB_SMALL_CAP ? RSB_SPANS_SMALL : RSB_SPANS; }
+// pass B's blocks: ceil(spans of row r / rsb_spans(cap)) per row, spans <= instances <= cap
+__host__ __device__ inline int rsb_blocks_max(int64_t cap, int gy) { return (int)(cap / rsb_spans(cap)) + gy + 1; }
 
 // ---- control words (uint32 [16]) inside the geom buffer (a device copy of what
 // preprocess publishes to the host: num_rendered, the prefiltered error) ----

@@ -58,8 +58,8 @@ constexpr int RS_COUNT_GRID = 2048;  // rowspan_b_count_kernel's grid at most (2
 #endif
 constexpr int RSA_ROUND = RS_THREADS * RSA_ITEMS, RSB_ROUND = RS_THREADS * RSB_ITEMS;
 constexpr int RSA_PER = RSA_GAUSS / RS_THREADS;  // Gaussians per thread
-constexpr int RSB_PER = RSB_SPANS / RS_THREADS;  // spans per thread
-static_assert(RSA_PER * RS_THREADS == RSA_GAUSS && RSB_PER * RS_THREADS == RSB_SPANS, "whole sources per thread");
+static_assert(RSA_PER * RS_THREADS == RSA_GAUSS && RSB_SPANS % RS_THREADS == 0 && RSB_SPANS_SMALL % RS_THREADS == 0,
+              "whole sources per thread");
 
 struct RowSpanArgs {
     int P, gx, gy;
@@ -79,6 +79,7 @@ struct RowSpanArgs {
     uint32_t *bhist;         // [RADIX][nBmax] column counts per block -> block offsets (the scan)
     const uint32_t *btot;    // [RADIX] instances per column
     int nBmax;
+    int spb;                 // spans per pass-B block (rsb_spans of the capacity)
     uint4 *btab;             // [nBmax] pass B's block table (rowspan_b_count_kernel)
     uint32_t *point_list;
     uint2 *ranges;           // [T] (zeroed by preprocess; empty tiles stay (0, 0))
@@ -159,7 +160,7 @@ __device__ __forceinline__ void scatter_round(uint32_t n, uint8_t *dig, T *pay, 
 __device__ __forceinline__ void write_b_segments(const RowSpanArgs &a, uint32_t *wsum) {
     const uint32_t t = threadIdx.x;
     const uint32_t tot = (int)t < a.gy ? a.atot[t] : 0u;
-    const uint32_t nb = (tot + RSB_SPANS - 1u) / RSB_SPANS;
+    const uint32_t nb = (tot + (uint32_t)a.spb - 1u) / (uint32_t)a.spb;
     uint32_t tb, ts;
     const uint32_t ib = block_inclusive_scan<RS_THREADS>(nb, wsum, &tb);
     const uint32_t is = block_inclusive_scan<RS_THREADS>(tot, wsum, &ts);
@@ -269,7 +270,7 @@ __global__ void __launch_bounds__(RS_THREADS) rowspan_b_count_kernel(RowSpanArgs
 #pragma unroll
         for (uint32_t step = RADIX / 2; step >= 1; step >>= 1)
             if (sfb[r + step] <= b) r += step;
-        const uint32_t s0 = sfs[r] + (b - sfb[r]) * RSB_SPANS, s1 = min(s0 + RSB_SPANS, sfs[r + 1]);
+        const uint32_t s0 = sfs[r] + (b - sfb[r]) * (uint32_t)a.spb, s1 = min(s0 + (uint32_t)a.spb, sfs[r + 1]);
         if (threadIdx.x == 0) a.btab[b] = make_uint4(s0, r | ((s1 - s0) << 16), sfb[r], sfb[r + 1]);
         for (uint32_t s = s0 + threadIdx.x; s < s1; s += RS_THREADS) {
             const uint32_t x = a.span_x[s];
@@ -289,8 +290,9 @@ __global__ void __launch_bounds__(RS_THREADS) rowspan_b_count_kernel(RowSpanArgs
 // the dispatcher's fresh workgroups overlap each other's load chains better); the
 // grid is sized by the capacity and the workgroups beyond the device's block count
 // exit at once.
-template <int NB>
+template <int NB, int SPB>
 __global__ void __launch_bounds__(RS_THREADS, GSR_RSB_WAVES) rowspan_b_kernel(RowSpanArgs a) {
+    constexpr int RSB_PER = SPB / RS_THREADS;  // spans per thread
     __shared__ uint8_t dig[RSB_ROUND];
     __shared__ uint32_t pay[RSB_ROUND];
     __shared__ uint32_t cnt[RS_WAVES][RADIX];
@@ -383,6 +385,7 @@ static RowSpanArgs rowspan_args(int P, int W, int H, void *geom, void *binning, 
     a.bhist = at<uint32_t>(binning, B.hist);
     a.btot = at<const uint32_t>(binning, B.totals);
     a.nBmax = (int)B.hist_stride;
+    a.spb = rsb_spans(cap > 0 ? cap : 1);
     a.btab = at<uint4>(binning, B.rs_btab);
     a.point_list = at<uint32_t>(binning, B.off[GSR_BIN_POINT_LIST]);
     a.ranges = at<uint2>(geom, L.off[GSR_GEOM_RANGES]);
@@ -411,10 +414,12 @@ hipError_t launch_rowspan_b(int P, int W, int H, void *geom, void *binning, int6
     if (hipError_t e = launch_count_scan(a.bhist, a.nBmax, a.seg + RADIX, const_cast<uint32_t *>(a.btot), a.gx, g, s))
         return e;
     const dim3 bgrid(a.nBmax);
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, bgrid, block, 0, s, a); };
+    const bool small = a.spb == RSB_SPANS_SMALL;
     switch (nb_class(a.gx)) {
-        case 6: hipLaunchKernelGGL(rowspan_b_kernel<6>, bgrid, block, 0, s, a); break;
-        case 7: hipLaunchKernelGGL(rowspan_b_kernel<7>, bgrid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL(rowspan_b_kernel<8>, bgrid, block, 0, s, a); break;
+        case 6: small ? go(rowspan_b_kernel<6, RSB_SPANS_SMALL>) : go(rowspan_b_kernel<6, RSB_SPANS>); break;
+        case 7: small ? go(rowspan_b_kernel<7, RSB_SPANS_SMALL>) : go(rowspan_b_kernel<7, RSB_SPANS>); break;
+        default: small ? go(rowspan_b_kernel<8, RSB_SPANS_SMALL>) : go(rowspan_b_kernel<8, RSB_SPANS>); break;
     }
     return hipGetLastError();
 }

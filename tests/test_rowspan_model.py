@@ -20,7 +20,7 @@ import pytest
 
 from helpers import activated, case
 
-RSA_GAUSS, RSB_SPANS = 256, 1024
+RSA_GAUSS, RSB_SPANS = 256, 1024  # pass B: 1,024 spans per block, 256 up to a capacity of 2^20 (gsr_common.hpp)
 
 
 def excl(v):
@@ -45,8 +45,9 @@ def spans_of(x0, x1, y0, y1, mask):
     return out
 
 
-def rowspan_model(ids, spans, gx, gy):
-    """point_list, ranges from the kernels' arithmetic; ids / spans in rank order."""
+def rowspan_model(ids, spans, gx, gy, spb=RSB_SPANS):
+    """point_list, ranges from the kernels' arithmetic; ids / spans in rank order;
+    spb: spans per pass-B block."""
     P = len(ids)
     nA = max(1, -(-P // RSA_GAUSS))
     # pass A counts (rank_gather_kernel) and their per-row scan (launch_count_scan)
@@ -70,7 +71,7 @@ def rowspan_model(ids, spans, gx, gy):
             span_x[pos], span_id[pos], span_row[pos] = xa | (xb << 16), i, y
     assert (span_row >= 0).all()
     # the segment table (write_b_segments)
-    nb = -(-atot // RSB_SPANS)
+    nb = -(-atot // spb)
     fb, fs, nB = excl(nb), excl(atot), int(nb.sum())
     fb = np.append(fb, nB)
     fs = np.append(fs, S)
@@ -78,8 +79,8 @@ def rowspan_model(ids, spans, gx, gy):
     blocks = []
     for b in range(nB):  # rowspan_b_count_kernel: the difference array
         r = int(np.searchsorted(fb[:-1], b, "right") - 1)
-        s0 = fs[r] + (b - fb[r]) * RSB_SPANS
-        s1 = min(s0 + RSB_SPANS, fs[r + 1])
+        s0 = fs[r] + (b - fb[r]) * spb
+        s1 = min(s0 + spb, fs[r + 1])
         h = np.zeros(gx + 1, np.int64)
         for s in range(s0, s1):
             assert span_row[s] == r
@@ -116,8 +117,9 @@ def rank_order(depths, visible):
     return idx[np.lexsort((idx, depths[idx].view(np.uint32)))]
 
 
+@pytest.mark.parametrize("spb", [1024, 256])
 @pytest.mark.parametrize("P,W,H,seed", [(3_000, 333, 201, 1), (2_500, 160, 120, 5), (1_200, 800, 256, 7)])
-def test_rowspan_model_matches_oracle_rect(oracle, P, W, H, seed):
+def test_rowspan_model_matches_oracle_rect(oracle, P, W, H, seed, spb):
     cam, g = case(P, W, H, 0, seed=seed, scale_range=(0.003, 0.08))
     a = activated(g)
     r = oracle.forward(a["means3D"].numpy(), a["opacities"].numpy(), cam.world_view_transform.numpy(),
@@ -128,13 +130,14 @@ def test_rowspan_model_matches_oracle_rect(oracle, P, W, H, seed):
     order = rank_order(r["depths"], r["radii"] > 0)
     rc = r["rects"][order]
     spans = spans_of(rc[:, 0], rc[:, 2], rc[:, 1], rc[:, 3], [None] * len(order))
-    assert len(order) > RSA_GAUSS and sum(map(len, spans)) > RSB_SPANS  # several blocks in both passes
-    pl, ranges = rowspan_model(order, spans, gx, gy)
+    assert len(order) > RSA_GAUSS and sum(map(len, spans)) > spb  # several blocks in both passes
+    pl, ranges = rowspan_model(order, spans, gx, gy, spb)
     np.testing.assert_array_equal(pl, r["point_list"])
     np.testing.assert_array_equal(ranges, r["ranges"].astype(np.int64))
 
 
-def test_rowspan_model_masked_footprints():
+@pytest.mark.parametrize("spb", [1024, 256])
+def test_rowspan_model_masked_footprints(spb):
     """Tight-footprint masks (per row one run of columns or nothing, rects of at most
     64 tiles), mixed with full rects: the lists are the (tile, rank) sort."""
     rng = np.random.default_rng(3)
@@ -158,7 +161,7 @@ def test_rowspan_model_masked_footprints():
         masks.append(m)
     ids = rng.permutation(P)  # rank r holds Gaussian ids[r]
     spans = spans_of(x0, x1, y0, y1, masks)
-    pl, ranges = rowspan_model(ids, spans, gx, gy)
+    pl, ranges = rowspan_model(ids, spans, gx, gy, spb)
     tiles = [(y * gx + x, r) for r, s in enumerate(spans) for (y, xa, xb) in s for x in range(xa, xb)]
     tiles.sort()
     np.testing.assert_array_equal(pl, ids[[r for (_, r) in tiles]])
