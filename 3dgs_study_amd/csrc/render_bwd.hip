@@ -101,8 +101,11 @@ __device__ __forceinline__ float swz_fold(float c) {
 
 // MASKS: the forward's chunk cull masks are in a.qmask (a separate instantiation:
 // one kernel carrying both the mask and the cull path ran out of VGPRs)
+#ifndef GSR_BWD_WAVES
+#define GSR_BWD_WAVES 6
+#endif
 template <bool MASKS>
-__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(6))) render_bwd_kernel(RenderBwdArgs a) {
+__global__ void __launch_bounds__(BLEND_THREADS) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES))) render_bwd_kernel(RenderBwdArgs a) {
     static_assert(BLEND_WAVES == 1, "the backward wave order needs one-wave workgroups");
     // workgroup 8 r + x: XCD x's r-th quadrant in bucket order (gsr_blend.hpp)
     const int lane = threadIdx.x & 63;
