@@ -354,6 +354,43 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     // RXM_UNPACK stages the packed words alone (the value is in the word)
     __shared__ uint32_t stage_k[TILE_N], stage_v[MODE == RXM_UNPACK ? 1 : TILE_N], stage_w[CARRY ? TILE_N : 1];
     if (pass_skipped(a)) return;
+    // A grouped first depth pass has no digit scan to reduce the candidate key
+    // range: every block reduces the per-block ranges itself (the same operations,
+    // so the same base and pass count everywhere), and block 0 publishes them
+    uint2 bp = make_uint2(0u, 0u);
+    const bool local_base = MODE == RXM_KV && a.role == RX_DEPTH_FIRST && a.sup != nullptr;
+    if (local_base) {
+        uint32_t kmin = 0xffffffffu, kmax = 0u;
+        for (int i = threadIdx.x; i < a.NB; i += RX_THREADS) {
+            const uint2 m = a.minmax[i];
+            kmin = min(kmin, m.x);
+            kmax = max(kmax, m.y);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+            kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            stage_k[threadIdx.x >> 6] = kmin;
+            stage_k[RX_WAVES + (threadIdx.x >> 6)] = kmax;
+        }
+        __syncthreads();
+        for (int k = 0; k < RX_WAVES; k++) {
+            kmin = min(kmin, stage_k[k]);
+            kmax = max(kmax, stage_k[RX_WAVES + k]);
+        }
+        bp = dsort_base_passes(kmin, kmax);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            a.ctrl_out[DCTRL_KEY_BASE] = bp.x;
+            a.ctrl_out[DCTRL_PASSES] = bp.y;
+            if (a.host_ctrl) {  // the host launches the fourth pass only when it is needed
+                __hip_atomic_store(&a.host_ctrl[CTRL_DSORT_PASSES], bp.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+            }
+        }
+        __syncthreads();  // (stage_k is reused below)
+    }
     // three-pass depth sort: the third pass is the last one
     const bool final3 = a.role == RX_DEPTH_THIRD && a.ctrl[DCTRL_PASSES] == 3;
     uint32_t *const kout = final3 ? nullptr : a.kout;
@@ -430,7 +467,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
         if constexpr (MODE == RXM_PACK)
             kk[r] = ok ? (uint32_t)reinterpret_cast<const uint8_t *>(a.kin)[idx] : 0u;
         else
-            kk[r] = ok ? load_key(a, idx) : 0u;
+            kk[r] = ok ? (local_base ? key_rel(a.kin[idx], bp.x, bp.y) : load_key(a, idx)) : 0u;
         if constexpr (MODE != RXM_UNPACK) vv[r] = a.vin ? (ok ? a.vin[idx] : 0u) : idx;
         if constexpr (CARRY) ww[r] = ok ? (a.win ? a.win[idx] : rect_word(a.rin[idx])) : 0u;
     }
@@ -879,18 +916,29 @@ struct DepthKeyArgs {
     uint2 *minmax;    // [NB]
     uint32_t *zero;   // the grouped passes' group counts, cleared here (every block a slice), or NULL
     int zero_n;
+    // grouped first pass (dsort_grouped): the block's digit-count row (hist
+    // block-major) and its group's running counts (zeroed by preprocess), and
+    // workgroup NB publishes num_rendered (the digit scan it replaces did); NULL otherwise
+    uint32_t *sup0;
+    const uint4 *pub_sums;
+    int pub_n;
+    uint32_t *pub_ctrl, *pub_host;
 };
 template <int ITEMS>
 __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) {
     constexpr int TILE_N = RX_THREADS * ITEMS;
     __shared__ uint32_t h[RX_WAVES][RADIX];
     __shared__ uint32_t wmin[RX_WAVES], wmax[RX_WAVES];
+    if (a.zero)  // (every workgroup of the grid its slice, the publishing one included)
+        for (int i = blockIdx.x * RX_THREADS + threadIdx.x; i < a.zero_n; i += gridDim.x * RX_THREADS) a.zero[i] = 0u;
+    if (a.sup0 && (int)blockIdx.x == a.NB) {  // the grouped form's extra workgroup
+        publish_total<RX_THREADS>(a.pub_sums, a.pub_n, a.pub_ctrl, a.pub_host);
+        return;
+    }
     const int w = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) h[k][threadIdx.x] = 0;
     const uint32_t blk = radix_block(a.NB);
-    if (a.zero)
-        for (int i = blockIdx.x * RX_THREADS + threadIdx.x; i < a.zero_n; i += gridDim.x * RX_THREADS) a.zero[i] = 0u;
     const Mat4 V = load_mat4(a.viewmatrix);
     float z[ITEMS];
 #pragma unroll
@@ -929,7 +977,12 @@ __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) 
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < RX_WAVES; k++) c += h[k][threadIdx.x];
-    a.hist[(size_t)threadIdx.x * a.NB + blk] = c;
+    if (a.sup0) {  // grouped (as radix_upsweep_kernel's grouped form)
+        a.hist[(size_t)blk * RADIX + threadIdx.x] = c;
+        if (c) atomicAdd(&a.sup0[(size_t)(blk >> DSORT_SB_LOG2) * RADIX + threadIdx.x], c);
+    } else {
+        a.hist[(size_t)threadIdx.x * a.NB + blk] = c;
+    }
     if (threadIdx.x == 0) {
         for (int k = 1; k < RX_WAVES; k++) {
             kmin = min(kmin, wmin[k]);
@@ -984,9 +1037,10 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p, bool carry) 
     a.shift = 8 * p;
     a.nbits = RADIX_BITS;
     a.dmask = RADIX - 1;
-    if (p > 0 && dsort_grouped(P)) {
+    if (p > 0 ? dsort_grouped(P) : dsort_grouped1(P)) {  // passes 2-4, and the first (counts from depth_keys_kernel)
         a.nsup = dsort_nsup(P);
-        a.sup = at<uint32_t>(geom, L.dsort_sup) + (size_t)(p - 1) * a.nsup * RADIX;
+        a.sup = p > 0 ? at<uint32_t>(geom, L.dsort_sup) + (size_t)(p - 1) * a.nsup * RADIX
+                      : at<uint32_t>(geom, L.dsort_sup0);
     }
     return a;
 }
@@ -1005,7 +1059,15 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     k.minmax = at<uint2>(geom, L.dsort_minmax);
     k.zero = dsort_grouped(P) ? at<uint32_t>(geom, L.dsort_sup) : nullptr;
     k.zero_n = dsort_grouped(P) ? 3 * dsort_nsup(P) * RADIX : 0;
-    hipLaunchKernelGGL(depth_keys_kernel<ITEMS>, dim3(k.NB), dim3(RX_THREADS), 0, s, k);
+    // grouped: the first pass needs no digit scan either; num_rendered's publish
+    // (that scan's extra workgroup) moves to this launch's extra workgroup
+    const bool g1 = dsort_grouped1(P);
+    k.sup0 = g1 ? at<uint32_t>(geom, L.dsort_sup0) : nullptr;
+    k.pub_sums = at<const uint4>(geom, L.block_sums);
+    k.pub_n = pre_blocks(P);
+    k.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+    k.pub_host = host_ctrl;
+    hipLaunchKernelGGL(depth_keys_kernel<ITEMS>, dim3(k.NB + (g1 ? 1 : 0)), dim3(RX_THREADS), 0, s, k);
     // passes 3: the host reads the published pass count after its sync and launches
     // the fourth (launch_depth_sort_fourth) when the keys need it — three
     // early-returning launches (~14 us at config C) saved in the common case;
@@ -1013,12 +1075,14 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     // when three suffice
     for (int p = 0; p < passes; p++) {
         RadixPass a = depth_pass(P, W, H, geom, p, carry);
-        if (p == 0) {  // the first digit scan publishes the pass count and num_rendered
+        if (p == 0) {  // the first digit scan (or, grouped, the first downsweep) publishes the pass count ...
             a.host_ctrl = host_ctrl;
-            a.pub_sums = at<const uint4>(geom, L.block_sums);
-            a.pub_n = pre_blocks(P);
-            a.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
-            a.pub_host = host_ctrl;
+            if (!g1) {  // ... and num_rendered (grouped: depth_keys_kernel's extra workgroup)
+                a.pub_sums = at<const uint4>(geom, L.block_sums);
+                a.pub_n = pre_blocks(P);
+                a.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+                a.pub_host = host_ctrl;
+            }
         }
         hipError_t e = radix_pass<ITEMS>(a, s, p == 0);
         if (e != hipSuccess) return e;

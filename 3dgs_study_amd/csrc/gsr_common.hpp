@@ -106,6 +106,13 @@ constexpr int DSORT_SB_LOG2 = 5, DSORT_SB = 1 << DSORT_SB_LOG2;
 #define GSR_DSORT_GROUPED_NB 1536
 #endif
 __host__ __device__ inline bool dsort_grouped(int P) { return radix_blocks(P, dsort_items(P)) <= GSR_DSORT_GROUPED_NB; }
+// the first pass grouped too (its counts from depth_keys_kernel, num_rendered published
+// by that launch's extra workgroup, the key base reduced in every downsweep block):
+// no digit-scan launch in the whole depth sort
+#ifndef GSR_DSORT_GROUP1
+#define GSR_DSORT_GROUP1 1
+#endif
+__host__ __device__ inline bool dsort_grouped1(int P) { return GSR_DSORT_GROUP1 && dsort_grouped(P); }
 __host__ __device__ inline int dsort_nsup(int P) {
     return dsort_grouped(P) ? (radix_blocks(P, dsort_items(P)) + DSORT_SB - 1) / DSORT_SB : 1;
 }
@@ -203,6 +210,7 @@ struct GeomLayout {
     size_t dsort_minmax;  // uint2 [radix_blocks(P, dsort_items(P))] candidate key range per first-pass block
     size_t dsort_ctrl;    // uint32 [16] DsortCtrlWord
     size_t dsort_sup;     // uint32 [3][dsort_nsup(P)][RADIX] passes 2-4: digit counts per group of DSORT_SB blocks
+    size_t dsort_sup0;    // uint32 [dsort_nsup(P)][RADIX] the same for pass 1 (depth_keys_kernel; zeroed by preprocess)
     size_t emit_sums;     // uint32 [emit_blocks(P)] instances before each emit block within its rank-gather block
     size_t emit_super;    // uint32 [rg_blocks(P)] instances per rank-gather block (RG_SUPER emit blocks)
     size_t rs_ahist;      // uint32 [gy][rsa_blocks(P)] row-span pass A: spans per (tile row, block) -> block offsets
@@ -240,6 +248,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.dsort_minmax = take((size_t)radix_blocks(P, dsort_items(P)) * 8);
     L.dsort_ctrl = take(CTRL_WORDS * 4);
     L.dsort_sup = take((size_t)3 * dsort_nsup(P) * RADIX * 4);
+    L.dsort_sup0 = take((size_t)dsort_nsup(P) * RADIX * 4);
     L.off[GSR_GEOM_DSORT_CTRL] = L.dsort_ctrl;
     L.emit_sums = take((size_t)emit_blocks(P) * 4 + 4);
     L.emit_super = take((size_t)rg_blocks(P) * 4 + 4);

@@ -13,19 +13,22 @@
 namespace gsr {
 
 constexpr int TOTAL_THREADS = 1024;
+// (THREADS: the workgroup's size — 1024 in the digit scan, 256 in depth_keys_kernel
+// when the first depth pass is grouped)
+template <int THREADS = TOTAL_THREADS>
 __device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t *ctrl, uint32_t *host_ctrl) {
-    __shared__ unsigned long long part[TOTAL_THREADS / 64];
-    __shared__ uint32_t perr[TOTAL_THREADS / 64];
+    __shared__ unsigned long long part[THREADS / 64];
+    __shared__ uint32_t perr[THREADS / 64];
     unsigned long long t = 0;
     uint32_t e = 0;
     // 8 loads in flight per thread (one at a time: 12 us for config E's 19.5k
     // workgroup records, on the host's critical path)
     constexpr int U = 8;
-    for (int i0 = threadIdx.x; i0 < n; i0 += TOTAL_THREADS * U) {
+    for (int i0 = threadIdx.x; i0 < n; i0 += THREADS * U) {
         uint4 v[U];
 #pragma unroll
         for (int j = 0; j < U; j++) {
-            const int i = i0 + j * TOTAL_THREADS;
+            const int i = i0 + j * THREADS;
             v[j] = i < n ? sums[i] : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
@@ -45,7 +48,7 @@ __device__ __forceinline__ void publish_total(const uint4 *sums, int n, uint32_t
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int k = 1; k < TOTAL_THREADS / 64; k++) {
+        for (int k = 1; k < THREADS / 64; k++) {
             t += part[k];
             e |= perr[k];
         }

@@ -36,6 +36,8 @@ struct PreArgs {
     uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, 0, 0, 0}
     int32_t *radii;
     uint32_t *order_cnt;
+    uint32_t *sup0;   // the grouped first depth pass's group counts (binning.hip), zeroed here, or NULL
+    int sup0_n;
     float *shjac;     // [9][P] the SH direction Jacobian, when a backward will follow (else NULL)
     uint32_t *ctrl;   // geom control words (CTRL_SHJAC)
 };
@@ -246,6 +248,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     // (stores are counted by vmcnt too: issued here, after the geometry, they do not
     // hold up its waits for the per-Gaussian loads)
     for (int t = idx; t < a.tiles; t += gridDim.x * PRE_THREADS) a.ranges[t] = make_uint2(0u, 0u);
+    for (int t = idx; t < a.sup0_n; t += gridDim.x * PRE_THREADS) a.sup0[t] = 0u;
     if (idx < 8 * ORDER_NBUCKET) a.order_cnt[idx] = 0u;  // the backward wave-order buckets (render_bwd.hip)
     if (idx == 0) {  // and the flag words (one block may be all there is)
         a.order_cnt[ORDER_FILED] = 0u;
@@ -399,6 +402,8 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, b
     a.radii = radii;
     a.order_cnt = at<uint32_t>(geom, L.order_cnt);
     a.ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
+    a.sup0 = dsort_grouped1(in.P) ? at<uint32_t>(geom, L.dsort_sup0) : nullptr;
+    a.sup0_n = dsort_grouped1(in.P) ? dsort_nsup(in.P) * RADIX : 0;
     a.shjac = (in.flags & GSR_FLAG_PREPARE_BACKWARD) && in.sh && !in.colors_precomp ? at<float>(geom, L.shjac) : nullptr;
     const int nb = pre_blocks(in.P);
     const bool split = in.sh_rest != nullptr;

@@ -17,7 +17,9 @@ d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 s = d["stages_ms"]
 e = d.get("config_E_render") or {}
 es = " E %.1f fps (%s)" % (e["value"], " ".join(f"{k[:5]}={v * 1e3:.0f}" for k, v in e["stages_ms"].items())) if e else ""
-print(f"{sys.argv[1]:>10} {d['value']:8.2f}  " + " ".join(f"{k[:8]}={v * 1e3:.0f}" for k, v in s.items() if v) + es)
+b = d.get("config_B") or {}
+bs = " B %.1f (%s; depth=%.1f)" % (b["value"], b.get("form"), b["stages_ms"]["depth_sort"] * 1e3) if b else ""
+print(f"{sys.argv[1]:>10} {d['value']:8.2f}  " + " ".join(f"{k[:8]}={v * 1e3:.0f}" for k, v in s.items() if v) + es + bs)
 PY
   done
 done
