@@ -837,6 +837,7 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
+        t_host = time.perf_counter() - t0
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         stages = _C.timing_read()
@@ -851,6 +852,7 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
     ms = 1e3 * dt / steps
     return {"value": round(steps / dt, 3), "unit": "train-iters/s", "ms_per_step": round(ms, 4), "steps": steps,
             "vs_plain_ms": round(ms / plain_ms, 4) if plain_ms else None, "fused_leaves": plan,
+            "host_ms_per_step": round(1e3 * t_host / steps, 4),
             "exchange_wait_ms": round(st["exchange_wait_ms"], 4), "sh_rebuild_ms": round(st["sh_rebuild_ms"], 4),
             "bytes_per_rank": st["bytes_per_rank"], "collective_backend": "RCCL (one rank, every collective forced)"}
 
