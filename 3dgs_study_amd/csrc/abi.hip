@@ -335,8 +335,10 @@ double gsr_host_wait_us(int reset) {
 
 int gsr_colour_mode(int mode) {
     if (mode == -2) return g_colour_mode.load();
-    if (mode != 0 && mode != 1) {
-        fail(GSR_ERR_ARGS, "colour mode %d: 1 (colour half on a side stream), 0 (fused) or -2 (query)", mode);
+    if (mode != 0 && mode != 1 && mode != 2) {
+        fail(GSR_ERR_ARGS,
+             "colour mode %d: 2 (colour half riding the depth sort), 1 (on a side stream), 0 (fused) or -2 (query)",
+             mode);
         return -3;
     }
     return g_colour_mode.exchange(mode);
@@ -386,8 +388,15 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
     SideStream *side = nullptr;
     if (colour_join && !dbg && g_colour_mode.load() == 1 && in->sh && !in->colors_precomp) side = side_stream();
     if (colour_join) *colour_join = nullptr;
+    // colour riding: the colour half runs as extra workgroups of the depth sort's
+    // downsweeps (binning.hip), in stream order — no second queue
+    ColourRide ride{};
+    const bool riding = !side && g_colour_mode.load() == 2 && colour_ride_plan(*in, geom, radii, &ride);
     if (int rc = step(timed(GSR_STAGE_PREPROCESS, s,
-                            [&] { return launch_preprocess(*in, geom, radii, carry, s, side ? PRE_PHASE_GEOM : PRE_PHASE_FUSED); }),
+                            [&] {
+                                return launch_preprocess(*in, geom, radii, carry, s,
+                                                         side || riding ? PRE_PHASE_GEOM : PRE_PHASE_FUSED);
+                            }),
                       "preprocess", dbg, s))
         return rc;
     if (side) {
@@ -405,7 +414,7 @@ static int queue_preprocess(const gsr_inputs *in, void *geom, int32_t *radii, in
     if (int rc = step(timed(GSR_STAGE_DEPTH_SORT, s,
                             [&] {
                                 return launch_depth_sort(in->P, in->W, in->H, in->means3D, in->viewmatrix, geom,
-                                                         passes, g_pinned, carry, s);
+                                                         passes, g_pinned, carry, s, riding ? &ride : nullptr);
                             }),
                       "depth sort", dbg, s))
         return rc;

@@ -43,6 +43,7 @@
 // carries the running count from round to round — no atomics anywhere.
 #pragma clang fp contract(off)
 
+#include "gsr_colour.hpp"
 #include "gsr_kernels.hpp"
 #include "gsr_math.hpp"
 #include "gsr_publish.hpp"
@@ -113,6 +114,9 @@ struct RadixPass {
     const uint4 *rin;
     const uint32_t *win;
     uint32_t *wout, *wout_final;
+    // the colour half of preprocess riding this downsweep (gsr_colour.hpp): its
+    // ride.nb workgroups follow the NB sorting ones in the grid; nb == 0 = none
+    ColourRide ride;
 };
 enum RadixRole { RX_PLAIN = 0, RX_DEPTH_FIRST, RX_DEPTH_THIRD, RX_DEPTH_FOURTH };
 enum RadixMode { RXM_KV = 0, RXM_PACK, RXM_UNPACK };
@@ -340,8 +344,22 @@ hipError_t launch_count_scan(uint32_t *hist, int NB, const uint32_t *nb_dev, uin
     return hipGetLastError();
 }
 
-template <int ITEMS, int MODE, bool CARRY = false>
+template <int ITEMS, int MODE, bool CARRY = false, bool RIDE = false>
 __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a) {
+    if constexpr (RIDE) {
+        // colour riders: the workgroups past the sorting ones.  The sort is bound by
+        // its launch and dependency latency and leaves most of the chip idle; the
+        // colour half streams the SH rows meanwhile, in the same launch (no second
+        // queue).  Whole workgroups return here, before any barrier.
+        if ((int)blockIdx.x >= a.NB) {
+            const int cb = a.ride.b0 + (int)blockIdx.x - a.NB;
+            if (a.ride.sh_rest)
+                colour_rows48<true>(a.ride, cb);
+            else
+                colour_rows48<false>(a.ride, cb);
+            return;
+        }
+    }
     constexpr int TILE_N = RX_THREADS * ITEMS, WAVE_N = TILE_N / RX_WAVES;
     constexpr int SEG = MODE == RXM_UNPACK ? RADIX + 1 : 1;
     __shared__ uint32_t cnt[RX_WAVES][RADIX];
@@ -586,10 +604,18 @@ static hipError_t radix_pass(const RadixPass &a, hipStream_t s, bool counted = f
     if (!a.sup)  // grouped depth passes: each downsweep block sums its own prefix
         hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(a.pub_sums ? RADIX + 2 : a.minmax ? RADIX + 1 : RADIX),
                            dim3(DSCAN_THREADS), 0, s, a);
-    if (MODE == RXM_KV && (a.wout || a.wout_final))
+    const bool carry = MODE == RXM_KV && (a.wout || a.wout_final);
+    if (MODE == RXM_KV && a.ride.nb > 0) {
+        const dim3 grid(a.NB + a.ride.nb);
+        if (carry)
+            hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, RXM_KV, true, true>), grid, dim3(RX_THREADS), 0, s, a);
+        else
+            hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, RXM_KV, false, true>), grid, dim3(RX_THREADS), 0, s, a);
+    } else if (carry) {
         hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, RXM_KV, true>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
-    else
+    } else {
         hipLaunchKernelGGL((radix_downsweep_kernel<ITEMS, MODE>), dim3(a.NB), dim3(RX_THREADS), 0, s, a);
+    }
     return hipGetLastError();
 }
 
@@ -999,6 +1025,12 @@ __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) 
 // key range needs it.  The order lands in GSR_GEOM_DEPTH_ORDER either way.
 // carry: the rect footprint's words travel with the ids (rank_gather_kernel and the
 // row-span pass A then read them in rank order: no random gather of the rects)
+// the colour riders spread over the first RIDE_PASSES depth passes (always launched)
+#ifndef GSR_RIDE_PASSES
+#define GSR_RIDE_PASSES 3
+#endif
+constexpr int RIDE_PASSES = GSR_RIDE_PASSES;
+static_assert(RIDE_PASSES >= 1 && RIDE_PASSES <= 3, "passes 1-3 always run");
 static RadixPass depth_pass(int P, int W, int H, void *geom, int p, bool carry) {
     const GeomLayout L = geom_layout(P, W, H);
     RadixPass a = {};
@@ -1047,7 +1079,8 @@ static RadixPass depth_pass(int P, int W, int H, void *geom, int p, bool carry) 
 
 template <int ITEMS>
 static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                                   int passes, uint32_t *host_ctrl, bool carry, hipStream_t s) {
+                                   int passes, uint32_t *host_ctrl, bool carry, const ColourRide *ride,
+                                   hipStream_t s) {
     const GeomLayout L = geom_layout(P, W, H);
     DepthKeyArgs k;
     k.means3D = means3D;
@@ -1075,6 +1108,11 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     // when three suffice
     for (int p = 0; p < passes; p++) {
         RadixPass a = depth_pass(P, W, H, geom, p, carry);
+        if (ride && ride->nb > 0 && p < RIDE_PASSES) {  // this pass's share of the colour blocks
+            a.ride = *ride;
+            a.ride.b0 = ride->b0 + (int)((int64_t)ride->nb * p / RIDE_PASSES);
+            a.ride.nb = ride->b0 + (int)((int64_t)ride->nb * (p + 1) / RIDE_PASSES) - a.ride.b0;
+        }
         if (p == 0) {  // the first digit scan (or, grouped, the first downsweep) publishes the pass count ...
             a.host_ctrl = host_ctrl;
             if (!g1) {  // ... and num_rendered (grouped: depth_keys_kernel's extra workgroup)
@@ -1091,11 +1129,11 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
 }
 
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             int passes, uint32_t *host_ctrl, bool carry, hipStream_t s) {
+                             int passes, uint32_t *host_ctrl, bool carry, hipStream_t s, const ColourRide *ride) {
     if (P <= 0) return hipSuccess;
     return dsort_items(P) == DSORT_ITEMS_BIG
-               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, carry, s)
-               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, carry, s);
+               ? depth_sort_items<DSORT_ITEMS_BIG>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, carry, ride, s)
+               : depth_sort_items<DSORT_ITEMS>(P, W, H, means3D, viewmatrix, geom, passes, host_ctrl, carry, ride, s);
 }
 
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, bool carry, hipStream_t s) {

@@ -178,6 +178,20 @@ enum DsortCtrlWord {
 // host queued only three depth passes, unless three sufficed: a four-pass sort's
 // rank order is not ready yet).  The host then re-runs what it must (gsr_forward).
 // ctrl == NULL: not speculative, the host-side count is exact.
+// The colour half of preprocess as riders on the depth sort (gsr_colour.hpp,
+// gsr_colour_mode 2): colour blocks [b0, b0 + nb) of PRE_THREADS Gaussians run as
+// extra workgroups of a depth-pass downsweep.  The degree-3 register path only (48
+// floats per SH row: one cat row 16-B aligned, or the two leaves); nb == 0 = none.
+struct ColourRide {
+    const float *sh, *sh_rest, *means3D, *campos;
+    const int32_t *radii;
+    float *shjac;      // [9][P], or NULL
+    float4 *splats;    // [P][3]: the colour words are written
+    uint8_t *clamped;
+    int P, D;
+    int b0, nb;
+};
+
 struct SpecGuard {
     const uint32_t *ctrl;   // geom control words (CTRL_NUM_RENDERED_LO / HI)
     const uint32_t *dctrl;  // the depth sort's control words (DCTRL_PASSES)

@@ -17,6 +17,9 @@ namespace gsr {
 enum PrePhase { PRE_PHASE_FUSED = 0, PRE_PHASE_GEOM = 1, PRE_PHASE_COLOUR = 2 };
 hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s,
                              int phase = PRE_PHASE_FUSED);
+// The colour half's arguments as depth-sort riders (gsr_colour.hpp): false when the
+// inputs do not take the degree-3 register path (the fused kernel then runs)
+bool colour_ride_plan(const gsr_inputs &in, void *geom, int32_t *radii, ColourRide *ride);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 
@@ -27,8 +30,11 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 // pass count and num_rendered (after preprocess, in stream order).
 // carry: the rect footprint's words travel with the ids (the row-span binning of the
 // rect footprint; gsr_spans.hpp rect_word)
+// ride: the colour half of preprocess as extra workgroups of the downsweeps
+// (colour_ride_plan; preprocess then ran PRE_PHASE_GEOM), or NULL
 hipError_t launch_depth_sort(int P, int W, int H, const float *means3D, const float *viewmatrix, void *geom,
-                             int passes, uint32_t *host_ctrl, bool carry, hipStream_t s);
+                             int passes, uint32_t *host_ctrl, bool carry, hipStream_t s,
+                             const ColourRide *ride = nullptr);
 hipError_t launch_depth_sort_fourth(int P, int W, int H, void *geom, bool carry, hipStream_t s);
 // rowspan: the row-span binning follows (pass A's row counts and their scan)
 hipError_t launch_rank_gather(int P, int W, int H, void *geom, bool require3, bool rowspan, bool carry,

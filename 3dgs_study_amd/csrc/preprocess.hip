@@ -11,6 +11,7 @@
 #pragma clang fp contract(off)
 
 #include "gsr_blend.hpp"
+#include "gsr_colour.hpp"
 #include "gsr_kernels.hpp"
 #include "gsr_math.hpp"
 #include "gsr_publish.hpp"
@@ -41,33 +42,6 @@ struct PreArgs {
     float *shjac;     // [9][P] the SH direction Jacobian, when a backward will follow (else NULL)
     uint32_t *ctrl;   // geom control words (CTRL_SHJAC)
 };
-
-// SH -> RGB for one Gaussian, per channel (forward.cu computeColorFromSH).
-__device__ inline float sh_channel(const float *sh, int c, int deg, float x, float y, float z) {
-#define SH(k) sh[3 * (k) + c]
-    float result = SH_C0 * SH(0);
-    if (deg > 0) {
-        result = ((result - (SH_C1 * y) * SH(1)) + (SH_C1 * z) * SH(2)) - (SH_C1 * x) * SH(3);
-        if (deg > 1) {
-            float xx = x * x, yy = y * y, zz = z * z;
-            float xy = x * y, yz = y * z, xz = x * z;
-            result = ((((result + (SH_C2_0 * xy) * SH(4)) + (SH_C2_1 * yz) * SH(5)) +
-                       (SH_C2_2 * ((2.0f * zz - xx) - yy)) * SH(6)) +
-                      (SH_C2_3 * xz) * SH(7)) +
-                     (SH_C2_4 * (xx - yy)) * SH(8);
-            if (deg > 2) {
-                result = ((((((result + ((SH_C3_0 * y) * (3.0f * xx - yy)) * SH(9)) + ((SH_C3_1 * xy) * z) * SH(10)) +
-                            ((SH_C3_2 * y) * ((4.0f * zz - xx) - yy)) * SH(11)) +
-                           ((SH_C3_3 * z) * ((2.0f * zz - 3.0f * xx) - 3.0f * yy)) * SH(12)) +
-                          ((SH_C3_4 * x) * ((4.0f * zz - xx) - yy)) * SH(13)) +
-                         ((SH_C3_5 * z) * (xx - yy)) * SH(14)) +
-                        ((SH_C3_6 * x) * (xx - 3.0f * yy)) * SH(15);
-            }
-        }
-    }
-#undef SH
-    return result + 0.5f;
-}
 
 // SPLIT: the SH rows come from GaussianModel's two leaves (gsr_inputs.sh_rest)
 // instead of their cat.  GEOM: everything but the colour (no SH rows read; the
@@ -306,6 +280,24 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     if (threadIdx.x == 0) a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), 0u, 0u, 0u);
 }
 
+// The colour half's inputs and outputs (gsr_colour.hpp), from the preprocess arguments.
+__host__ __device__ inline ColourRide colour_ride(const gsr_inputs &in, const PreArgs &a) {
+    ColourRide c{};
+    c.sh = in.sh;
+    c.sh_rest = in.sh_rest;
+    c.means3D = in.means3D;
+    c.campos = in.campos;
+    c.radii = a.radii;
+    c.shjac = a.shjac;
+    c.splats = a.splats;
+    c.clamped = a.clamped;
+    c.P = in.P;
+    c.D = in.D;
+    c.b0 = 0;
+    c.nb = 0;
+    return c;
+}
+
 // The colour half of preprocess for the Gaussians the geometry half kept (radii >
 // 0; launched after it on a side stream, beside the depth sort and the binning,
 // which are bound by their launches' latency and leave the CUs mostly idle):
@@ -314,15 +306,19 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
 // as the fused kernel's colour stage, so the same bits.
 template <int RWC, bool SPLIT>
 __global__ void __launch_bounds__(PRE_THREADS) preprocess_colour_kernel(PreArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
-    const gsr_inputs &in = a.in;
-    const int g0 = blockIdx.x * PRE_THREADS;
-    const int idx = g0 + threadIdx.x;
-    const int RW = RWC > 0 ? RWC : 3 * in.M;
-    const int n = min(PRE_THREADS, in.P - g0);
     constexpr bool DIRECT = RWC == 48;
-    const bool emit = idx < in.P && a.radii[idx] > 0;
-    if constexpr (!DIRECT) {  // the workgroup's rows through LDS (coalesced), every thread takes part
+    if constexpr (DIRECT) {  // each thread's own row in registers (gsr_colour.hpp)
+        colour_rows48<SPLIT>(colour_ride(a.in, a), (int)blockIdx.x);
+        return;
+    } else {
+        extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // [PRE_THREADS][3M + 1]
+        const gsr_inputs &in = a.in;
+        const int g0 = blockIdx.x * PRE_THREADS;
+        const int idx = g0 + threadIdx.x;
+        const int RW = RWC > 0 ? RWC : 3 * in.M;
+        const int n = min(PRE_THREADS, in.P - g0);
+        const bool emit = idx < in.P && a.radii[idx] > 0;
+        // the workgroup's rows through LDS (coalesced), every thread takes part
         if constexpr (SPLIT) {
             rows_to_lds_cols<PRE_THREADS>(in.sh, g0, n, 3, 0, RW + 1, sh_lds);
             if (RW > 3) rows_to_lds_cols<PRE_THREADS>(in.sh_rest, g0, n, RW - 3, 3, RW + 1, sh_lds);
@@ -330,43 +326,32 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_colour_kernel(PreArgs 
             rows_to_lds<PRE_THREADS, RWC>(in.sh, g0, n, RW, sh_lds);
         }
         __syncthreads();
-    }
-    if (!emit) return;
-    float4 rowv[DIRECT ? 12 : 1];
-    if constexpr (DIRECT && SPLIT) {
-        float r[48];
-        load_sh_row_split(in.sh, in.sh_rest, (size_t)idx, r);
+        if (!emit) return;
+        const f3 p = {in.means3D[3 * idx], in.means3D[3 * idx + 1], in.means3D[3 * idx + 2]};
+        const float dx = p.x - in.campos[0], dy = p.y - in.campos[1], dz = p.z - in.campos[2];
+        const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+        const float x = dx / len, y = dy / len, z = dz / len;
+        const float *sh = sh_lds + threadIdx.x * (RW + 1);
+        float rgb[3];
+        uint8_t clampbits = 0;
 #pragma unroll
-        for (int b = 0; b < 12; b++) rowv[b] = make_float4(r[4 * b], r[4 * b + 1], r[4 * b + 2], r[4 * b + 3]);
-    } else if constexpr (DIRECT) {
-        const float4 *r4 = reinterpret_cast<const float4 *>(in.sh + (size_t)idx * 48);
+        for (int c = 0; c < 3; c++) {
+            const float v = sh_channel(sh, c, in.D, x, y, z);
+            clampbits |= (v < 0) ? (uint8_t)(1u << c) : (uint8_t)0;
+            rgb[c] = fmaxf(v, 0.0f);
+        }
+        if (a.shjac) {
+            float J[9];
+            sh_dir_jacobian(sh, in.D, x, y, z, J);
 #pragma unroll
-        for (int b = 0; b < 12; b++) rowv[b] = r4[b];
+            for (int k = 0; k < 9; k++) a.shjac[(size_t)k * in.P + idx] = J[k];
+        }
+        // the record's colour words: floats 6, 7 ({cc, opacity, r, g}) and 8 ({b, ...})
+        float *rec = reinterpret_cast<float *>(a.splats + 3 * (size_t)idx);
+        *reinterpret_cast<float2 *>(rec + 6) = make_float2(rgb[0], rgb[1]);
+        rec[8] = rgb[2];
+        a.clamped[idx] = clampbits;
     }
-    const f3 p = {in.means3D[3 * idx], in.means3D[3 * idx + 1], in.means3D[3 * idx + 2]};
-    const float dx = p.x - in.campos[0], dy = p.y - in.campos[1], dz = p.z - in.campos[2];
-    const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
-    const float x = dx / len, y = dy / len, z = dz / len;
-    const float *sh = DIRECT ? reinterpret_cast<const float *>(rowv) : sh_lds + threadIdx.x * (RW + 1);
-    float rgb[3];
-    uint8_t clampbits = 0;
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-        const float v = sh_channel(sh, c, in.D, x, y, z);
-        clampbits |= (v < 0) ? (uint8_t)(1u << c) : (uint8_t)0;
-        rgb[c] = fmaxf(v, 0.0f);
-    }
-    if (a.shjac) {
-        float J[9];
-        sh_dir_jacobian(sh, in.D, x, y, z, J);
-#pragma unroll
-        for (int k = 0; k < 9; k++) a.shjac[(size_t)k * in.P + idx] = J[k];
-    }
-    // the record's colour words: floats 6, 7 ({cc, opacity, r, g}) and 8 ({b, ...})
-    float *rec = reinterpret_cast<float *>(a.splats + 3 * (size_t)idx);
-    *reinterpret_cast<float2 *>(rec + 6) = make_float2(rgb[0], rgb[1]);
-    rec[8] = rgb[2];
-    a.clamped[idx] = clampbits;
 }
 
 // auxiliary.h in_frustum via checkFrustum (markVisible).
@@ -379,8 +364,7 @@ __global__ void mark_visible_kernel(int P, const float *means3D, const float *vi
     present[idx] = !(pv.z <= 0.2f);
 }
 
-hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s,
-                             int phase) {
+static PreArgs pre_args(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords) {
     const GeomLayout L = geom_layout(in.P, in.W, in.H);
     const GridDims g = grid_dims(in.W, in.H);
     PreArgs a;
@@ -405,10 +389,28 @@ hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, b
     a.sup0 = dsort_grouped1(in.P) ? at<uint32_t>(geom, L.dsort_sup0) : nullptr;
     a.sup0_n = dsort_grouped1(in.P) ? dsort_nsup(in.P) * RADIX : 0;
     a.shjac = (in.flags & GSR_FLAG_PREPARE_BACKWARD) && in.sh && !in.colors_precomp ? at<float>(geom, L.shjac) : nullptr;
+    return a;
+}
+
+// the register prefetch of cat rows reads them as float4: 16-B aligned only
+static bool direct_rows(const gsr_inputs &in) {
+    return in.sh && !in.colors_precomp && 3 * in.M == 48 && (in.sh_rest != nullptr || ((uintptr_t)in.sh & 15u) == 0);
+}
+
+bool colour_ride_plan(const gsr_inputs &in, void *geom, int32_t *radii, ColourRide *ride) {
+    if (!direct_rows(in) || in.P <= 0) return false;
+    const PreArgs a = pre_args(in, geom, radii, false);
+    *ride = colour_ride(in, a);
+    ride->nb = pre_blocks(in.P);
+    return true;
+}
+
+hipError_t launch_preprocess(const gsr_inputs &in, void *geom, int32_t *radii, bool rwords, hipStream_t s,
+                             int phase) {
+    const PreArgs a = pre_args(in, geom, radii, rwords);
     const int nb = pre_blocks(in.P);
     const bool split = in.sh_rest != nullptr;
-    // the register prefetch of cat rows reads them as float4: 16-B aligned only
-    const bool direct = in.sh && !in.colors_precomp && 3 * in.M == 48 && (split || ((uintptr_t)in.sh & 15u) == 0);
+    const bool direct = direct_rows(in);
     const size_t lds = (in.sh && !in.colors_precomp && !direct) ? (size_t)PRE_THREADS * (3 * in.M + 1) * sizeof(float) : 0;
     // SH row width as a compile-time constant for the common degrees (cheap LDS
     // row indexing); any other width takes the run-time path

@@ -135,11 +135,25 @@ def set_colour_apart(on: bool) -> bool:
     """Preprocess's colour half on a side stream beside the binning (include/gsr.h
     gsr_colour_mode; opt-in, measured slower) or one fused kernel (the default).
     Returns the previous setting."""
-    return bool(load_library().gsr_colour_mode(1 if on else 0))
+    return load_library().gsr_colour_mode(1 if on else 0) == 1
 
 
 def get_colour_apart() -> bool:
-    return bool(load_library().gsr_colour_mode(-2))
+    return load_library().gsr_colour_mode(-2) == 1
+
+
+def set_colour_mode(mode: int) -> int:
+    """Where preprocess's colour half runs (include/gsr.h gsr_colour_mode): 0 in the
+    fused kernel, 1 on a side stream, 2 as extra workgroups of the depth sort's
+    downsweeps.  The same bits in every mode.  Returns the previous mode."""
+    prev = load_library().gsr_colour_mode(int(mode))
+    if prev < -1:
+        raise ValueError(load_library().gsr_last_error().decode())
+    return prev
+
+
+def get_colour_mode() -> int:
+    return load_library().gsr_colour_mode(-2)
 
 
 def get_split() -> int:

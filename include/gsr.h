@@ -419,9 +419,12 @@ int gsr_forward_status(int64_t capacity, int passes, int64_t *num_rendered);
  * its geometry half on the caller's stream and its colour half (SH -> RGB, the clamp
  * bits, the SH direction Jacobian) on a low-priority side stream forked after it,
  * beside the depth sort and the binning, joined before the blend; 0 (default) — one
- * fused preprocess kernel (the side queue measured slower: DESIGN.md §9).  SH inputs
- * only, never in debug mode or the two-call form.  The same bits either way.  -2
- * queries; returns the previous mode, or -3 for an invalid argument. */
+ * fused preprocess kernel (the side queue measured slower: DESIGN.md §9); 2 — the
+ * geometry half in line and the colour half as extra workgroups of the depth sort's
+ * first three downsweeps (one queue; degree-3 SH rows only, else the fused kernel;
+ * both forward forms, debug mode too).  Mode 1: SH inputs only, never in debug mode
+ * or the two-call form.  The same bits in every mode.  -2 queries; returns the
+ * previous mode, or -3 for an invalid argument. */
 int gsr_colour_mode(int mode);
 /* Microseconds the host has spent in the forward's one wait (the num_rendered
  * read-back) since the last reset, summed over threads; reset != 0 also zeroes it.

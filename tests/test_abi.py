@@ -367,11 +367,16 @@ def test_colour_mode_values():
     """gsr_colour_mode: set / query / reject (no GPU call)."""
     from diff_gaussian_rasterization import _C
 
-    prev = _C.get_colour_apart()
+    prev = _C.get_colour_mode()
     try:
-        assert _C.set_colour_apart(False) == prev
+        assert _C.set_colour_mode(0) == prev
         assert _C.get_colour_apart() is False
+        assert _C.set_colour_mode(2) == 0
+        assert _C.get_colour_mode() == 2 and _C.get_colour_apart() is False
+        assert _C.set_colour_apart(True) is False and _C.get_colour_mode() == 1
         assert _C.load_library().gsr_colour_mode(7) == -3
-        assert _C.get_colour_apart() is False
+        with pytest.raises(ValueError):
+            _C.set_colour_mode(3)
+        assert _C.get_colour_mode() == 1
     finally:
-        _C.set_colour_apart(prev)
+        _C.set_colour_mode(prev)
