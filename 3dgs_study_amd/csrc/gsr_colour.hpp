@@ -74,7 +74,7 @@ __device__ __forceinline__ void colour_rows48(const ColourRide &c, int blk) {
         float J[9];
         sh_dir_jacobian(sh, c.D, x, y, z, J);
 #pragma unroll
-        for (int k = 0; k < 9; k++) c.shjac[(size_t)k * c.P + idx] = J[k];
+        for (int k = 0; k < 9; k++) store_jac(c.shjac + (size_t)k * c.P + idx, J[k]);
     }
     float *rec = reinterpret_cast<float *>(c.splats + 3 * (size_t)idx);
     *reinterpret_cast<float2 *>(rec + 6) = make_float2(rgb[0], rgb[1]);

@@ -178,6 +178,43 @@ enum DsortCtrlWord {
 // host queued only three depth passes, unless three sufficed: a four-pass sort's
 // rank order is not ready yet).  The host then re-runs what it must (gsr_forward).
 // ctrl == NULL: not speculative, the host-side count is exact.
+// Streaming stores for outputs no kernel of the step reads again (the leaf
+// gradients preprocess_bwd writes last; read by the optimizer or the next step's
+// exchange, long after): non-temporal, so they leave the Infinity Cache instead of
+// sitting there dirty until the next step's preprocess evicts them while it streams
+// the parameters in (its reads then wait behind the write-backs: preprocess 84 →
+// 68 µs at config C with the dsh rows streamed).  GSR_NT_GRAD: 0 plain stores, 1
+// the dsh rest rows only, 2 every leaf gradient.
+#ifndef GSR_NT_GRAD
+#define GSR_NT_GRAD 2
+#endif
+#ifndef GSR_NT_JAC
+#define GSR_NT_JAC 1  // the forward's SH Jacobian planes streamed too (read back by preprocess_bwd only)
+#endif
+typedef float gsr_v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_jac(float *p, float v) {
+    if constexpr (GSR_NT_JAC)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+template <int LEVEL>
+__device__ __forceinline__ void store_stream(float *p, float v) {
+    if constexpr (GSR_NT_GRAD >= LEVEL)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+template <int LEVEL>
+__device__ __forceinline__ void store_stream(float4 *p, float4 v) {
+    if constexpr (GSR_NT_GRAD >= LEVEL) {
+        const gsr_v4f w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<gsr_v4f *>(p));
+    } else {
+        *p = v;
+    }
+}
+
 // The colour half of preprocess as riders on the depth sort (gsr_colour.hpp,
 // gsr_colour_mode 2): colour blocks [b0, b0 + nb) of PRE_THREADS Gaussians run as
 // extra workgroups of a depth-pass downsweep.  The degree-3 register path only (48

@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 float J[9];
                 sh_dir_jacobian(sh, in.D, x, y, z, J);
 #pragma unroll
-                for (int k = 0; k < 9; k++) a.shjac[(size_t)k * in.P + idx] = J[k];
+                for (int k = 0; k < 9; k++) store_jac(a.shjac + (size_t)k * in.P + idx, J[k]);
             }
         }
         a.depths[idx] = depth;
@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_colour_kernel(PreArgs 
             float J[9];
             sh_dir_jacobian(sh, in.D, x, y, z, J);
 #pragma unroll
-            for (int k = 0; k < 9; k++) a.shjac[(size_t)k * in.P + idx] = J[k];
+            for (int k = 0; k < 9; k++) store_jac(a.shjac + (size_t)k * in.P + idx, J[k]);
         }
         // the record's colour words: floats 6, 7 ({cc, opacity, r, g}) and 8 ({b, ...})
         float *rec = reinterpret_cast<float *>(a.splats + 3 * (size_t)idx);

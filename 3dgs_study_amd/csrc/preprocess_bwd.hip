@@ -146,7 +146,10 @@ __device__ __forceinline__ void leaf_sh_store_basis(const gsr_leaf_grads &L, int
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             float *p = L.dsh_dc + 3 * (size_t)idx + c;
-            *p = add ? *p + coef(0, c) : coef(0, c);
+            if (add)
+                *p += coef(0, c);
+            else
+                store_stream<2>(p, coef(0, c));
         }
     const int lane = threadIdx.x & 63;
     float *buf = stage[threadIdx.x >> 6];
@@ -173,7 +176,7 @@ __device__ __forceinline__ void leaf_sh_store_basis(const gsr_leaf_grads &L, int
                         const float4 o = *d;
                         *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
                     } else {
-                        *d = v;
+                        store_stream<1>(d, v);
                     }
                 } else {
                     const float vv[4] = {v.x, v.y, v.z, v.w};
@@ -340,9 +343,9 @@ __global__ void __launch_bounds__(PB_THREADS) preprocess_bwd_kernel(PreBwdArgs a
             dm[1] += dmean.y;
             dm[2] += dmean.z;
         } else {
-            dm[0] = dmean.x;
-            dm[1] = dmean.y;
-            dm[2] = dmean.z;
+            store_stream<2>(dm, dmean.x);
+            store_stream<2>(dm + 1, dmean.y);
+            store_stream<2>(dm + 2, dmean.z);
         }
     }
     if constexpr (LB) {
@@ -418,7 +421,12 @@ __device__ __forceinline__ void write_activation_grads(const PreBwdArgs &a, int 
     const BwdOutputs &o = a.o;
     const gsr_leaf_grads &L = o.leaf;
     const int act = a.in.activations;
-    auto put = [&](float *p, size_t i, float v, int bit) { p[i] = (L.accumulate & bit) ? p[i] + v : v; };
+    auto put = [&](float *p, size_t i, float v, int bit) {
+        if (L.accumulate & bit)
+            p[i] += v;
+        else
+            store_stream<2>(p + i, v);
+    };
     if (L.dopacity || (act & GSR_ACT_OPACITY)) {
         const float sg = opac;  // sigmoid(x): in.opacities[idx], or the activation of the logit
         const float v = (dop * (1.0f - sg)) * sg;  // sigmoid_backward: grad * (1 - y) * y
@@ -532,9 +540,9 @@ __device__ ShStage preprocess_bwd_geom(const PreBwdArgs &a, int idx, const f3 me
     const float kx = cc * det_inv, ky = -cb * det_inv, kz = ca * det_inv;
     const float g2x = -0.5f * (kx * sx + ky * sy) * (float)in.W;
     const float g2y = -0.5f * (ky * sx + kz * sy) * (float)in.H;
-    o.dmeans2D[3 * (size_t)idx + 0] = g2x;
-    o.dmeans2D[3 * (size_t)idx + 1] = g2y;
-    o.dmeans2D[3 * (size_t)idx + 2] = 0.f;
+    store_stream<2>(o.dmeans2D + 3 * (size_t)idx + 0, g2x);
+    store_stream<2>(o.dmeans2D + 3 * (size_t)idx + 1, g2y);
+    store_stream<2>(o.dmeans2D + 3 * (size_t)idx + 2, 0.f);
     float dL_da = 0, dL_db = 0, dL_dc = 0;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
     float dc3[6] = {0, 0, 0, 0, 0, 0};
