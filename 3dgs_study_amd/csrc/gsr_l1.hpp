@@ -12,6 +12,7 @@
 namespace gsr {
 
 constexpr int L1_THREADS = 256, L1_BLOCKS = 1024;
+typedef float l1_v4f __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline int l1_blocks(size_t n) {
     const size_t want = (n / 4 + L1_THREADS - 1) / L1_THREADS;
@@ -34,7 +35,11 @@ __device__ __forceinline__ void l1_block_partial(const float *x, const float *y,
     const float4 *x4 = reinterpret_cast<const float4 *>(x), *y4 = reinterpret_cast<const float4 *>(y);
     float acc = 0.f;
     for (size_t i = (size_t)blk * L1_THREADS + threadIdx.x; i < n4; i += stride) {
-        const float4 a = x4[i], b = y4[i];
+        // both images are read once here: non-temporal, so they do not displace what
+        // the render backward is about to gather (render_bwd -1.5 to -2 us at config C)
+        const l1_v4f av = __builtin_nontemporal_load(reinterpret_cast<const l1_v4f *>(x4 + i));
+        const l1_v4f bv = __builtin_nontemporal_load(reinterpret_cast<const l1_v4f *>(y4 + i));
+        const float4 a = make_float4(av.x, av.y, av.z, av.w), b = make_float4(bv.x, bv.y, bv.z, bv.w);
         acc += (fabsf(a.x - b.x) + fabsf(a.y - b.y)) + (fabsf(a.z - b.z) + fabsf(a.w - b.w));
         if (sign) {
             const uint32_t s = (uint32_t)(uint8_t)(int8_t)l1_sign_of(a.x - b.x) |
