@@ -260,8 +260,10 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
                 for (int k = 0; k < 9; k++) store_jac(a.shjac + (size_t)k * in.P + idx, J[k]);
             }
         }
-        a.depths[idx] = depth;
-        a.means2D[idx] = make_float2(px, py);
+        // (depths and means2D: introspection only — no kernel of the step reads them)
+        store_stream<1>(a.depths + idx, depth);
+        store_stream<1>(&a.means2D[idx].x, px);
+        store_stream<1>(&a.means2D[idx].y, py);
         // conic and bound stored times -1/2 (exact): the blend kernels then
         // evaluate upstream's power -0.5 * d^T conic d as d^T conic' d, bit for
         // bit, one multiply fewer per (pixel, Gaussian).  The record also carries
