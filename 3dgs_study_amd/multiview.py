@@ -49,6 +49,7 @@ returns, so the exchange follows the model instead of going stale.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Callable, Sequence, Union
 
@@ -564,6 +565,8 @@ class GradAllReduce:
         return slot[0]
 
     def _side(self, device) -> "torch.cuda.Stream":
+        if not self.exchange_stream:  # everything in line on the compute stream
+            return torch.cuda.current_stream(device)
         st = getattr(self, "_side_stream", None)
         if st is None or st.device != device:
             st = self._side_stream = torch.cuda.Stream(device=device)
@@ -587,6 +590,10 @@ class GradAllReduce:
     # the SH rebuild on the exchange stream right behind the gather (beside
     # preprocess_bwd), or (False) on the compute stream after preprocess_bwd
     rebuild_on_side = True
+    # the colour kernel, the record gather and the SH rebuild on a stream of their
+    # own beside the per-Gaussian backward (True), or in line on the compute stream
+    # (False: no second hardware queue, no cross-queue waits)
+    exchange_stream = os.environ.get("GSR_EXCHANGE_STREAM", "1") != "0"
 
     def push(self, rec: torch.Tensor, campos: torch.Tensor, sh_degree: int, ready=None, write=None) -> None:
         """Exchange a view's record (from ``record``): the all-gather starts behind
