@@ -180,7 +180,10 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int k) { return (uint32_
 // XCD_STRIP consecutive tiles (which share most of their Gaussians) are given
 // to one XCD's L2, and the strips are dealt round-robin over the XCDs so that
 // every XCD gets an even share of the heavy centre of the image.
-constexpr int XCD_STRIP = 4;
+#ifndef GSR_XCD_STRIP
+#define GSR_XCD_STRIP 4
+#endif
+constexpr int XCD_STRIP = GSR_XCD_STRIP;
 template <int STRIP = XCD_STRIP>
 __device__ __forceinline__ int xcd_tile(int b, int tiles) {
     const int x = b & 7, j = b >> 3;

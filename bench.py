@@ -834,10 +834,12 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
         torch.cuda.synchronize()
         ar.reset_stats()
         _C.timing_enable(list(EXCHANGE_STAGES))
+        _C.host_wait_ms(reset=True)
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         t_host = time.perf_counter() - t0
+        t_wait = _C.host_wait_ms() * 1e-3
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         stages = _C.timing_read()
@@ -852,7 +854,10 @@ def exchange_one_rank_rates(cam, P: int, deg: int, target, bg, steps: int, warmu
     ms = 1e3 * dt / steps
     return {"value": round(steps / dt, 3), "unit": "train-iters/s", "ms_per_step": round(ms, 4), "steps": steps,
             "vs_plain_ms": round(ms / plain_ms, 4) if plain_ms else None, "fused_leaves": plan,
-            "host_ms_per_step": round(1e3 * t_host / steps, 4),
+            # the host's time in the forward's one wait: > 0 means the device, not the
+            # host's Python / autograd / exchange work, sets the step
+            "host_wait_ms_per_step": round(1e3 * t_wait / steps, 4),
+            "host_busy_ms_per_step": round(1e3 * (t_host - t_wait) / steps, 4),
             "exchange_wait_ms": round(st["exchange_wait_ms"], 4), "sh_rebuild_ms": round(st["sh_rebuild_ms"], 4),
             "bytes_per_rank": st["bytes_per_rank"], "collective_backend": "RCCL (one rank, every collective forced)"}
 
