@@ -184,9 +184,12 @@ enum DsortCtrlWord {
 // sitting there dirty until the next step's preprocess evicts them while it streams
 // the parameters in (its reads then wait behind the write-backs: preprocess 84 →
 // 68 µs at config C with the dsh rows streamed).  GSR_NT_GRAD: 0 plain stores, 1
-// the dsh rest rows only, 2 every leaf gradient.
+// (default) the dsh rest rows only — whole 128-B lines from the LDS-staged float4
+// stores; 2 also the 4-16 B per-Gaussian leaf rows (written by scalar stores that
+// cover a line only together: streamed, they cost preprocess_bwd 7 us for 2 us of
+// preprocess at config C).
 #ifndef GSR_NT_GRAD
-#define GSR_NT_GRAD 2
+#define GSR_NT_GRAD 1
 #endif
 #ifndef GSR_NT_JAC
 #define GSR_NT_JAC 1  // the forward's SH Jacobian planes streamed too (read back by preprocess_bwd only)
