@@ -12,6 +12,10 @@
 
 #include "gsr.h"
 
+#ifndef GSR_ACCUM_STRIDE
+#define GSR_ACCUM_STRIDE 16  // floats per Gaussian in the backward accumulator
+#endif
+
 namespace gsr {
 
 constexpr int TILE_X = 16;  // BLOCK_X (upstream config.h)
@@ -310,7 +314,7 @@ __host__ __device__ inline GeomLayout geom_layout(int P, int W, int H) {
     L.rs_atot = take((size_t)RADIX * 4);
     L.rs_words = L.rects_ranked;
     L.order_cnt = take((8 * 32 + 2) * 4);
-    L.accum = take((size_t)(P > 0 ? P : 1) * 16 * 4);
+    L.accum = take((size_t)(P > 0 ? P : 1) * GSR_ACCUM_STRIDE * 4);
     L.shjac = take((size_t)9 * (P > 0 ? P : 1) * 4);
     L.bytes = o;
     return L;
@@ -451,7 +455,7 @@ __host__ __device__ inline ImgLayout img_layout(int W, int H) {
     return L;
 }
 
-constexpr int ACCUM_STRIDE = 16;  // floats per Gaussian in the backward accumulator (64 B row)
+constexpr int ACCUM_STRIDE = GSR_ACCUM_STRIDE;  // floats per Gaussian in the backward accumulator (64 B row)
 // flag words after the 8 x 32 wave-order counts in GeomLayout::order_cnt
 enum OrderFlag {
     ORDER_FILED = 8 * 32,  // the quadrants are filed in img.qlist (by the forward's prepare or a backward)
