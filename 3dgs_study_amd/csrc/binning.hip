@@ -114,6 +114,9 @@ struct RadixPass {
     const uint4 *rin;
     const uint32_t *win;
     uint32_t *wout, *wout_final;
+    // grouped first pass whose key base depth_keys_kernel's publishing workgroup
+    // already wrote (from preprocess's per-workgroup key ranges): no block reduces it
+    int base_published;
     // the colour half of preprocess riding this downsweep (gsr_colour.hpp): its
     // ride.nb workgroups follow the NB sorting ones in the grid; nb == 0 = none
     ColourRide ride;
@@ -137,13 +140,7 @@ __device__ __forceinline__ bool pass_skipped(const RadixPass &a) {
     return a.role == RX_DEPTH_FOURTH && a.ctrl[DCTRL_PASSES] == 3;
 }
 
-// Which candidate key range decides the depth sort: base = the smallest key with
-// its low byte cleared, three passes when every candidate lies within 2^24 of it.
-__device__ __forceinline__ uint2 dsort_base_passes(uint32_t kmin, uint32_t kmax) {
-    const bool any = kmin <= kmax;
-    const uint32_t base = any ? (kmin & ~0xffu) : 0u;
-    return make_uint2(base, any && kmax - base > 0xffffffu ? 4u : 3u);
-}
+// (dsort_base_passes: gsr_publish.hpp)
 __device__ __forceinline__ uint32_t key_rel(uint32_t k, uint32_t base, uint32_t passes) {
     const uint32_t d = k - base;
     return passes == 3 && d > 0xffffffu ? (0xffff00u | (d & 0xffu)) : d;
@@ -376,7 +373,7 @@ __global__ void __launch_bounds__(RX_THREADS) radix_downsweep_kernel(RadixPass a
     // range: every block reduces the per-block ranges itself (the same operations,
     // so the same base and pass count everywhere), and block 0 publishes them
     uint2 bp = make_uint2(0u, 0u);
-    const bool local_base = MODE == RXM_KV && a.role == RX_DEPTH_FIRST && a.sup != nullptr;
+    const bool local_base = MODE == RXM_KV && a.role == RX_DEPTH_FIRST && a.sup != nullptr && !a.base_published;
     if (local_base) {
         uint32_t kmin = 0xffffffffu, kmax = 0u;
         for (int i = threadIdx.x; i < a.NB; i += RX_THREADS) {
@@ -949,6 +946,7 @@ struct DepthKeyArgs {
     const uint4 *pub_sums;
     int pub_n;
     uint32_t *pub_ctrl, *pub_host;
+    uint32_t *pub_dctrl;  // ... and the depth sort's key base and pass count (GeomLayout::dsort_ctrl), or NULL
 };
 template <int ITEMS>
 __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) {
@@ -958,7 +956,7 @@ __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) 
     if (a.zero)  // (every workgroup of the grid its slice, the publishing one included)
         for (int i = blockIdx.x * RX_THREADS + threadIdx.x; i < a.zero_n; i += gridDim.x * RX_THREADS) a.zero[i] = 0u;
     if (a.sup0 && (int)blockIdx.x == a.NB) {  // the grouped form's extra workgroup
-        publish_total<RX_THREADS>(a.pub_sums, a.pub_n, a.pub_ctrl, a.pub_host);
+        publish_total<RX_THREADS>(a.pub_sums, a.pub_n, a.pub_ctrl, a.pub_host, a.pub_dctrl);
         return;
     }
     const int w = threadIdx.x >> 6;
@@ -1025,6 +1023,9 @@ __global__ void __launch_bounds__(RX_THREADS) depth_keys_kernel(DepthKeyArgs a) 
 // key range needs it.  The order lands in GSR_GEOM_DEPTH_ORDER either way.
 // carry: the rect footprint's words travel with the ids (rank_gather_kernel and the
 // row-span pass A then read them in rank order: no random gather of the rects)
+#ifndef GSR_PUBLISH_BASE
+#define GSR_PUBLISH_BASE 1
+#endif
 // the colour riders spread over the first RIDE_PASSES depth passes (always launched)
 #ifndef GSR_RIDE_PASSES
 #define GSR_RIDE_PASSES 3
@@ -1100,6 +1101,9 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
     k.pub_n = pre_blocks(P);
     k.pub_ctrl = at<uint32_t>(geom, L.off[GSR_GEOM_CTRL]);
     k.pub_host = host_ctrl;
+    // the key base from preprocess's per-workgroup candidate ranges (GSR_PUBLISH_BASE)
+    const bool pb = g1 && GSR_PUBLISH_BASE;
+    k.pub_dctrl = pb ? at<uint32_t>(geom, L.dsort_ctrl) : nullptr;
     hipLaunchKernelGGL(depth_keys_kernel<ITEMS>, dim3(k.NB + (g1 ? 1 : 0)), dim3(RX_THREADS), 0, s, k);
     // passes 3: the host reads the published pass count after its sync and launches
     // the fourth (launch_depth_sort_fourth) when the keys need it — three
@@ -1115,6 +1119,7 @@ static hipError_t depth_sort_items(int P, int W, int H, const float *means3D, co
         }
         if (p == 0) {  // the first digit scan (or, grouped, the first downsweep) publishes the pass count ...
             a.host_ctrl = host_ctrl;
+            a.base_published = pb ? 1 : 0;
             if (!g1) {  // ... and num_rendered (grouped: depth_keys_kernel's extra workgroup)
                 a.pub_sums = at<const uint4>(geom, L.block_sums);
                 a.pub_n = pre_blocks(P);

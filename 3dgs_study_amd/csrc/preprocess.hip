@@ -34,7 +34,7 @@ struct PreArgs {
     uint32_t *rwords;  // instead (the row-span binning of the rect footprint): the rect as one word (gsr_spans.hpp)
     uint2 *ranges;           // [T] zeroed here (empty tiles keep (0, 0); binning.hip fills the rest)
     int tiles;
-    uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, 0, 0, 0}
+    uint4 *block_sums;       // [pre_blocks(P)] {instances | prefiltered error << 31, smallest, largest candidate depth key, 0}
     int32_t *radii;
     uint32_t *order_cnt;
     uint32_t *sup0;   // the grouped first depth pass's group counts (binning.hip), zeroed here, or NULL
@@ -111,6 +111,10 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     }
     uint32_t touched = 0;
     bool perr = false;
+    // the depth sort's candidate key range (gsr_publish.hpp): depth_keys_kernel keys
+    // a Gaussian in front of the near plane by its view depth's bits — the same
+    // xform_point4x3 as here, so the same bits
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
     // what the colour stage (after the barrier) needs
     bool emit = false;
     float px = 0.f, py = 0.f, conic_x = 0.f, conic_y = 0.f, conic_z = 0.f, qmax = 0.f, depth = 0.f;
@@ -121,6 +125,7 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
         const float p_w = 1.0f / (p_hom.w + 0.0000001f);
         const f3 p_proj = {p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w};
         const f3 p_view = xform_point4x3(p, V);
+        if (p_view.z > 0.2f) kmin = kmax = __float_as_uint(p_view.z);
         bool ok = true;
         if (p_view.z <= 0.2f) {
             ok = false;
@@ -279,7 +284,24 @@ __global__ void __launch_bounds__(PRE_THREADS) preprocess_fwd_kernel(PreArgs a) 
     // workgroup stores its sum (bit 31 flags a prefiltered violation)
     const uint32_t tot = block_sum<PRE_THREADS>(touched, wsum);
     const int berr = __syncthreads_or(perr);
-    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), 0u, 0u, 0u);
+    __shared__ uint32_t wmin[PRE_THREADS / 64], wmax[PRE_THREADS / 64];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wmin[threadIdx.x >> 6] = kmin;
+        wmax[threadIdx.x >> 6] = kmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < PRE_THREADS / 64; k++) {
+            kmin = min(kmin, wmin[k]);
+            kmax = max(kmax, wmax[k]);
+        }
+        a.block_sums[blockIdx.x] = make_uint4(tot | (berr ? 0x80000000u : 0u), kmin, kmax, 0u);
+    }
 }
 
 // The colour half's inputs and outputs (gsr_colour.hpp), from the preprocess arguments.
