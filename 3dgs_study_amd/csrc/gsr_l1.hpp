@@ -11,7 +11,11 @@
 
 namespace gsr {
 
-constexpr int L1_THREADS = 256, L1_BLOCKS = 1024;
+#ifndef GSR_L1_BLOCKS
+#define GSR_L1_BLOCKS 1024  // at most 1024: the finish emulates a 1024-thread reduction
+#endif
+constexpr int L1_THREADS = 256, L1_BLOCKS = GSR_L1_BLOCKS;
+static_assert(L1_BLOCKS <= 1024, "the finish reads at most 1024 partials");
 typedef float l1_v4f __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline int l1_blocks(size_t n) {
